@@ -1,0 +1,137 @@
+"""Headline benchmark: Mamba-2 280M DDP training throughput (tokens/s, whole job).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+         --master-port P bench.py --gpus N --steps K --warmup W
+
+Config = BASELINE.json's headline: Mamba-2 280M (d_model 768, 64 layers, vocab 50304), seq 1024,
+micro-batch 32, global batch 524,288 tokens (= 512 sequences; grad-accum 16/N), bf16 autocast,
+fused AdamW, grad clip 1.0, DDP over RCCL.  Synthetic tokens, random init (no dataset/weights
+on the box).  A "step" is one full optimizer step (all micro-batches + all-reduce + clip + AdamW).
+W untimed warmup steps, then exactly K steps between barrier+synchronize pairs; the MAX elapsed
+over ranks is reported; rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+BASELINE_TOK_S = 238000.0  # BASELINE.md derived 8xA100 node throughput (no published tok/s)
+METRIC = "tokens/sec (whole node) Mamba-2 280M DDP at 1/2/4/8 MI355X; HellaSwag acc"
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--model", default="mamba2-280m")
+    p.add_argument("--B", type=int, default=32)
+    p.add_argument("--T", type=int, default=1024)
+    p.add_argument("--global-batch-tokens", type=int, default=524288)
+    p.add_argument("--bucket-cap-mb", type=float, default=100.0)
+    p.add_argument("--grad-comm-dtype", default="fp32")
+    p.add_argument("--reference-ops", action="store_true", help="A/B: run the PyTorch reference ops")
+    p.add_argument("--no-fused-ce", action="store_true")
+    p.add_argument("--profile-steps", type=int, default=0, help="torch.profiler trace of N extra steps")
+    a = p.parse_args()
+    if a.reference_ops:
+        os.environ["MAMBA_AMD_FORCE_REFERENCE"] = "1"
+
+    from mamba_distributed_amd import LMHeadModel, preset
+    from mamba_distributed_amd.data.loader import SyntheticTokens
+    from mamba_distributed_amd.parallel import ddp as ddp_mod
+    from mamba_distributed_amd.parallel.dist import all_reduce_avg, all_reduce_max, barrier, destroy, init_distributed
+
+    info = init_distributed("auto")
+    world = info.world_size
+    dev = info.device
+    assert a.global_batch_tokens % (a.B * a.T * world) == 0
+    accum = a.global_batch_tokens // (a.B * a.T * world)
+    torch.manual_seed(1337)
+    cfg = preset(a.model)
+    model = LMHeadModel(cfg, device=dev)
+    dmodel = ddp_mod.wrap_ddp(model, info, a.bucket_cap_mb, a.grad_comm_dtype)
+    opt = model.configure_optimizers(0.1, 6e-4, "cuda" if dev.startswith("cuda") else "cpu", False)
+    loader = SyntheticTokens(a.B, a.T, cfg.vocab_size, info.rank, world, device=dev)
+    fused = not a.no_fused_ce
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        loss_acc = torch.zeros((), device=dev)
+        for micro in range(accum):
+            x, y = loader.next_batch()
+            ddp_mod.set_grad_sync(dmodel, micro == accum - 1)
+            with torch.autocast(device_type="cuda", dtype=torch.bfloat16):
+                _, loss = dmodel(x, y, return_logits=not fused)
+            loss = loss / accum
+            loss_acc += loss.detach().float()
+            loss.backward()
+        all_reduce_avg(loss_acc)
+        torch.nn.utils.clip_grad_norm_(dmodel.parameters(), 1.0)
+        opt.step()
+        return loss_acc
+
+    for _ in range(a.warmup):
+        step()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        last = step()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = torch.tensor(time.perf_counter() - t0, device=dev, dtype=torch.float64)
+    all_reduce_max(elapsed)
+    elapsed = float(elapsed.item())
+    loss_v = float(last.item())
+    if a.profile_steps and info.master:
+        from torch.profiler import ProfilerActivity, profile
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+            for _ in range(a.profile_steps):
+                step()
+            torch.cuda.synchronize()
+        os.makedirs("gpurun_out", exist_ok=True)
+        with open("gpurun_out/torch_profile.txt", "w") as f:
+            f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
+    tokens = a.global_batch_tokens * a.steps
+    value = tokens / elapsed
+    if info.master:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1000 * elapsed / a.steps, 2),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": round(value / BASELINE_TOK_S, 3),
+            "dtype": "bf16",
+            "data": "synthetic (uniform random tokens, random-init weights)",
+            "config": {
+                "model": f"{a.model} (d_model={cfg.d_model}, n_layer={cfg.n_layer}, vocab={cfg.vocab_size}, "
+                         f"layer={cfg.layer_type})",
+                "global_batch": a.global_batch_tokens // a.T,
+                "global_batch_tokens": a.global_batch_tokens,
+                "micro_batch": a.B,
+                "grad_accum": accum,
+                "seq_len": a.T,
+                "parallelism": f"dp{world}",
+                "ops": "pytorch-reference" if a.reference_ops else "native-hip",
+                "final_loss": round(loss_v, 4),
+            },
+        }
+        print(json.dumps(out), flush=True)
+    destroy()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,603 @@
+// PyTorch operator registrations for the gfx950 kernels: torch.ops.mamba_amd.*
+//
+// Every op: validates device / dtype / shape / stride assumptions of its kernel with TORCH_CHECK
+// (a kernel is never launched on operands whose layout it does not handle), allocates outputs
+// with the caching allocator, launches on the current torch HIP stream, and checks the launch.
+#include <ATen/ATen.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <torch/library.h>
+
+#include "kernels/launchers.h"
+#include "kernels/selective_scan.h"
+#include "kernels/ssd.h"
+
+using at::Tensor;
+using c10::optional;
+
+namespace {
+
+hipStream_t cur_stream() { return at::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+
+int dcode(at::ScalarType t) {
+  switch (t) {
+    case at::kFloat: return mamba_amd::kF32;
+    case at::kBFloat16: return mamba_amd::kBF16;
+    default: TORCH_CHECK(false, "mamba_amd: unsupported dtype ", t);
+  }
+  return -1;
+}
+
+#define HIPCHK(e)                                                                              \
+  do {                                                                                         \
+    hipError_t _e = (e);                                                                       \
+    TORCH_CHECK(_e == hipSuccess, "mamba_amd HIP launch failed: ", hipGetErrorString(_e));     \
+  } while (0)
+
+void check_cuda(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "mamba_amd: ", name, " must be a GPU tensor");
+}
+void check_same_device(const Tensor& a, const Tensor& b) {
+  TORCH_CHECK(a.device() == b.device(), "mamba_amd: tensors on different devices");
+}
+Tensor f32c(const Tensor& t) { return t.to(at::kFloat).contiguous(); }
+Tensor f32c_opt(const optional<Tensor>& t) { return t.has_value() && t->defined() ? f32c(*t) : Tensor(); }
+const float* fptr(const Tensor& t) { return t.defined() ? t.data_ptr<float>() : nullptr; }
+
+// ---------------------------------------------------------------------------------------------
+// norms
+std::tuple<Tensor, Tensor, Tensor> add_rmsnorm_fwd(Tensor x, optional<Tensor> residual, Tensor weight, double eps,
+                                                   at::ScalarType out_dtype, at::ScalarType res_dtype) {
+  check_cuda(x, "x");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be (M, D) with unit column stride");
+  const int64_t M = x.size(0), D = x.size(1);
+  TORCH_CHECK(D % 4 == 0 && D <= 20 * 256 && x.stride(0) % 4 == 0, "D must be a multiple of 4 and <= 5120");
+  Tensor res;
+  if (residual.has_value() && residual->defined()) {
+    res = *residual;
+    TORCH_CHECK(res.dim() == 2 && res.size(0) == M && res.size(1) == D && res.stride(1) == 1 && res.stride(0) % 4 == 0,
+                "residual shape/stride mismatch");
+    check_same_device(x, res);
+  }
+  Tensor w = f32c(weight);
+  TORCH_CHECK(w.numel() == D, "weight size mismatch");
+  auto y = at::empty({M, D}, x.options().dtype(out_dtype));
+  auto ro = at::empty({M, D}, x.options().dtype(res_dtype));
+  auto rstd = at::empty({M}, x.options().dtype(at::kFloat));
+  HIPCHK(mamba_amd::launch_add_rmsnorm_fwd(x.data_ptr(), dcode(x.scalar_type()), x.stride(0),
+                                           res.defined() ? res.data_ptr() : nullptr,
+                                           res.defined() ? dcode(res.scalar_type()) : 0, res.defined() ? res.stride(0) : 0,
+                                           w.data_ptr<float>(), y.data_ptr(), dcode(out_dtype), ro.data_ptr(),
+                                           dcode(res_dtype), rstd.data_ptr<float>(), M, (int)D, (float)eps, cur_stream()));
+  return {y, ro, rstd};
+}
+
+std::tuple<Tensor, Tensor, Tensor> add_rmsnorm_bwd(Tensor dy, optional<Tensor> dres_out, Tensor res_out, Tensor weight,
+                                                   Tensor rstd, at::ScalarType dx_dtype, at::ScalarType dres_dtype,
+                                                   bool write_dres) {
+  check_cuda(dy, "dy");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
+  dy = dy.contiguous();
+  res_out = res_out.contiguous();
+  const int64_t M = res_out.size(0), D = res_out.size(1);
+  TORCH_CHECK(dy.size(0) == M && dy.size(1) == D, "dy shape mismatch");
+  Tensor dro;
+  if (dres_out.has_value() && dres_out->defined()) {
+    dro = dres_out->contiguous();
+    TORCH_CHECK(dro.size(0) == M && dro.size(1) == D, "dres_out shape mismatch");
+  }
+  Tensor w = f32c(weight);
+  auto dx = at::empty({M, D}, dy.options().dtype(dx_dtype));
+  Tensor dres = write_dres ? at::empty({M, D}, dy.options().dtype(dres_dtype)) : at::empty({0}, dy.options());
+  const int rows = mamba_amd::add_rmsnorm_bwd_partial_rows(M);
+  auto part = at::empty({rows, D}, dy.options().dtype(at::kFloat));
+  auto dw = at::empty({D}, dy.options().dtype(at::kFloat));
+  HIPCHK(mamba_amd::launch_add_rmsnorm_bwd(dy.data_ptr(), dcode(dy.scalar_type()), dro.defined() ? dro.data_ptr() : nullptr,
+                                           dro.defined() ? dcode(dro.scalar_type()) : 0, res_out.data_ptr(),
+                                           dcode(res_out.scalar_type()), w.data_ptr<float>(), rstd.data_ptr<float>(),
+                                           dx.data_ptr(), dcode(dx_dtype), write_dres ? dres.data_ptr() : nullptr,
+                                           dcode(dres_dtype), part.data_ptr<float>(), dw.data_ptr<float>(), M, (int)D,
+                                           cur_stream()));
+  return {dx, dres, dw.to(weight.scalar_type())};
+}
+
+std::tuple<Tensor, Tensor> gated_rmsnorm_fwd(Tensor x, Tensor z, Tensor weight, double eps, int64_t group_size,
+                                             bool norm_before_gate) {
+  check_cuda(x, "x");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  TORCH_CHECK(x.dim() == 2 && z.dim() == 2 && x.stride(1) == 1 && z.stride(1) == 1, "x, z must be (M, D), unit col stride");
+  const int64_t M = x.size(0), D = x.size(1);
+  TORCH_CHECK(z.size(0) == M && z.size(1) == D, "z shape mismatch");
+  TORCH_CHECK(D % 4 == 0 && D <= 20 * 256 && group_size % 4 == 0 && D % group_size == 0 && D / group_size <= 64,
+              "unsupported D / group_size");
+  TORCH_CHECK(x.stride(0) % 4 == 0 && z.stride(0) % 4 == 0, "row strides must be multiples of 4");
+  Tensor w = f32c(weight);
+  auto y = at::empty({M, D}, x.options());
+  auto rstd = at::empty({M, D / group_size}, x.options().dtype(at::kFloat));
+  HIPCHK(mamba_amd::launch_gated_rmsnorm_fwd(x.data_ptr(), dcode(x.scalar_type()), x.stride(0), z.data_ptr(),
+                                             dcode(z.scalar_type()), z.stride(0), w.data_ptr<float>(), y.data_ptr(),
+                                             dcode(x.scalar_type()), rstd.data_ptr<float>(), M, (int)D, (int)group_size,
+                                             (float)eps, norm_before_gate, cur_stream()));
+  return {y, rstd};
+}
+
+std::tuple<Tensor, Tensor, Tensor> gated_rmsnorm_bwd(Tensor dy, Tensor x, Tensor z, Tensor weight, Tensor rstd,
+                                                     int64_t group_size, bool norm_before_gate, optional<Tensor> dx_out,
+                                                     optional<Tensor> dz_out) {
+  check_cuda(dy, "dy");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
+  dy = dy.contiguous();
+  const int64_t M = x.size(0), D = x.size(1);
+  TORCH_CHECK(x.stride(1) == 1 && z.stride(1) == 1 && x.stride(0) % 4 == 0 && z.stride(0) % 4 == 0, "x/z layout");
+  Tensor dx = dx_out.has_value() && dx_out->defined() ? *dx_out : at::empty({M, D}, x.options());
+  Tensor dz = dz_out.has_value() && dz_out->defined() ? *dz_out : at::empty({M, D}, z.options());
+  TORCH_CHECK(dx.size(0) == M && dx.size(1) == D && dx.stride(1) == 1 && dx.stride(0) % 4 == 0 &&
+                  dx.scalar_type() == x.scalar_type(), "dx_out layout");
+  TORCH_CHECK(dz.size(0) == M && dz.size(1) == D && dz.stride(1) == 1 && dz.stride(0) % 4 == 0 &&
+                  dz.scalar_type() == z.scalar_type(), "dz_out layout");
+  Tensor w = f32c(weight);
+  const int rows = mamba_amd::norm_bwd_partial_rows(M);
+  auto part = at::empty({rows, D}, dy.options().dtype(at::kFloat));
+  auto dw = at::empty({D}, dy.options().dtype(at::kFloat));
+  HIPCHK(mamba_amd::launch_gated_rmsnorm_bwd(dy.data_ptr(), dcode(dy.scalar_type()), x.data_ptr(), dcode(x.scalar_type()),
+                                             x.stride(0), z.data_ptr(), dcode(z.scalar_type()), z.stride(0),
+                                             w.data_ptr<float>(), rstd.data_ptr<float>(), dx.data_ptr(), dx.stride(0),
+                                             dz.data_ptr(), dz.stride(0), part.data_ptr<float>(), dw.data_ptr<float>(), M,
+                                             (int)D, (int)group_size, norm_before_gate, cur_stream()));
+  return {dx, dz, dw.to(weight.scalar_type())};
+}
+
+// ---------------------------------------------------------------------------------------------
+// cross entropy
+Tensor ce_fwd(Tensor logits, Tensor targets, int64_t ignore_index, Tensor scale, optional<Tensor> grad) {
+  check_cuda(logits, "logits");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(logits.device());
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits must be (M, V) with unit col stride");
+  const int64_t M = logits.size(0), V = logits.size(1);
+  auto t = targets.to(at::kLong).contiguous();
+  TORCH_CHECK(t.numel() == M, "targets size mismatch");
+  auto sc = scale.to(at::kFloat).contiguous();
+  auto loss = at::empty({M}, logits.options().dtype(at::kFloat));
+  void* g = nullptr;
+  int64_t ldg = 0;
+  if (grad.has_value() && grad->defined()) {
+    TORCH_CHECK(grad->size(0) == M && grad->size(1) == V && grad->stride(1) == 1 &&
+                grad->scalar_type() == logits.scalar_type(), "grad layout");
+    g = grad->data_ptr();
+    ldg = grad->stride(0);
+  }
+  HIPCHK(mamba_amd::launch_ce_fwd(logits.data_ptr(), dcode(logits.scalar_type()), logits.stride(0), t.data_ptr<int64_t>(),
+                                  M, (int)V, ignore_index, sc.data_ptr<float>(), loss.data_ptr<float>(), g, ldg,
+                                  cur_stream()));
+  return loss;
+}
+
+// ---------------------------------------------------------------------------------------------
+// causal conv1d
+Tensor conv1d_cf_fwd(Tensor x, Tensor weight, optional<Tensor> bias, bool silu) {
+  check_cuda(x, "x");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1, "x must be (b, d, l) with unit time stride");
+  const int64_t B = x.size(0), D = x.size(1), L = x.size(2);
+  Tensor w = f32c(weight);
+  TORCH_CHECK(w.dim() == 2 && w.size(0) == D && w.size(1) >= 2 && w.size(1) <= 4, "weight must be (d, w), 2<=w<=4");
+  Tensor bb = f32c_opt(bias);
+  auto out = at::empty({D, B, L}, x.options()).permute({1, 0, 2});
+  HIPCHK(mamba_amd::launch_conv_cf_fwd(x.data_ptr(), dcode(x.scalar_type()), x.stride(0), x.stride(1), w.data_ptr<float>(),
+                                       fptr(bb), out.data_ptr(), out.stride(0), out.stride(1), (int)B, (int)D, (int)L,
+                                       (int)w.size(1), silu, cur_stream()));
+  return out;
+}
+
+std::tuple<Tensor, Tensor, Tensor> conv1d_cf_bwd(Tensor x, Tensor weight, optional<Tensor> bias, Tensor dout, bool silu,
+                                                 optional<Tensor> dx_out) {
+  check_cuda(x, "x");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1, "x must be (b, d, l) with unit time stride");
+  if (dout.stride(2) != 1) dout = dout.contiguous();
+  const int64_t B = x.size(0), D = x.size(1), L = x.size(2);
+  TORCH_CHECK(dout.size(0) == B && dout.size(1) == D && dout.size(2) == L && dout.scalar_type() == x.scalar_type(),
+              "dout mismatch");
+  Tensor w = f32c(weight);
+  Tensor bb = f32c_opt(bias);
+  Tensor dx = dx_out.has_value() && dx_out->defined() ? *dx_out : at::empty({D, B, L}, x.options()).permute({1, 0, 2});
+  TORCH_CHECK(dx.size(0) == B && dx.size(1) == D && dx.size(2) == L && dx.stride(2) == 1 &&
+              dx.scalar_type() == x.scalar_type(), "dx_out layout");
+  const int W = (int)w.size(1);
+  auto part = at::empty({B, D, W + 1}, x.options().dtype(at::kFloat));
+  auto dw = at::empty({D, W}, x.options().dtype(at::kFloat));
+  auto db = at::empty({D}, x.options().dtype(at::kFloat));
+  HIPCHK(mamba_amd::launch_conv_cf_bwd(x.data_ptr(), dcode(x.scalar_type()), x.stride(0), x.stride(1), w.data_ptr<float>(),
+                                       fptr(bb), dout.data_ptr(), dout.stride(0), dout.stride(1), dx.data_ptr(),
+                                       dx.stride(0), dx.stride(1), part.data_ptr<float>(), dw.data_ptr<float>(),
+                                       db.data_ptr<float>(), (int)B, (int)D, (int)L, W, silu, cur_stream()));
+  return {dx, dw, db};
+}
+
+Tensor conv1d_cl_fwd(Tensor x, Tensor weight, optional<Tensor> bias, bool silu) {
+  check_cuda(x, "x");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1, "x must be (b, l, c) with unit channel stride");
+  const int64_t B = x.size(0), L = x.size(1), C = x.size(2);
+  Tensor w = f32c(weight);
+  TORCH_CHECK(w.dim() == 2 && w.size(0) == C && w.size(1) >= 2 && w.size(1) <= 4, "weight must be (c, w), 2<=w<=4");
+  Tensor bb = f32c_opt(bias);
+  auto out = at::empty({B, L, C}, x.options());
+  HIPCHK(mamba_amd::launch_conv_cl_fwd(x.data_ptr(), dcode(x.scalar_type()), x.stride(0), x.stride(1), w.data_ptr<float>(),
+                                       fptr(bb), out.data_ptr(), out.stride(0), out.stride(1), (int)B, (int)L, (int)C,
+                                       (int)w.size(1), silu, cur_stream()));
+  return out;
+}
+
+std::tuple<Tensor, Tensor, Tensor> conv1d_cl_bwd(Tensor x, Tensor weight, optional<Tensor> bias, Tensor dout, bool silu,
+                                                 optional<Tensor> dx_out) {
+  check_cuda(x, "x");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1, "x must be (b, l, c) with unit channel stride");
+  if (dout.stride(2) != 1) dout = dout.contiguous();
+  const int64_t B = x.size(0), L = x.size(1), C = x.size(2);
+  TORCH_CHECK(dout.size(0) == B && dout.size(1) == L && dout.size(2) == C && dout.scalar_type() == x.scalar_type(),
+              "dout mismatch");
+  Tensor w = f32c(weight);
+  Tensor bb = f32c_opt(bias);
+  Tensor dx = dx_out.has_value() && dx_out->defined() ? *dx_out : at::empty({B, L, C}, x.options());
+  TORCH_CHECK(dx.size(0) == B && dx.size(1) == L && dx.size(2) == C && dx.stride(2) == 1 &&
+              dx.scalar_type() == x.scalar_type(), "dx_out layout");
+  const int W = (int)w.size(1);
+  auto part = at::empty({mamba_amd::conv_cl_bwd_partial_rows((int)B, (int)L), C, W + 1}, x.options().dtype(at::kFloat));
+  auto dw = at::empty({C, W}, x.options().dtype(at::kFloat));
+  auto db = at::empty({C}, x.options().dtype(at::kFloat));
+  HIPCHK(mamba_amd::launch_conv_cl_bwd(x.data_ptr(), dcode(x.scalar_type()), x.stride(0), x.stride(1), w.data_ptr<float>(),
+                                       fptr(bb), dout.data_ptr(), dout.stride(0), dout.stride(1), dx.data_ptr(),
+                                       dx.stride(0), dx.stride(1), part.data_ptr<float>(), dw.data_ptr<float>(),
+                                       db.data_ptr<float>(), (int)B, (int)L, (int)C, W, silu, cur_stream()));
+  return {dx, dw, db};
+}
+
+Tensor conv1d_update(Tensor x, Tensor conv_state, Tensor weight, optional<Tensor> bias, bool silu) {
+  check_cuda(x, "x");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be (b, c)");
+  const int64_t B = x.size(0), C = x.size(1);
+  Tensor w = f32c(weight);
+  TORCH_CHECK(w.size(0) == C && conv_state.size(0) == B && conv_state.size(1) == C && conv_state.size(2) == w.size(1) - 1 &&
+              conv_state.stride(2) == 1 && conv_state.scalar_type() == x.scalar_type(), "conv_state layout");
+  Tensor bb = f32c_opt(bias);
+  auto out = at::empty({B, C}, x.options());
+  HIPCHK(mamba_amd::launch_conv_update(x.data_ptr(), dcode(x.scalar_type()), x.stride(0), conv_state.data_ptr(),
+                                       conv_state.stride(0), conv_state.stride(1), w.data_ptr<float>(), fptr(bb),
+                                       out.data_ptr(), (int)B, (int)C, (int)w.size(1), silu, cur_stream()));
+  return out;
+}
+
+// ---------------------------------------------------------------------------------------------
+// SSD
+int pick_hg(int B, int nc, int H, int G) {
+  const int hpg = H / G;
+  int best = 1;
+  for (int d = 1; d <= 8 && d <= hpg; ++d)
+    if (hpg % d == 0 && (int64_t)B * nc * (H / d) >= 1536) best = d;
+  return best;
+}
+
+void ssd_common(mamba_amd::SSDArgs& a, const Tensor& x, const Tensor& dt, const Tensor& A, const Tensor& Bm,
+                const Tensor& Cm, int64_t chunk, bool softplus, double dt_min, double dt_max) {
+  TORCH_CHECK(chunk == 64, "native SSD chunk must be 64");
+  TORCH_CHECK(x.dim() == 4 && x.stride(3) == 1 && x.scalar_type() == at::kBFloat16, "x must be bf16 (b,l,h,p), unit p");
+  TORCH_CHECK(x.size(3) == 64, "native SSD supports headdim 64");
+  TORCH_CHECK(Bm.dim() == 4 && Cm.dim() == 4 && Bm.stride(3) == 1 && Cm.stride(3) == 1 &&
+              Bm.scalar_type() == at::kBFloat16 && Cm.scalar_type() == at::kBFloat16, "B/C must be bf16 (b,l,g,n)");
+  a.B = x.size(0); a.L = x.size(1); a.H = x.size(2); a.G = Bm.size(2); a.N = Bm.size(3);
+  TORCH_CHECK(a.N == 64 || a.N == 128, "native SSD supports d_state 64 or 128");
+  TORCH_CHECK(a.H % a.G == 0 && Bm.size(0) == a.B && Bm.size(1) == a.L && Cm.sizes() == Bm.sizes(), "B/C shape");
+  TORCH_CHECK(dt.dim() == 3 && dt.size(0) == a.B && dt.size(1) == a.L && dt.size(2) == a.H, "dt shape");
+  TORCH_CHECK(A.numel() == a.H, "A shape");
+  // 16-B aligned rows for the tile loads
+  auto al = [](const Tensor& t, int64_t s) { return ((uintptr_t)t.data_ptr() % 16 == 0) && (s % 8 == 0); };
+  TORCH_CHECK(al(x, x.stride(1)) && x.stride(2) % 8 == 0 && x.stride(0) % 8 == 0, "x rows must be 16-B aligned");
+  TORCH_CHECK(al(Bm, Bm.stride(1)) && al(Cm, Cm.stride(1)) && Bm.stride(0) % 8 == 0 && Cm.stride(0) % 8 == 0 &&
+              Bm.stride(2) % 8 == 0 && Cm.stride(2) % 8 == 0, "B/C rows must be 16-B aligned");
+  a.nc = (a.L + 63) / 64; a.Lp = a.nc * 64;
+  a.HG = pick_hg(a.B, a.nc, a.H, a.G); a.nhg = a.H / a.HG;
+  a.x = (const mamba_amd::bf16_t*)x.data_ptr(); a.sxb = x.stride(0); a.sxl = x.stride(1); a.sxh = x.stride(2);
+  a.dt = dt.data_ptr(); a.dt_dtype = dcode(dt.scalar_type());
+  a.sdtb = dt.stride(0); a.sdtl = dt.stride(1); a.sdth = dt.stride(2);
+  a.Bm = (const mamba_amd::bf16_t*)Bm.data_ptr(); a.sBb = Bm.stride(0); a.sBl = Bm.stride(1); a.sBg = Bm.stride(2);
+  a.Cm = (const mamba_amd::bf16_t*)Cm.data_ptr(); a.sCb = Cm.stride(0); a.sCl = Cm.stride(1); a.sCg = Cm.stride(2);
+  a.softplus = softplus; a.dt_min = (float)dt_min; a.dt_max = (float)dt_max;
+}
+
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> ssd_fwd(Tensor x, Tensor dt, Tensor A, Tensor Bm, Tensor Cm,
+                                                           optional<Tensor> D, optional<Tensor> dt_bias,
+                                                           optional<Tensor> init, int64_t chunk, bool softplus,
+                                                           double dt_min, double dt_max) {
+  check_cuda(x, "x");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  mamba_amd::SSDArgs a{};
+  ssd_common(a, x, dt, A, Bm, Cm, chunk, softplus, dt_min, dt_max);
+  Tensor Af = f32c(A), Df = f32c_opt(D), bf = f32c_opt(dt_bias), If = f32c_opt(init);
+  if (Df.defined()) TORCH_CHECK(Df.numel() == a.H, "D must be (h,)");
+  if (bf.defined()) TORCH_CHECK(bf.numel() == a.H, "dt_bias must be (h,)");
+  if (If.defined()) TORCH_CHECK(If.numel() == (int64_t)a.B * a.H * 64 * a.N, "initial_states must be (b,h,p,n)");
+  a.A = Af.data_ptr<float>(); a.D = fptr(Df); a.dt_bias = fptr(bf); a.init = fptr(If);
+  auto fo = x.options().dtype(at::kFloat);
+  auto dtp = at::empty({a.B, a.H, a.Lp}, fo);
+  auto cum = at::empty({a.B, a.H, a.Lp}, fo);
+  auto states = at::empty({a.B, a.nc, a.H, 64, a.N}, x.options());
+  auto final_ = at::empty({a.B, a.H, 64, a.N}, fo);
+  auto y = at::empty({a.B, a.L, a.H, 64}, x.options());
+  a.dtp = dtp.data_ptr<float>(); a.cum = cum.data_ptr<float>();
+  a.states = (mamba_amd::bf16_t*)states.data_ptr(); a.final_state = final_.data_ptr<float>();
+  a.y = (mamba_amd::bf16_t*)y.data_ptr(); a.syb = y.stride(0); a.syl = y.stride(1); a.syh = y.stride(2);
+  HIPCHK(mamba_amd::launch_ssd_fwd(a, cur_stream()));
+  return {y, cum, dtp, states, final_};
+}
+
+std::vector<Tensor> ssd_bwd(Tensor dy, Tensor x, Tensor dt, Tensor A, Tensor Bm, Tensor Cm, optional<Tensor> D,
+                            optional<Tensor> dt_bias, optional<Tensor> init, Tensor cum, Tensor dtp, Tensor states,
+                            optional<Tensor> dfinal, int64_t chunk, bool softplus, double dt_min, double dt_max,
+                            optional<Tensor> dx_out, optional<Tensor> ddt_out, optional<Tensor> dB_out,
+                            optional<Tensor> dC_out) {
+  check_cuda(x, "x");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  mamba_amd::SSDArgs a{};
+  ssd_common(a, x, dt, A, Bm, Cm, chunk, softplus, dt_min, dt_max);
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.stride(3) == 1 && dy.scalar_type() == at::kBFloat16, "dy layout");
+  if (!(((uintptr_t)dy.data_ptr() % 16 == 0) && dy.stride(1) % 8 == 0 && dy.stride(2) % 8 == 0 && dy.stride(0) % 8 == 0))
+    dy = dy.contiguous();
+  Tensor Af = f32c(A), Df = f32c_opt(D), bf = f32c_opt(dt_bias), If = f32c_opt(init), dF = f32c_opt(dfinal);
+  a.A = Af.data_ptr<float>(); a.D = fptr(Df); a.dt_bias = fptr(bf); a.init = fptr(If);
+  TORCH_CHECK(cum.is_contiguous() && dtp.is_contiguous() && states.is_contiguous(), "saved tensors must be contiguous");
+  a.cum = cum.data_ptr<float>(); a.dtp = dtp.data_ptr<float>(); a.states = (mamba_amd::bf16_t*)states.data_ptr();
+  a.dy = (const mamba_amd::bf16_t*)dy.data_ptr(); a.sdyb = dy.stride(0); a.sdyl = dy.stride(1); a.sdyh = dy.stride(2);
+  a.dfinal = fptr(dF);
+  auto fo = x.options().dtype(at::kFloat);
+  auto dstates = at::empty_like(states);
+  a.dstates = (mamba_amd::bf16_t*)dstates.data_ptr();
+  Tensor dinit = If.defined() ? at::empty({a.B, a.H, 64, a.N}, fo) : at::empty({0}, fo);
+  a.dinit = If.defined() ? dinit.data_ptr<float>() : nullptr;
+  Tensor dx = dx_out.has_value() && dx_out->defined() ? *dx_out : at::empty_like(x, at::MemoryFormat::Contiguous);
+  TORCH_CHECK(dx.sizes() == x.sizes() && dx.stride(3) == 1 && dx.scalar_type() == at::kBFloat16 &&
+              (uintptr_t)dx.data_ptr() % 16 == 0 && dx.stride(1) % 8 == 0 && dx.stride(0) % 8 == 0 &&
+              dx.stride(2) % 8 == 0, "dx layout");
+  Tensor ddt = ddt_out.has_value() && ddt_out->defined() ? *ddt_out : at::empty(dt.sizes(), dt.options());
+  TORCH_CHECK(ddt.sizes() == dt.sizes(), "ddt shape");
+  Tensor dB = dB_out.has_value() && dB_out->defined() ? *dB_out : at::empty(Bm.sizes(), Bm.options());
+  Tensor dC = dC_out.has_value() && dC_out->defined() ? *dC_out : at::empty(Cm.sizes(), Cm.options());
+  auto chk = [](const Tensor& t) {
+    TORCH_CHECK(t.stride(3) == 1 && t.scalar_type() == at::kBFloat16 && (uintptr_t)t.data_ptr() % 16 == 0 &&
+                t.stride(1) % 8 == 0 && t.stride(0) % 8 == 0 && t.stride(2) % 8 == 0, "dB/dC layout");
+  };
+  chk(dB);
+  chk(dC);
+  a.dx = (mamba_amd::bf16_t*)dx.data_ptr(); a.sdxb = dx.stride(0); a.sdxl = dx.stride(1); a.sdxh = dx.stride(2);
+  a.ddt = ddt.data_ptr(); a.ddt_dtype = dcode(ddt.scalar_type());
+  a.sddtb = ddt.stride(0); a.sddtl = ddt.stride(1); a.sddth = ddt.stride(2);
+  a.dB = (mamba_amd::bf16_t*)dB.data_ptr(); a.sdBb = dB.stride(0); a.sdBl = dB.stride(1); a.sdBg = dB.stride(2);
+  a.dC = (mamba_amd::bf16_t*)dC.data_ptr(); a.sdCb = dC.stride(0); a.sdCl = dC.stride(1); a.sdCg = dC.stride(2);
+  auto part_dcb = at::empty({a.B, a.nc, a.nhg, 64, 64}, fo);
+  auto part_db = at::empty({a.B, a.nc, a.nhg, 64, a.N}, fo);
+  auto part_dc = at::empty({a.B, a.nc, a.nhg, 64, a.N}, fo);
+  auto part_small = at::empty({3, a.B, a.nc, a.H}, fo);
+  a.part_dcb = part_dcb.data_ptr<float>(); a.part_db = part_db.data_ptr<float>(); a.part_dc = part_dc.data_ptr<float>();
+  a.part_dA = part_small[0].data_ptr<float>(); a.part_dD = part_small[1].data_ptr<float>();
+  a.part_dbias = part_small[2].data_ptr<float>();
+  HIPCHK(mamba_amd::launch_ssd_bwd(a, cur_stream()));
+  auto sums = part_small.sum({1, 2});  // (3, H), fixed-order reduction
+  Tensor dA = sums[0].to(A.scalar_type());
+  Tensor dD = D.has_value() && D->defined() ? sums[1].to(D->scalar_type()) : at::empty({0}, fo);
+  Tensor dbias = dt_bias.has_value() && dt_bias->defined() ? sums[2].to(dt_bias->scalar_type()) : at::empty({0}, fo);
+  return {dx, ddt, dA, dB, dC, dD, dbias, dinit};
+}
+
+// ---------------------------------------------------------------------------------------------
+// selective scan (Mamba-1)
+void selscan_common(mamba_amd::SelScanArgs& a, const Tensor& u, const Tensor& delta, const Tensor& A, const Tensor& Bm,
+                    const Tensor& Cm, const Tensor& z, bool softplus) {
+  TORCH_CHECK(u.dim() == 3 && u.stride(2) == 1 && delta.stride(2) == 1, "u/delta must be (b,d,l) with unit time stride");
+  TORCH_CHECK(delta.sizes() == u.sizes() && delta.scalar_type() == u.scalar_type(), "delta mismatch");
+  TORCH_CHECK(Bm.dim() == 4 && Cm.dim() == 4 && Bm.stride(3) == 1 && Cm.stride(3) == 1, "B/C must be (b,g,n,l), unit l");
+  TORCH_CHECK(Bm.scalar_type() == u.scalar_type() && Cm.scalar_type() == u.scalar_type(), "B/C dtype must match u");
+  a.B = u.size(0); a.D = u.size(1); a.L = u.size(2); a.G = Bm.size(1); a.N = Bm.size(2);
+  TORCH_CHECK(A.dim() == 2 && A.size(0) == a.D && A.size(1) == a.N, "A must be (d, n)");
+  TORCH_CHECK(a.N == 16 || a.N == 8 || a.N == 4, "native selective scan supports d_state 4/8/16");
+  TORCH_CHECK(a.D % a.G == 0 && Bm.size(3) == a.L && Cm.sizes() == Bm.sizes(), "B/C shape");
+  a.dtype = dcode(u.scalar_type());
+  a.Kc = 64;
+  a.softplus = softplus;
+  auto v8 = [&](const Tensor& t, int64_t s0, int64_t s1) {
+    return a.dtype == mamba_amd::kBF16 && (uintptr_t)t.data_ptr() % 16 == 0 && s0 % 8 == 0 && s1 % 8 == 0;
+  };
+  a.vec = v8(u, u.stride(0), u.stride(1)) && v8(delta, delta.stride(0), delta.stride(1));
+  a.vecbc = v8(Bm, Bm.stride(0), Bm.stride(2)) && v8(Cm, Cm.stride(0), Cm.stride(2)) && Bm.stride(1) % 8 == 0 &&
+            Cm.stride(1) % 8 == 0;
+  a.vecz = z.defined() && v8(z, z.stride(0), z.stride(1));
+  a.u_ = u.data_ptr(); a.sub = u.stride(0); a.sud = u.stride(1);
+  a.delta_ = delta.data_ptr(); a.sdb = delta.stride(0); a.sdd = delta.stride(1);
+  a.Bm_ = Bm.data_ptr(); a.sBb = Bm.stride(0); a.sBg = Bm.stride(1); a.sBn = Bm.stride(2);
+  a.Cm_ = Cm.data_ptr(); a.sCb = Cm.stride(0); a.sCg = Cm.stride(1); a.sCn = Cm.stride(2);
+  if (z.defined()) {
+    TORCH_CHECK(z.sizes() == u.sizes() && z.stride(2) == 1 && z.scalar_type() == u.scalar_type(), "z layout");
+    a.z_ = z.data_ptr(); a.szb = z.stride(0); a.szd = z.stride(1);
+  }
+}
+
+std::tuple<Tensor, Tensor, Tensor> selscan_fwd(Tensor u, Tensor delta, Tensor A, Tensor Bm, Tensor Cm,
+                                               optional<Tensor> D, optional<Tensor> z, optional<Tensor> delta_bias,
+                                               bool softplus) {
+  check_cuda(u, "u");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(u.device());
+  mamba_amd::SelScanArgs a{};
+  Tensor zz = z.has_value() && z->defined() ? *z : Tensor();
+  selscan_common(a, u, delta, A, Bm, Cm, zz, softplus);
+  Tensor Af = f32c(A), Df = f32c_opt(D), bf = f32c_opt(delta_bias);
+  a.A = Af.data_ptr<float>(); a.D_ = fptr(Df); a.delta_bias = fptr(bf);
+  auto out = at::empty({a.D, a.B, a.L}, u.options()).permute({1, 0, 2});
+  a.out_ = out.data_ptr(); a.sob = out.stride(0); a.sod = out.stride(1);
+  const int nt = mamba_amd::selscan_ntiles(a.L);
+  auto fo = u.options().dtype(at::kFloat);
+  auto carries = at::empty({a.B, a.D, nt, a.N}, fo);
+  auto last = at::empty({a.B, a.D, a.N}, fo);
+  a.carries = carries.data_ptr<float>(); a.last_state = last.data_ptr<float>();
+  HIPCHK(mamba_amd::launch_selscan_fwd(a, cur_stream()));
+  return {out, carries, last};
+}
+
+std::vector<Tensor> selscan_bwd_impl(Tensor dout, Tensor u, Tensor delta, Tensor A, Tensor Bm, Tensor Cm,
+                                     optional<Tensor> D, optional<Tensor> z, optional<Tensor> delta_bias, Tensor carries,
+                                     bool softplus, optional<Tensor> dz_out, optional<Tensor> dB_out,
+                                     optional<Tensor> dC_out) {
+  check_cuda(u, "u");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(u.device());
+  mamba_amd::SelScanArgs a{};
+  Tensor zz = z.has_value() && z->defined() ? *z : Tensor();
+  selscan_common(a, u, delta, A, Bm, Cm, zz, softplus);
+  if (dout.stride(2) != 1 || dout.scalar_type() != u.scalar_type()) dout = dout.to(u.scalar_type()).contiguous();
+  TORCH_CHECK(dout.sizes() == u.sizes(), "dout shape");
+  TORCH_CHECK(carries.is_contiguous() && carries.size(2) == mamba_amd::selscan_ntiles(a.L), "carries");
+  Tensor Af = f32c(A), Df = f32c_opt(D), bf = f32c_opt(delta_bias);
+  a.A = Af.data_ptr<float>(); a.D_ = fptr(Df); a.delta_bias = fptr(bf);
+  a.carries = carries.data_ptr<float>();
+  a.dout_ = dout.data_ptr(); a.sgb = dout.stride(0); a.sgd = dout.stride(1);
+  a.vecg = a.dtype == mamba_amd::kBF16 && (uintptr_t)dout.data_ptr() % 16 == 0 && dout.stride(0) % 8 == 0 &&
+           dout.stride(1) % 8 == 0;
+  auto mk = [&]() { return at::empty({a.D, a.B, a.L}, u.options()).permute({1, 0, 2}); };
+  Tensor du = mk(), ddelta = mk();
+  a.du_ = du.data_ptr(); a.sdub = du.stride(0); a.sdud = du.stride(1);
+  a.ddelta_ = ddelta.data_ptr(); a.sddb = ddelta.stride(0); a.sddd = ddelta.stride(1);
+  Tensor dz;
+  if (zz.defined()) {
+    dz = dz_out.has_value() && dz_out->defined() ? *dz_out : mk();
+    TORCH_CHECK(dz.sizes() == u.sizes() && dz.stride(2) == 1 && dz.scalar_type() == u.scalar_type(), "dz layout");
+    a.dz_ = dz.data_ptr(); a.sdzb = dz.stride(0); a.sdzd = dz.stride(1);
+  }
+  Tensor dB = dB_out.has_value() && dB_out->defined() ? *dB_out : at::empty(Bm.sizes(), Bm.options());
+  Tensor dC = dC_out.has_value() && dC_out->defined() ? *dC_out : at::empty(Cm.sizes(), Cm.options());
+  TORCH_CHECK(dB.sizes() == Bm.sizes() && dC.sizes() == Cm.sizes() && dB.stride(3) == 1 && dC.stride(3) == 1 &&
+              dB.scalar_type() == u.scalar_type() && dC.scalar_type() == u.scalar_type(), "dB/dC layout");
+  a.dB_ = dB.data_ptr(); a.sdBb = dB.stride(0); a.sdBg = dB.stride(1); a.sdBn = dB.stride(2);
+  a.dC_ = dC.data_ptr(); a.sdCb = dC.stride(0); a.sdCg = dC.stride(1); a.sdCn = dC.stride(2);
+  auto fo = u.options().dtype(at::kFloat);
+  const int ndg = (a.D + a.Kc - 1) / a.Kc;
+  auto part_bc = at::empty({2, a.B, ndg, a.N, a.L}, fo);
+  a.part_dB = part_bc[0].data_ptr<float>(); a.part_dC = part_bc[1].data_ptr<float>();
+  auto part_dA = at::zeros({a.B, a.D, a.N}, fo);
+  auto part_dd = at::zeros({2, a.B, a.D}, fo);
+  a.part_dA = part_dA.data_ptr<float>(); a.part_dD = part_dd[0].data_ptr<float>(); a.part_dbias = part_dd[1].data_ptr<float>();
+  HIPCHK(mamba_amd::launch_selscan_bwd(a, cur_stream()));
+  Tensor dA = part_dA.sum(0).to(A.scalar_type());
+  auto s2 = part_dd.sum(1);
+  Tensor dD = D.has_value() && D->defined() ? s2[0].to(D->scalar_type()) : at::empty({0}, fo);
+  Tensor dbias = delta_bias.has_value() && delta_bias->defined() ? s2[1].to(delta_bias->scalar_type()) : at::empty({0}, fo);
+  if (!dz.defined()) dz = at::empty({0}, u.options());
+  return {du, ddelta, dA, dB, dC, dD, dz, dbias};
+}
+
+std::vector<Tensor> selscan_bwd(Tensor dout, Tensor u, Tensor delta, Tensor A, Tensor Bm, Tensor Cm, optional<Tensor> D,
+                                optional<Tensor> z, optional<Tensor> delta_bias, Tensor carries, bool softplus) {
+  return selscan_bwd_impl(dout, u, delta, A, Bm, Cm, D, z, delta_bias, carries, softplus, c10::nullopt, c10::nullopt,
+                          c10::nullopt);
+}
+
+std::vector<Tensor> selscan_bwd_into(Tensor dout, Tensor u, Tensor delta, Tensor A, Tensor Bm, Tensor Cm,
+                                     optional<Tensor> D, optional<Tensor> z, optional<Tensor> delta_bias, Tensor carries,
+                                     bool softplus, Tensor dz_out, Tensor dB_out, Tensor dC_out) {
+  return selscan_bwd_impl(dout, u, delta, A, Bm, Cm, D, z, delta_bias, carries, softplus, dz_out, dB_out, dC_out);
+}
+
+// decode-time recurrent update; Mamba-1: state (b,d,n), x/dt/z (b,d), A (d,n), B/C (b,n), D (d)
+//                               Mamba-2: state (b,h,p,n), x/z (b,h,p), dt (b,h), A (h), B/C (b,g,n), D (h)
+Tensor ssm_state_update(Tensor state, Tensor x, Tensor dt, Tensor A, Tensor Bm, Tensor Cm, optional<Tensor> D,
+                        optional<Tensor> z, optional<Tensor> dt_bias, bool softplus) {
+  check_cuda(x, "x");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  TORCH_CHECK(state.scalar_type() == at::kFloat && state.is_contiguous(), "state must be contiguous fp32");
+  mamba_amd::SSMUpdateArgs a{};
+  a.dtype = dcode(x.scalar_type());
+  a.softplus = softplus;
+  a.B = x.size(0);
+  Tensor Af = f32c(A), Df = f32c_opt(D), bf = f32c_opt(dt_bias);
+  Tensor xx = x, zz = z.has_value() && z->defined() ? *z : Tensor(), dtt = dt, Bb = Bm, Cc = Cm;
+  if (state.dim() == 3) {  // Mamba-1 as H = d, P = 1
+    a.H = state.size(1); a.P = 1; a.N = state.size(2); a.G = 1;
+    a.A_per_n = true; a.D_per_p = false; a.dt_bias_per_p = false;
+    xx = x.unsqueeze(-1);
+    if (zz.defined()) zz = zz.unsqueeze(-1);
+    dtt = dt.unsqueeze(-1);
+    Bb = Bm.unsqueeze(1);
+    Cc = Cm.unsqueeze(1);
+  } else {
+    a.H = state.size(1); a.P = state.size(2); a.N = state.size(3); a.G = Bm.size(1);
+    a.A_per_n = false; a.D_per_p = false; a.dt_bias_per_p = false;
+    dtt = dt.unsqueeze(-1).expand({a.B, a.H, a.P});
+  }
+  TORCH_CHECK(xx.stride(2) == 1 && Bb.stride(2) == 1 && Cc.stride(2) == 1, "unit inner strides required");
+  TORCH_CHECK(Bb.scalar_type() == x.scalar_type() && Cc.scalar_type() == x.scalar_type() &&
+              dtt.scalar_type() == x.scalar_type(), "dtype mismatch");
+  a.state = state.data_ptr<float>();
+  a.x_ = xx.data_ptr(); a.sxb = xx.stride(0); a.sxh = xx.stride(1);
+  a.dt_ = dtt.data_ptr(); a.sdtb = dtt.stride(0); a.sdth = dtt.stride(1); a.sdtp = dtt.stride(2);
+  a.A = Af.data_ptr<float>(); a.D = fptr(Df); a.dt_bias = fptr(bf);
+  a.Bm_ = Bb.data_ptr(); a.sBb = Bb.stride(0); a.sBg = Bb.stride(1);
+  a.Cm_ = Cc.data_ptr(); a.sCb = Cc.stride(0); a.sCg = Cc.stride(1);
+  if (zz.defined()) { a.z_ = zz.data_ptr(); a.szb = zz.stride(0); a.szh = zz.stride(1); }
+  auto out = at::empty(x.sizes(), x.options());
+  a.out_ = out.data_ptr();
+  HIPCHK(mamba_amd::launch_ssm_update(a, cur_stream()));
+  return out;
+}
+
+}  // namespace
+
+TORCH_LIBRARY(mamba_amd, m) {
+  m.def("add_rmsnorm_fwd(Tensor x, Tensor? residual, Tensor weight, float eps, ScalarType out_dtype, "
+        "ScalarType res_dtype) -> (Tensor, Tensor, Tensor)");
+  m.def("add_rmsnorm_bwd(Tensor dy, Tensor? dres_out, Tensor res_out, Tensor weight, Tensor rstd, "
+        "ScalarType dx_dtype, ScalarType dres_dtype, bool write_dres) -> (Tensor, Tensor, Tensor)");
+  m.def("gated_rmsnorm_fwd(Tensor x, Tensor z, Tensor weight, float eps, int group_size, bool norm_before_gate) "
+        "-> (Tensor, Tensor)");
+  m.def("gated_rmsnorm_bwd(Tensor dy, Tensor x, Tensor z, Tensor weight, Tensor rstd, int group_size, "
+        "bool norm_before_gate, Tensor(a!)? dx_out, Tensor(b!)? dz_out) -> (Tensor, Tensor, Tensor)");
+  m.def("ce_fwd(Tensor logits, Tensor targets, int ignore_index, Tensor scale, Tensor(a!)? grad) -> Tensor");
+  m.def("conv1d_cf_fwd(Tensor x, Tensor weight, Tensor? bias, bool silu) -> Tensor");
+  m.def("conv1d_cf_bwd(Tensor x, Tensor weight, Tensor? bias, Tensor dout, bool silu, Tensor(a!)? dx_out) "
+        "-> (Tensor, Tensor, Tensor)");
+  m.def("conv1d_cl_fwd(Tensor x, Tensor weight, Tensor? bias, bool silu) -> Tensor");
+  m.def("conv1d_cl_bwd(Tensor x, Tensor weight, Tensor? bias, Tensor dout, bool silu, Tensor(a!)? dx_out) "
+        "-> (Tensor, Tensor, Tensor)");
+  m.def("conv1d_update(Tensor x, Tensor(a!) conv_state, Tensor weight, Tensor? bias, bool silu) -> Tensor");
+  m.def("ssd_fwd(Tensor x, Tensor dt, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? dt_bias, Tensor? init, "
+        "int chunk, bool softplus, float dt_min, float dt_max) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
+  m.def("ssd_bwd(Tensor dy, Tensor x, Tensor dt, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? dt_bias, "
+        "Tensor? init, Tensor cum, Tensor dtp, Tensor states, Tensor? dfinal, int chunk, bool softplus, float dt_min, "
+        "float dt_max, Tensor(a!)? dx_out, Tensor(b!)? ddt_out, Tensor(c!)? dB_out, Tensor(d!)? dC_out) -> Tensor[]");
+  m.def("selscan_fwd(Tensor u, Tensor delta, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? z, Tensor? delta_bias, "
+        "bool softplus) -> (Tensor, Tensor, Tensor)");
+  m.def("selscan_bwd(Tensor dout, Tensor u, Tensor delta, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? z, "
+        "Tensor? delta_bias, Tensor carries, bool softplus) -> Tensor[]");
+  m.def("selscan_bwd_into(Tensor dout, Tensor u, Tensor delta, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? z, "
+        "Tensor? delta_bias, Tensor carries, bool softplus, Tensor(a!) dz_out, Tensor(b!) dB_out, Tensor(c!) dC_out) "
+        "-> Tensor[]");
+  m.def("ssm_state_update(Tensor(a!) state, Tensor x, Tensor dt, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? z, "
+        "Tensor? dt_bias, bool softplus) -> Tensor");
+}
+
+TORCH_LIBRARY_IMPL(mamba_amd, CUDA, m) {
+  m.impl("add_rmsnorm_fwd", &add_rmsnorm_fwd);
+  m.impl("add_rmsnorm_bwd", &add_rmsnorm_bwd);
+  m.impl("gated_rmsnorm_fwd", &gated_rmsnorm_fwd);
+  m.impl("gated_rmsnorm_bwd", &gated_rmsnorm_bwd);
+  m.impl("ce_fwd", &ce_fwd);
+  m.impl("conv1d_cf_fwd", &conv1d_cf_fwd);
+  m.impl("conv1d_cf_bwd", &conv1d_cf_bwd);
+  m.impl("conv1d_cl_fwd", &conv1d_cl_fwd);
+  m.impl("conv1d_cl_bwd", &conv1d_cl_bwd);
+  m.impl("conv1d_update", &conv1d_update);
+  m.impl("ssd_fwd", &ssd_fwd);
+  m.impl("ssd_bwd", &ssd_bwd);
+  m.impl("selscan_fwd", &selscan_fwd);
+  m.impl("selscan_bwd", &selscan_bwd);
+  m.impl("selscan_bwd_into", &selscan_bwd_into);
+  m.impl("ssm_state_update", &ssm_state_update);
+}

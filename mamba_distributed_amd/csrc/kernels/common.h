@@ -1,0 +1,97 @@
+// Shared device helpers for the gfx950 (MI355X / CDNA4) kernels.
+//
+// * wave64 everywhere: lane = threadIdx.x & 63, reductions over 64 lanes.
+// * bf16 stored as raw 16-bit words (`bf16_t`), converted with v_cvt_pk_bf16_f32 (RNE, NaN-safe)
+//   via the HIP intrinsic; loads are 16-byte vectors wherever alignment allows (Guideline 13).
+// * every launcher takes an explicit hipStream_t (the caller's torch stream) and never syncs,
+//   so all launches are hipGraph-capturable.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+#include "types.h"
+
+namespace mamba_amd {
+
+__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((unsigned)v) << 16); }
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  return __bfloat16_as_ushort(__float2bfloat16(f));
+}
+
+// generic scalar load/store by element type
+template <typename T> __device__ __forceinline__ float ld(const T* p);
+template <> __device__ __forceinline__ float ld<float>(const float* p) { return *p; }
+template <> __device__ __forceinline__ float ld<bf16_t>(const bf16_t* p) { return bf2f(*p); }
+template <typename T> __device__ __forceinline__ void st(T* p, float v);
+template <> __device__ __forceinline__ void st<float>(float* p, float v) { *p = v; }
+template <> __device__ __forceinline__ void st<bf16_t>(bf16_t* p, float v) { *p = f2bf(v); }
+
+// 4-element vector load/store (8 B for bf16, 16 B for f32) — p must be aligned accordingly
+template <typename T> __device__ __forceinline__ void ld4(const T* p, float (&o)[4]);
+template <> __device__ __forceinline__ void ld4<float>(const float* p, float (&o)[4]) {
+  float4 v = *reinterpret_cast<const float4*>(p);
+  o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+}
+template <> __device__ __forceinline__ void ld4<bf16_t>(const bf16_t* p, float (&o)[4]) {
+  uint2 v = *reinterpret_cast<const uint2*>(p);
+  o[0] = __uint_as_float(v.x << 16); o[1] = __uint_as_float(v.x & 0xffff0000u);
+  o[2] = __uint_as_float(v.y << 16); o[3] = __uint_as_float(v.y & 0xffff0000u);
+}
+template <typename T> __device__ __forceinline__ void st4(T* p, const float (&o)[4]);
+template <> __device__ __forceinline__ void st4<float>(float* p, const float (&o)[4]) {
+  *reinterpret_cast<float4*>(p) = make_float4(o[0], o[1], o[2], o[3]);
+}
+__device__ __forceinline__ unsigned pack2(float a, float b) {
+  return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
+}
+template <> __device__ __forceinline__ void st4<bf16_t>(bf16_t* p, const float (&o)[4]) {
+  *reinterpret_cast<uint2*>(p) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+}
+
+// 8 x bf16 = 16 B
+__device__ __forceinline__ void ld8bf(const bf16_t* p, float (&o)[8]) {
+  uint4 v = *reinterpret_cast<const uint4*>(p);
+  unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    o[2 * i] = __uint_as_float(w[i] << 16);
+    o[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void st8bf(bf16_t* p, const float (&o)[8]) {
+  *reinterpret_cast<uint4*>(p) = make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]),
+                                            pack2(o[6], o[7]));
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m, 64));
+  return v;
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float siluf_(float x) { return x * sigmoidf_(x); }
+__device__ __forceinline__ float softplusf_(float x) { return x <= 20.f ? log1pf(__expf(x)) : x; }
+
+// XCD-aware remap of a linear block id (bijective for any grid size; MI355X has 8 XCDs and
+// dispatches blocks round-robin over them, so ids b and b+8 share an L2).  Consecutive logical
+// tiles land on the same XCD -> neighbouring tiles share L2 lines.  Speed only, never correctness.
+__device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
+  const int nx = 8;
+  int q = nblocks / nx, r = nblocks % nx;
+  int xcd = bid % nx, idx = bid / nx;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+}  // namespace mamba_amd
+
+#define MAMBA_HIP_CHECK(expr)                                                    \
+  do {                                                                           \
+    hipError_t _e = (expr);                                                      \
+    if (_e != hipSuccess) return _e;                                             \
+  } while (0)

@@ -1,0 +1,557 @@
+// Causal depthwise conv1d (+ optional SiLU), both memory layouts, for gfx950.
+//   out[b,c,t] = act(bias_c + sum_{k<W} w[c,k] * x[b,c,t-(W-1)+k])      (zero left padding)
+// Reference semantics: causal-conv1d.
+//
+// Channel-first (Mamba-1; x is (b, d, l) with unit time stride):
+//   one wavefront per (b, d) row walks time in 512-step chunks; lane i owns 8 consecutive steps
+//   (one 16-B bf16 load).  The W-1 halo comes from lane i-1 by __shfl_up; lane 0 takes it from the
+//   previous chunk's lane 63 (carried in registers) — every x element is read from HBM once.
+//   Backward walks the chunks in reverse and carries the next chunk's first W-1 dpre values the
+//   same way; dw/db are wave-reduced per row and summed over the batch in a second, fixed-order
+//   pass (deterministic; no float atomics).
+// Channel-last (Mamba-2; xBC is a column slice of the token-major in_proj output):
+//   lane = 8 consecutive channels (16-B), a wave = 512 channels of one time tile, each lane slides
+//   a W-row register window down its T_TILE timesteps.  dw/db: per-lane registers -> the block's
+//   4 waves (4 time tiles) summed through LDS -> one partial row per block -> fixed-order sum.
+#include "common.h"
+#include "launchers.h"
+
+namespace mamba_amd {
+
+template <typename T> struct Vec8 {
+  static __device__ __forceinline__ void load(const T* p, float (&o)[8]);
+  static __device__ __forceinline__ void store(T* p, const float (&o)[8]);
+};
+template <> struct Vec8<bf16_t> {
+  static __device__ __forceinline__ void load(const bf16_t* p, float (&o)[8]) { ld8bf(p, o); }
+  static __device__ __forceinline__ void store(bf16_t* p, const float (&o)[8]) { st8bf(p, o); }
+};
+template <> struct Vec8<float> {
+  static __device__ __forceinline__ void load(const float* p, float (&o)[8]) {
+    float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+  }
+  static __device__ __forceinline__ void store(float* p, const float (&o)[8]) {
+    reinterpret_cast<float4*>(p)[0] = make_float4(o[0], o[1], o[2], o[3]);
+    reinterpret_cast<float4*>(p)[1] = make_float4(o[4], o[5], o[6], o[7]);
+  }
+};
+
+// load 8 consecutive elements starting at p (index t0..t0+7 of a row of length L), zero beyond L
+template <typename T, bool VEC>
+__device__ __forceinline__ void load_run(const T* p, int t0, int L, float (&o)[8]) {
+  if (VEC && t0 + 8 <= L) {
+    Vec8<T>::load(p, o);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (t0 + j < L) ? ld(p + j) : 0.f;
+  }
+}
+template <typename T, bool VEC>
+__device__ __forceinline__ void store_run(T* p, int t0, int L, const float (&o)[8]) {
+  if (VEC && t0 + 8 <= L) {
+    Vec8<T>::store(p, o);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (t0 + j < L) st(p + j, o[j]);
+  }
+}
+
+__device__ __forceinline__ float act_fwd(float a, bool silu) { return silu ? siluf_(a) : a; }
+__device__ __forceinline__ float act_bwd(float a, float g, bool silu) {
+  if (!silu) return g;
+  const float s = sigmoidf_(a);
+  return g * s * (1.f + a * (1.f - s));
+}
+
+// =========================== channel-first ===============================================
+template <typename T, int W, bool VEC>
+__global__ __launch_bounds__(256) void conv_cf_fwd_k(const T* __restrict__ x, int64_t sxb, int64_t sxd,
+                                                     const float* __restrict__ w, const float* __restrict__ bias,
+                                                     T* __restrict__ out, int64_t sob, int64_t sod, int Bn, int Dn,
+                                                     int L, bool silu) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= (int64_t)Bn * Dn) return;  // whole wave exits together
+  const int b = (int)(row / Dn), d = (int)(row % Dn);
+  const T* xr = x + b * sxb + d * sxd;
+  T* orow = out + b * sob + d * sod;
+  float wk[W];
+#pragma unroll
+  for (int k = 0; k < W; ++k) wk[k] = w[d * W + k];
+  const float bs = bias ? bias[d] : 0.f;
+  float carry[3] = {0.f, 0.f, 0.f};  // x[t0-3..t0-1] for lane 0 of the current chunk
+  for (int c0 = 0; c0 < L; c0 += 512) {
+    const int t0 = c0 + lane * 8;
+    float cur[8];
+    load_run<T, VEC>(xr + t0, t0, L, cur);
+    float prev[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      float v = __shfl_up(cur[5 + j], 1, 64);
+      prev[j] = lane == 0 ? carry[j] : v;
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) carry[j] = __shfl(cur[5 + j], 63, 64);
+    float win[11];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) win[j] = prev[j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) win[3 + j] = cur[j];
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float a = bs;
+#pragma unroll
+      for (int k = 0; k < W; ++k) a += wk[k] * win[3 + j - (W - 1) + k];
+      o[j] = act_fwd(a, silu);
+    }
+    if (t0 < L) store_run<T, VEC>(orow + t0, t0, L, o);
+  }
+}
+
+template <typename T, int W, bool VEC>
+__global__ __launch_bounds__(256) void conv_cf_bwd_k(const T* __restrict__ x, int64_t sxb, int64_t sxd,
+                                                     const float* __restrict__ w, const float* __restrict__ bias,
+                                                     const T* __restrict__ dout, int64_t sgb, int64_t sgd,
+                                                     T* __restrict__ dx, int64_t sdb, int64_t sdd,
+                                                     float* __restrict__ part, int Bn, int Dn, int L, bool silu) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= (int64_t)Bn * Dn) return;
+  const int b = (int)(row / Dn), d = (int)(row % Dn);
+  const T* xr = x + b * sxb + d * sxd;
+  const T* gr = dout + b * sgb + d * sgd;
+  T* dxr = dx + b * sdb + d * sdd;
+  float wk[W];
+#pragma unroll
+  for (int k = 0; k < W; ++k) wk[k] = w[d * W + k];
+  const float bs = bias ? bias[d] : 0.f;
+  float accw[W], accb = 0.f;
+#pragma unroll
+  for (int k = 0; k < W; ++k) accw[k] = 0.f;
+  float nextd[3] = {0.f, 0.f, 0.f};  // dpre[t_end .. t_end+2] of the chunk after this one
+  const int nchunks = (L + 511) / 512;
+  for (int ci = nchunks - 1; ci >= 0; --ci) {
+    const int c0 = ci * 512;
+    const int t0 = c0 + lane * 8;
+    float cur[8], g[8];
+    load_run<T, VEC>(xr + t0, t0, L, cur);
+    load_run<T, VEC>(gr + t0, t0, L, g);
+    float prev[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) prev[j] = __shfl_up(cur[5 + j], 1, 64);
+    if (lane == 0) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) prev[j] = (t0 - 3 + j >= 0) ? ld(xr + t0 - 3 + j) : 0.f;
+    }
+    float win[11];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) win[j] = prev[j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) win[3 + j] = cur[j];
+    float dp[11];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float a = bs;
+#pragma unroll
+      for (int k = 0; k < W; ++k) a += wk[k] * win[3 + j - (W - 1) + k];
+      dp[j] = (t0 + j < L) ? act_bwd(a, g[j], silu) : 0.f;
+    }
+    // dpre of the next 3 steps: from lane+1, lane 63 from the carried next chunk
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      float v = __shfl_down(dp[j], 1, 64);
+      dp[8 + j] = lane == 63 ? nextd[j] : v;
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) nextd[j] = __shfl(dp[j], 0, 64);
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < W; ++k) s += wk[k] * dp[j + (W - 1) - k];
+      o[j] = s;
+#pragma unroll
+      for (int k = 0; k < W; ++k) accw[k] += dp[j] * win[3 + j - (W - 1) + k];
+      accb += dp[j];
+    }
+    if (t0 < L) store_run<T, VEC>(dxr + t0, t0, L, o);
+  }
+#pragma unroll
+  for (int k = 0; k < W; ++k) accw[k] = wave_sum(accw[k]);
+  accb = wave_sum(accb);
+  if (lane == 0) {
+    float* pr = part + row * (W + 1);
+#pragma unroll
+    for (int k = 0; k < W; ++k) pr[k] = accw[k];
+    pr[W] = accb;
+  }
+}
+
+// part: (B, D, W+1) -> dw (D, W), db (D): sum over batch in fixed order
+__global__ void conv_reduce_batch_k(const float* __restrict__ part, int Bn, int Dn, int W, float* __restrict__ dw,
+                                    float* __restrict__ db) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // over D*(W+1)
+  if (i >= Dn * (W + 1)) return;
+  float s = 0.f;
+  for (int b = 0; b < Bn; ++b) s += part[(int64_t)b * Dn * (W + 1) + i];
+  const int d = i / (W + 1), k = i % (W + 1);
+  if (k < W) dw[d * W + k] = s;
+  else if (db) db[d] = s;
+}
+
+// =========================== channel-last ================================================
+constexpr int CL_T = 16;  // timesteps per wave tile
+
+template <typename T, int W, bool VEC>
+__global__ __launch_bounds__(256) void conv_cl_fwd_k(const T* __restrict__ x, int64_t sxb, int64_t sxl,
+                                                     const float* __restrict__ w, const float* __restrict__ bias,
+                                                     T* __restrict__ out, int64_t sob, int64_t sol, int Bn, int L,
+                                                     int C, bool silu) {
+  // grid: x = channel groups of 512, y = time tiles (4 per block), z = batch
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = (blockIdx.x * 64 + lane) * 8;
+  const int t0 = (blockIdx.y * 4 + wave) * CL_T;
+  const int b = blockIdx.z;
+  if (c >= C || t0 >= L) return;
+  const int nc = min(8, C - c);
+  float wk[W][8], bs[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int cc = j < nc ? c + j : c;
+#pragma unroll
+    for (int k = 0; k < W; ++k) wk[k][j] = w[cc * W + k];
+    bs[j] = bias ? bias[cc] : 0.f;
+  }
+  const T* xb = x + b * sxb + c;
+  T* ob = out + b * sob + c;
+  auto loadrow = [&](int t, float (&o)[8]) {
+    if (t < 0 || t >= L) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = 0.f;
+    } else if (VEC && nc == 8) {
+      Vec8<T>::load(xb + t * sxl, o);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = j < nc ? ld(xb + t * sxl + j) : 0.f;
+    }
+  };
+  float win[W][8];
+#pragma unroll
+  for (int k = 0; k < W - 1; ++k) loadrow(t0 - (W - 1) + k, win[k]);
+  for (int t = t0; t < min(t0 + CL_T, L); ++t) {
+    loadrow(t, win[W - 1]);
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float a = bs[j];
+#pragma unroll
+      for (int k = 0; k < W; ++k) a += wk[k][j] * win[k][j];
+      o[j] = act_fwd(a, silu);
+    }
+    if (VEC && nc == 8) {
+      Vec8<T>::store(ob + t * sol, o);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (j < nc) st(ob + t * sol + j, o[j]);
+    }
+#pragma unroll
+    for (int k = 0; k < W - 1; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) win[k][j] = win[k + 1][j];
+  }
+}
+
+constexpr int CLB_T = 32;  // backward time tile per wave
+
+template <typename T, int W, bool VEC>
+__global__ __launch_bounds__(256) void conv_cl_bwd_k(const T* __restrict__ x, int64_t sxb, int64_t sxl,
+                                                     const float* __restrict__ w, const float* __restrict__ bias,
+                                                     const T* __restrict__ dout, int64_t sgb, int64_t sgl,
+                                                     T* __restrict__ dx, int64_t sdb, int64_t sdl,
+                                                     float* __restrict__ part, int Bn, int L, int C, bool silu) {
+  __shared__ float red[4][64 * 8 * (W + 1)];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = (blockIdx.x * 64 + lane) * 8;
+  const int t0 = (blockIdx.y * 4 + wave) * CLB_T;
+  const int b = blockIdx.z;
+  float acc[W + 1][8];
+#pragma unroll
+  for (int k = 0; k < W + 1; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[k][j] = 0.f;
+  if (c < C && t0 < L) {
+    const int nc = min(8, C - c);
+    float wk[W][8], bs[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int cc = j < nc ? c + j : c;
+#pragma unroll
+      for (int k = 0; k < W; ++k) wk[k][j] = w[cc * W + k];
+      bs[j] = bias ? bias[cc] : 0.f;
+    }
+    const T* xb = x + b * sxb + c;
+    const T* gb = dout + b * sgb + c;
+    T* db_ = dx + b * sdb + c;
+    auto loadv = [&](const T* base, int64_t stride, int t, float (&o)[8]) {
+      if (t < 0 || t >= L) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = 0.f;
+      } else if (VEC && nc == 8) {
+        Vec8<T>::load(base + t * stride, o);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = j < nc ? ld(base + t * stride + j) : 0.f;
+      }
+    };
+    float xw[W][8];   // x[t-W+1 .. t]
+    float dpw[W][8];  // dpre[t-W+1 .. t]
+#pragma unroll
+    for (int k = 0; k < W - 1; ++k) {
+      loadv(xb, sxl, t0 - (W - 1) + k, xw[k]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dpw[k][j] = 0.f;
+    }
+    const int tend = min(t0 + CLB_T, L);
+    for (int t = t0; t < tend + W - 1; ++t) {
+      loadv(xb, sxl, t, xw[W - 1]);
+      float g[8];
+      loadv(gb, sgl, t, g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float a = bs[j];
+#pragma unroll
+        for (int k = 0; k < W; ++k) a += wk[k][j] * xw[k][j];
+        dpw[W - 1][j] = (t < L) ? act_bwd(a, g[j], silu) : 0.f;
+      }
+      if (t < tend) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+#pragma unroll
+          for (int k = 0; k < W; ++k) acc[k][j] += dpw[W - 1][j] * xw[k][j];
+          acc[W][j] += dpw[W - 1][j];
+        }
+      }
+      const int s = t - (W - 1);
+      if (s >= t0) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float v = 0.f;
+#pragma unroll
+          for (int k = 0; k < W; ++k) v += wk[k][j] * dpw[W - 1 - k][j];
+          o[j] = v;
+        }
+        if (VEC && nc == 8) {
+          Vec8<T>::store(db_ + s * sdl, o);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (j < nc) st(db_ + s * sdl + j, o[j]);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < W - 1; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xw[k][j] = xw[k + 1][j];
+          dpw[k][j] = dpw[k + 1][j];
+        }
+    }
+  }
+  // block reduction over the 4 time tiles, then one partial row per block
+#pragma unroll
+  for (int k = 0; k < W + 1; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[wave][(lane * 8 + j) * (W + 1) + k] = acc[k][j];
+  __syncthreads();
+  const int64_t prow = (int64_t)blockIdx.z * gridDim.y + blockIdx.y;
+  for (int i = threadIdx.x; i < 64 * 8 * (W + 1); i += 256) {
+    const int ch = blockIdx.x * 512 + i / (W + 1);
+    if (ch < C) part[prow * (int64_t)C * (W + 1) + (int64_t)ch * (W + 1) + i % (W + 1)] =
+        red[0][i] + red[1][i] + red[2][i] + red[3][i];
+  }
+}
+
+// =========================== decode update ===============================================
+template <typename T, int W>
+__global__ void conv_update_k(const T* __restrict__ x, int64_t sxb, T* __restrict__ state, int64_t ssb,
+                              int64_t ssc, const float* __restrict__ w, const float* __restrict__ bias,
+                              T* __restrict__ out, int Bn, int C, bool silu) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= Bn * C) return;
+  const int b = i / C, c = i % C;
+  T* sp = state + b * ssb + c * ssc;
+  float win[W];
+#pragma unroll
+  for (int k = 0; k < W - 1; ++k) win[k] = ld(sp + k);
+  win[W - 1] = ld(x + b * sxb + c);
+  float a = bias ? bias[c] : 0.f;
+#pragma unroll
+  for (int k = 0; k < W; ++k) a += w[c * W + k] * win[k];
+#pragma unroll
+  for (int k = 0; k < W - 1; ++k) st(sp + k, win[k + 1]);
+  st(out + (int64_t)b * C + c, act_fwd(a, silu));
+}
+
+// =========================== launchers ===================================================
+#define W_SWITCH(Wv, ...)                                         \
+  do {                                                            \
+    if ((Wv) == 2) { constexpr int WW = 2; __VA_ARGS__; }         \
+    else if ((Wv) == 3) { constexpr int WW = 3; __VA_ARGS__; }    \
+    else if ((Wv) == 4) { constexpr int WW = 4; __VA_ARGS__; }    \
+    else return hipErrorInvalidValue;                             \
+  } while (0)
+
+template <typename T>
+static hipError_t cf_fwd(const T* x, int64_t sxb, int64_t sxd, const float* w, const float* bias, T* out,
+                         int64_t sob, int64_t sod, int Bn, int Dn, int L, int Wd, bool silu, hipStream_t st) {
+  const bool vec = (L % 8 == 0) && (sxb % 8 == 0) && (sxd % 8 == 0) && (sob % 8 == 0) && (sod % 8 == 0) &&
+                   ((uintptr_t)x % 16 == 0) && ((uintptr_t)out % 16 == 0);
+  dim3 grid((unsigned)(((int64_t)Bn * Dn + 3) / 4)), block(256);
+  W_SWITCH(Wd, {
+    if (vec) hipLaunchKernelGGL((conv_cf_fwd_k<T, WW, true>), grid, block, 0, st, x, sxb, sxd, w, bias, out, sob,
+                                sod, Bn, Dn, L, silu);
+    else hipLaunchKernelGGL((conv_cf_fwd_k<T, WW, false>), grid, block, 0, st, x, sxb, sxd, w, bias, out, sob, sod,
+                            Bn, Dn, L, silu);
+  });
+  return hipGetLastError();
+}
+
+hipError_t launch_conv_cf_fwd(const void* x, int dt, int64_t sxb, int64_t sxd, const float* w, const float* bias,
+                              void* out, int64_t sob, int64_t sod, int Bn, int Dn, int L, int Wd, bool silu,
+                              hipStream_t st) {
+  if (dt == kBF16)
+    return cf_fwd<bf16_t>((const bf16_t*)x, sxb, sxd, w, bias, (bf16_t*)out, sob, sod, Bn, Dn, L, Wd, silu, st);
+  if (dt == kF32)
+    return cf_fwd<float>((const float*)x, sxb, sxd, w, bias, (float*)out, sob, sod, Bn, Dn, L, Wd, silu, st);
+  return hipErrorInvalidValue;
+}
+
+template <typename T>
+static hipError_t cf_bwd(const T* x, int64_t sxb, int64_t sxd, const float* w, const float* bias, const T* g,
+                         int64_t sgb, int64_t sgd, T* dx, int64_t sdb, int64_t sdd, float* part, float* dw, float* db,
+                         int Bn, int Dn, int L, int Wd, bool silu, hipStream_t st) {
+  const bool vec = (L % 8 == 0) && (sxb % 8 == 0) && (sxd % 8 == 0) && (sgb % 8 == 0) && (sgd % 8 == 0) &&
+                   (sdb % 8 == 0) && (sdd % 8 == 0) && ((uintptr_t)x % 16 == 0) && ((uintptr_t)g % 16 == 0) &&
+                   ((uintptr_t)dx % 16 == 0);
+  dim3 grid((unsigned)(((int64_t)Bn * Dn + 3) / 4)), block(256);
+  W_SWITCH(Wd, {
+    if (vec) hipLaunchKernelGGL((conv_cf_bwd_k<T, WW, true>), grid, block, 0, st, x, sxb, sxd, w, bias, g, sgb, sgd,
+                                dx, sdb, sdd, part, Bn, Dn, L, silu);
+    else hipLaunchKernelGGL((conv_cf_bwd_k<T, WW, false>), grid, block, 0, st, x, sxb, sxd, w, bias, g, sgb, sgd, dx,
+                            sdb, sdd, part, Bn, Dn, L, silu);
+  });
+  MAMBA_HIP_CHECK(hipGetLastError());
+  const int n = Dn * (Wd + 1);
+  hipLaunchKernelGGL(conv_reduce_batch_k, dim3((n + 255) / 256), dim3(256), 0, st, part, Bn, Dn, Wd, dw, db);
+  return hipGetLastError();
+}
+
+hipError_t launch_conv_cf_bwd(const void* x, int dt, int64_t sxb, int64_t sxd, const float* w, const float* bias,
+                              const void* g, int64_t sgb, int64_t sgd, void* dx, int64_t sdb, int64_t sdd,
+                              float* part, float* dw, float* db, int Bn, int Dn, int L, int Wd, bool silu,
+                              hipStream_t st) {
+  if (dt == kBF16)
+    return cf_bwd<bf16_t>((const bf16_t*)x, sxb, sxd, w, bias, (const bf16_t*)g, sgb, sgd, (bf16_t*)dx, sdb, sdd,
+                          part, dw, db, Bn, Dn, L, Wd, silu, st);
+  if (dt == kF32)
+    return cf_bwd<float>((const float*)x, sxb, sxd, w, bias, (const float*)g, sgb, sgd, (float*)dx, sdb, sdd, part,
+                         dw, db, Bn, Dn, L, Wd, silu, st);
+  return hipErrorInvalidValue;
+}
+
+template <typename T>
+static hipError_t cl_fwd(const T* x, int64_t sxb, int64_t sxl, const float* w, const float* bias, T* out,
+                         int64_t sob, int64_t sol, int Bn, int L, int C, int Wd, bool silu, hipStream_t st) {
+  const bool vec = (C % 8 == 0) && (sxb % 8 == 0) && (sxl % 8 == 0) && (sob % 8 == 0) && (sol % 8 == 0) &&
+                   ((uintptr_t)x % 16 == 0) && ((uintptr_t)out % 16 == 0);
+  dim3 grid((C + 511) / 512, (L + 4 * CL_T - 1) / (4 * CL_T), Bn), block(256);
+  W_SWITCH(Wd, {
+    if (vec) hipLaunchKernelGGL((conv_cl_fwd_k<T, WW, true>), grid, block, 0, st, x, sxb, sxl, w, bias, out, sob,
+                                sol, Bn, L, C, silu);
+    else hipLaunchKernelGGL((conv_cl_fwd_k<T, WW, false>), grid, block, 0, st, x, sxb, sxl, w, bias, out, sob, sol,
+                            Bn, L, C, silu);
+  });
+  return hipGetLastError();
+}
+
+hipError_t launch_conv_cl_fwd(const void* x, int dt, int64_t sxb, int64_t sxl, const float* w, const float* bias,
+                              void* out, int64_t sob, int64_t sol, int Bn, int L, int C, int Wd, bool silu,
+                              hipStream_t st) {
+  if (dt == kBF16)
+    return cl_fwd<bf16_t>((const bf16_t*)x, sxb, sxl, w, bias, (bf16_t*)out, sob, sol, Bn, L, C, Wd, silu, st);
+  if (dt == kF32)
+    return cl_fwd<float>((const float*)x, sxb, sxl, w, bias, (float*)out, sob, sol, Bn, L, C, Wd, silu, st);
+  return hipErrorInvalidValue;
+}
+
+int conv_cl_bwd_partial_rows(int Bn, int L) { return Bn * ((L + 4 * CLB_T - 1) / (4 * CLB_T)); }
+
+__global__ void conv_reduce_rows_k(const float* __restrict__ part, int nrows, int C, int W, float* __restrict__ dw,
+                                   float* __restrict__ db) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // over C*(W+1)
+  if (i >= C * (W + 1)) return;
+  float s = 0.f;
+  for (int r = 0; r < nrows; ++r) s += part[(int64_t)r * C * (W + 1) + i];
+  const int c = i / (W + 1), k = i % (W + 1);
+  if (k < W) dw[c * W + k] = s;
+  else if (db) db[c] = s;
+}
+
+template <typename T>
+static hipError_t cl_bwd(const T* x, int64_t sxb, int64_t sxl, const float* w, const float* bias, const T* g,
+                         int64_t sgb, int64_t sgl, T* dx, int64_t sdb, int64_t sdl, float* part, float* dw, float* db,
+                         int Bn, int L, int C, int Wd, bool silu, hipStream_t st) {
+  const bool vec = (C % 8 == 0) && (sxb % 8 == 0) && (sxl % 8 == 0) && (sgb % 8 == 0) && (sgl % 8 == 0) &&
+                   (sdb % 8 == 0) && (sdl % 8 == 0) && ((uintptr_t)x % 16 == 0) && ((uintptr_t)g % 16 == 0) &&
+                   ((uintptr_t)dx % 16 == 0);
+  dim3 grid((C + 511) / 512, (L + 4 * CLB_T - 1) / (4 * CLB_T), Bn), block(256);
+  W_SWITCH(Wd, {
+    if (vec) hipLaunchKernelGGL((conv_cl_bwd_k<T, WW, true>), grid, block, 0, st, x, sxb, sxl, w, bias, g, sgb, sgl,
+                                dx, sdb, sdl, part, Bn, L, C, silu);
+    else hipLaunchKernelGGL((conv_cl_bwd_k<T, WW, false>), grid, block, 0, st, x, sxb, sxl, w, bias, g, sgb, sgl, dx,
+                            sdb, sdl, part, Bn, L, C, silu);
+  });
+  MAMBA_HIP_CHECK(hipGetLastError());
+  const int n = C * (Wd + 1);
+  hipLaunchKernelGGL(conv_reduce_rows_k, dim3((n + 255) / 256), dim3(256), 0, st, part,
+                     conv_cl_bwd_partial_rows(Bn, L), C, Wd, dw, db);
+  return hipGetLastError();
+}
+
+hipError_t launch_conv_cl_bwd(const void* x, int dt, int64_t sxb, int64_t sxl, const float* w, const float* bias,
+                              const void* g, int64_t sgb, int64_t sgl, void* dx, int64_t sdb, int64_t sdl,
+                              float* part, float* dw, float* db, int Bn, int L, int C, int Wd, bool silu,
+                              hipStream_t st) {
+  if (dt == kBF16)
+    return cl_bwd<bf16_t>((const bf16_t*)x, sxb, sxl, w, bias, (const bf16_t*)g, sgb, sgl, (bf16_t*)dx, sdb, sdl,
+                          part, dw, db, Bn, L, C, Wd, silu, st);
+  if (dt == kF32)
+    return cl_bwd<float>((const float*)x, sxb, sxl, w, bias, (const float*)g, sgb, sgl, (float*)dx, sdb, sdl, part,
+                         dw, db, Bn, L, C, Wd, silu, st);
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_conv_update(const void* x, int dt, int64_t sxb, void* state, int64_t ssb, int64_t ssc,
+                              const float* w, const float* bias, void* out, int Bn, int C, int Wd, bool silu,
+                              hipStream_t st) {
+  const int n = Bn * C;
+  dim3 grid((n + 255) / 256), block(256);
+  if (dt == kBF16) {
+    W_SWITCH(Wd, hipLaunchKernelGGL((conv_update_k<bf16_t, WW>), grid, block, 0, st, (const bf16_t*)x, sxb,
+                                    (bf16_t*)state, ssb, ssc, w, bias, (bf16_t*)out, Bn, C, silu));
+  } else if (dt == kF32) {
+    W_SWITCH(Wd, hipLaunchKernelGGL((conv_update_k<float, WW>), grid, block, 0, st, (const float*)x, sxb,
+                                    (float*)state, ssb, ssc, w, bias, (float*)out, Bn, C, silu));
+  } else {
+    return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace mamba_amd

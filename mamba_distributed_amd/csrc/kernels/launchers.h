@@ -1,0 +1,52 @@
+// Host-side launchers exported by kernels/*.hip (pure HIP; no torch types) and called by
+// ../bindings.cpp.  All take raw device pointers + element strides + the caller's stream,
+// never allocate and never synchronise (graph-capturable).  dtype codes: see common.h DType.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mamba_amd {
+
+// ---- norm.hip -------------------------------------------------------------------------------
+hipError_t launch_add_rmsnorm_fwd(const void* x, int xdt, int64_t sx, const void* res, int rdt, int64_t sr,
+                                  const float* w, void* y, int ydt, void* ro, int rodt, float* rstd, int64_t M,
+                                  int D, float eps, hipStream_t st);
+int add_rmsnorm_bwd_partial_rows(int64_t M);
+hipError_t launch_add_rmsnorm_bwd(const void* dy, int ydt, const void* dro, int drodt, const void* ro, int rodt,
+                                  const float* w, const float* rstd, void* dx, int xdt, void* dres, int rdt,
+                                  float* part, float* dw, int64_t M, int D, hipStream_t st);
+hipError_t launch_gated_rmsnorm_fwd(const void* x, int xdt, int64_t sx, const void* z, int zdt, int64_t sz,
+                                    const float* w, void* y, int ydt, float* rstd, int64_t M, int D, int G,
+                                    float eps, bool nbg, hipStream_t st);
+int norm_bwd_partial_rows(int64_t M);
+hipError_t launch_gated_rmsnorm_bwd(const void* dy, int ydt, const void* x, int xdt, int64_t sx, const void* z,
+                                    int zdt, int64_t sz, const float* w, const float* rstd, void* dx, int64_t sdx,
+                                    void* dz, int64_t sdz, float* part, float* dw, int64_t M, int D, int G,
+                                    bool nbg, hipStream_t st);
+
+// ---- cross_entropy.hip ------------------------------------------------------------------------
+hipError_t launch_ce_fwd(const void* logits, int dt, int64_t ld, const int64_t* tgt, int64_t M, int V,
+                         int64_t ignore_index, const float* scale, float* loss, void* grad, int64_t ldg,
+                         hipStream_t st);
+
+// ---- conv1d.hip ---------------------------------------------------------------------------------
+hipError_t launch_conv_cf_fwd(const void* x, int dt, int64_t sxb, int64_t sxd, const float* w, const float* bias,
+                              void* out, int64_t sob, int64_t sod, int Bn, int Dn, int L, int Wd, bool silu,
+                              hipStream_t st);
+hipError_t launch_conv_cf_bwd(const void* x, int dt, int64_t sxb, int64_t sxd, const float* w, const float* bias,
+                              const void* g, int64_t sgb, int64_t sgd, void* dx, int64_t sdb, int64_t sdd,
+                              float* part, float* dw, float* db, int Bn, int Dn, int L, int Wd, bool silu,
+                              hipStream_t st);
+hipError_t launch_conv_cl_fwd(const void* x, int dt, int64_t sxb, int64_t sxl, const float* w, const float* bias,
+                              void* out, int64_t sob, int64_t sol, int Bn, int L, int C, int Wd, bool silu,
+                              hipStream_t st);
+int conv_cl_bwd_partial_rows(int Bn, int L);
+hipError_t launch_conv_cl_bwd(const void* x, int dt, int64_t sxb, int64_t sxl, const float* w, const float* bias,
+                              const void* g, int64_t sgb, int64_t sgl, void* dx, int64_t sdb, int64_t sdl,
+                              float* part, float* dw, float* db, int Bn, int L, int C, int Wd, bool silu,
+                              hipStream_t st);
+hipError_t launch_conv_update(const void* x, int dt, int64_t sxb, void* state, int64_t ssb, int64_t ssc,
+                              const float* w, const float* bias, void* out, int Bn, int C, int Wd, bool silu,
+                              hipStream_t st);
+
+}  // namespace mamba_amd

@@ -1,0 +1,385 @@
+// Fused residual-add + RMSNorm and gated RMSNorm, forward and backward, for gfx950.
+//
+// Design (memory-bound; the roofline is HBM bytes):
+//  * one wavefront per row, 4 rows per 256-thread block; each lane owns NCH chunks of 4
+//    consecutive columns (col = 4*(lane + 64*c)), loaded as one 8-B (bf16) / 16-B (f32) vector,
+//    so a wave instruction covers 512 B / 1 KiB of contiguous row -> fully coalesced.
+//  * statistics in fp32, one wave_sum per row (no LDS, no barriers on the row path).
+//  * the row stays in registers between the statistics pass and the output pass: HBM sees
+//    each input byte once and each output byte once.
+//  * weight gradients: each wave accumulates its rows' dy*xhat in registers over a
+//    grid-stride loop, the 4 waves of a block are summed through LDS, and one row of partials
+//    per block is written; a second kernel sums the partials column-wise in a fixed order
+//    (bitwise deterministic, no float atomics).
+// Reference semantics: upstream ops/triton/layer_norm.py and layernorm_gated.py.
+#include "common.h"
+#include "launchers.h"
+
+namespace mamba_amd {
+
+__device__ __forceinline__ void ld4_dyn(const void* p, int dt, int64_t i, float (&o)[4]) {
+  if (dt == kF32) ld4<float>(reinterpret_cast<const float*>(p) + i, o);
+  else ld4<bf16_t>(reinterpret_cast<const bf16_t*>(p) + i, o);
+}
+__device__ __forceinline__ void st4_dyn(void* p, int dt, int64_t i, const float (&o)[4]) {
+  if (dt == kF32) st4<float>(reinterpret_cast<float*>(p) + i, o);
+  else st4<bf16_t>(reinterpret_cast<bf16_t*>(p) + i, o);
+}
+
+// ------------------------------------------------------------------------------------------
+template <int NCH>
+__global__ __launch_bounds__(256) void add_rmsnorm_fwd_k(
+    const void* __restrict__ x, int xdt, int64_t sx, const void* __restrict__ res, int rdt, int64_t sr,
+    const float* __restrict__ w, void* __restrict__ y, int ydt, void* __restrict__ ro, int rodt,
+    float* __restrict__ rstd, int64_t M, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  float v[NCH][4];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = (lane + 64 * c) * 4;
+    if (col < D) {
+      ld4_dyn(x, xdt, row * sx + col, v[c]);
+      if (res) {
+        float r[4];
+        ld4_dyn(res, rdt, row * sr + col, r);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[c][k] += r[k];
+      }
+      st4_dyn(ro, rodt, row * D + col, v[c]);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ss += v[c][k] * v[c][k];
+    }
+  }
+  ss = wave_sum(ss);
+  const float rs = rsqrtf(ss / (float)D + eps);
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = (lane + 64 * c) * 4;
+    if (col < D) {
+      float wv[4], o[4];
+      ld4<float>(w + col, wv);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = v[c][k] * rs * wv[k];
+      st4_dyn(y, ydt, row * D + col, o);
+    }
+  }
+  if (lane == 0) rstd[row] = rs;
+}
+
+// block-level partial reduction of per-wave dw accumulators -> part[blockIdx.x][D]
+template <int NCH>
+__device__ __forceinline__ void block_dw_partial(float (&acc)[NCH][4], float* part, int D, float* lds) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = (lane + 64 * c) * 4;
+    if (col < D) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) lds[wave * D + col + k] = acc[c][k];
+    }
+  }
+  __syncthreads();
+  for (int col = threadIdx.x; col < D; col += blockDim.x) {
+    part[(int64_t)blockIdx.x * D + col] = lds[col] + lds[D + col] + lds[2 * D + col] + lds[3 * D + col];
+  }
+}
+
+template <int NCH>
+__global__ __launch_bounds__(256) void add_rmsnorm_bwd_k(
+    const void* __restrict__ dy, int ydt, const void* __restrict__ dro, int drodt,
+    const void* __restrict__ ro, int rodt, const float* __restrict__ w, const float* __restrict__ rstd,
+    void* __restrict__ dx, int xdt, void* __restrict__ dres, int rdt, float* __restrict__ part,
+    int64_t M, int D) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int lane = threadIdx.x & 63;
+  float acc[NCH][4];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[c][k] = 0.f;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < M; row += (int64_t)gridDim.x * 4) {
+    const float rs = rstd[row];
+    float xh[NCH][4], dyw[NCH][4];
+    float dot = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = (lane + 64 * c) * 4;
+      if (col < D) {
+        float r[4], g[4], wv[4];
+        ld4_dyn(ro, rodt, row * D + col, r);
+        ld4_dyn(dy, ydt, row * D + col, g);
+        ld4<float>(w + col, wv);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          xh[c][k] = r[k] * rs;
+          dyw[c][k] = g[k] * wv[k];
+          dot += dyw[c][k] * xh[c][k];
+          acc[c][k] += g[k] * xh[c][k];
+        }
+      }
+    }
+    dot = wave_sum(dot) / (float)D;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = (lane + 64 * c) * 4;
+      if (col < D) {
+        float o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = (dyw[c][k] - xh[c][k] * dot) * rs;
+        if (dro) {
+          float d2[4];
+          ld4_dyn(dro, drodt, row * D + col, d2);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) o[k] += d2[k];
+        }
+        st4_dyn(dx, xdt, row * D + col, o);
+        if (dres) st4_dyn(dres, rdt, row * D + col, o);
+      }
+    }
+  }
+  block_dw_partial<NCH>(acc, part, D, lds);
+}
+
+__global__ __launch_bounds__(256) void sum_rows_k(const float* __restrict__ part, int nrows, int D,
+                                                  float* __restrict__ out) {
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= D) return;
+  float s = 0.f;
+  for (int r = 0; r < nrows; ++r) s += part[(int64_t)r * D + col];
+  out[col] = s;
+}
+
+// ------------------------------------------------------------------------------------------
+// gated RMSNorm: y = RMSNorm_group(x * silu(z)) * w   (NBG = norm_before_gate=false)
+//                y = RMSNorm_group(x) * w * silu(z)    (NBG = true)
+template <int NCH, bool NBG>
+__global__ __launch_bounds__(256) void gated_rmsnorm_fwd_k(
+    const void* __restrict__ x, int xdt, int64_t sx, const void* __restrict__ z, int zdt, int64_t sz,
+    const float* __restrict__ w, void* __restrict__ y, int ydt, float* __restrict__ rstd, int64_t M, int D,
+    int G, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int ngroups = D / G;
+  float v[NCH][4], sz4[NCH][4], sq[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = (lane + 64 * c) * 4;
+    sq[c] = 0.f;
+    if (col < D) {
+      float zz[4];
+      ld4_dyn(x, xdt, row * sx + col, v[c]);
+      ld4_dyn(z, zdt, row * sz + col, zz);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        sz4[c][k] = siluf_(zz[k]);
+        if (!NBG) v[c][k] *= sz4[c][k];
+        sq[c] += v[c][k] * v[c][k];
+      }
+    }
+  }
+  float rsc[NCH];
+  for (int g = 0; g < ngroups; ++g) {
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = (lane + 64 * c) * 4;
+      if (col < D && col / G == g) s += sq[c];
+    }
+    s = wave_sum(s);
+    const float rs = rsqrtf(s / (float)G + eps);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = (lane + 64 * c) * 4;
+      if (col / G == g) rsc[c] = rs;
+    }
+    if (lane == 0) rstd[row * ngroups + g] = rs;
+  }
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = (lane + 64 * c) * 4;
+    if (col < D) {
+      float wv[4], o[4];
+      ld4<float>(w + col, wv);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        o[k] = v[c][k] * rsc[c] * wv[k];
+        if (NBG) o[k] *= sz4[c][k];
+      }
+      st4_dyn(y, ydt, row * D + col, o);
+    }
+  }
+}
+
+template <int NCH, bool NBG>
+__global__ __launch_bounds__(256) void gated_rmsnorm_bwd_k(
+    const void* __restrict__ dy, int ydt, const void* __restrict__ x, int xdt, int64_t sx,
+    const void* __restrict__ z, int zdt, int64_t sz, const float* __restrict__ w,
+    const float* __restrict__ rstd, void* __restrict__ dx, int64_t sdx, void* __restrict__ dz, int64_t sdz,
+    float* __restrict__ part, int64_t M, int D, int G) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int lane = threadIdx.x & 63;
+  const int ngroups = D / G;
+  float acc[NCH][4];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[c][k] = 0.f;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < M; row += (int64_t)gridDim.x * 4) {
+    float xv[NCH][4], zv[NCH][4], dyw[NCH][4], xh[NCH][4], rsc[NCH], dotc[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = (lane + 64 * c) * 4;
+      rsc[c] = 0.f;
+      dotc[c] = 0.f;
+      if (col < D) {
+        float g[4], wv[4];
+        ld4_dyn(x, xdt, row * sx + col, xv[c]);
+        ld4_dyn(z, zdt, row * sz + col, zv[c]);
+        ld4_dyn(dy, ydt, row * D + col, g);
+        ld4<float>(w + col, wv);
+        rsc[c] = rstd[row * ngroups + col / G];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float s = siluf_(zv[c][k]);
+          const float base = NBG ? xv[c][k] : xv[c][k] * s;
+          xh[c][k] = base * rsc[c];
+          const float dyn = NBG ? g[k] * s : g[k];
+          dyw[c][k] = dyn * wv[k];
+          dotc[c] += dyw[c][k] * xh[c][k];
+          acc[c][k] += dyn * xh[c][k];
+        }
+      }
+    }
+    float dotg[NCH];
+    for (int gi = 0; gi < ngroups; ++gi) {
+      float s = 0.f;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const int col = (lane + 64 * c) * 4;
+        if (col < D && col / G == gi) s += dotc[c];
+      }
+      s = wave_sum(s) / (float)G;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const int col = (lane + 64 * c) * 4;
+        if (col / G == gi) dotg[c] = s;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = (lane + 64 * c) * 4;
+      if (col < D) {
+        float ox[4], oz[4], g[4], wv[4];
+        if (NBG) {
+          ld4_dyn(dy, ydt, row * D + col, g);
+          ld4<float>(w + col, wv);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float sg = sigmoidf_(zv[c][k]);
+          const float s = zv[c][k] * sg;
+          const float dsilu = sg * (1.f + zv[c][k] * (1.f - sg));
+          const float dbase = (dyw[c][k] - xh[c][k] * dotg[c]) * rsc[c];
+          if (NBG) {
+            ox[k] = dbase;
+            oz[k] = g[k] * xh[c][k] * wv[k] * dsilu;
+          } else {
+            ox[k] = dbase * s;
+            oz[k] = dbase * xv[c][k] * dsilu;
+          }
+        }
+        st4_dyn(dx, xdt, row * sdx + col, ox);
+        st4_dyn(dz, zdt, row * sdz + col, oz);
+      }
+    }
+  }
+  block_dw_partial<NCH>(acc, part, D, lds);
+}
+
+// ------------------------------------------------------------------------------------------
+// host launchers
+#define NCH_SWITCH(D, ...)                                               \
+  do {                                                                   \
+    int _nch = ((D) + 255) / 256;                                        \
+    if (_nch <= 1) { constexpr int NCH = 1; __VA_ARGS__; }               \
+    else if (_nch <= 2) { constexpr int NCH = 2; __VA_ARGS__; }          \
+    else if (_nch <= 3) { constexpr int NCH = 3; __VA_ARGS__; }          \
+    else if (_nch <= 4) { constexpr int NCH = 4; __VA_ARGS__; }          \
+    else if (_nch <= 6) { constexpr int NCH = 6; __VA_ARGS__; }          \
+    else if (_nch <= 8) { constexpr int NCH = 8; __VA_ARGS__; }          \
+    else if (_nch <= 10) { constexpr int NCH = 10; __VA_ARGS__; }        \
+    else if (_nch <= 12) { constexpr int NCH = 12; __VA_ARGS__; }        \
+    else if (_nch <= 16) { constexpr int NCH = 16; __VA_ARGS__; }        \
+    else if (_nch <= 20) { constexpr int NCH = 20; __VA_ARGS__; }        \
+    else return hipErrorInvalidValue;                                    \
+  } while (0)
+
+static int bwd_grid(int64_t M) {
+  int64_t g = (M + 3) / 4;
+  return (int)(g < 1024 ? (g < 1 ? 1 : g) : 1024);
+}
+
+hipError_t launch_add_rmsnorm_fwd(const void* x, int xdt, int64_t sx, const void* res, int rdt, int64_t sr,
+                                  const float* w, void* y, int ydt, void* ro, int rodt, float* rstd, int64_t M,
+                                  int D, float eps, hipStream_t st) {
+  if (M == 0) return hipSuccess;
+  dim3 grid((unsigned)((M + 3) / 4)), block(256);
+  NCH_SWITCH(D, hipLaunchKernelGGL((add_rmsnorm_fwd_k<NCH>), grid, block, 0, st, x, xdt, sx, res, rdt, sr, w, y,
+                                   ydt, ro, rodt, rstd, M, D, eps));
+  return hipGetLastError();
+}
+
+int add_rmsnorm_bwd_partial_rows(int64_t M) { return bwd_grid(M); }
+
+hipError_t launch_add_rmsnorm_bwd(const void* dy, int ydt, const void* dro, int drodt, const void* ro, int rodt,
+                                  const float* w, const float* rstd, void* dx, int xdt, void* dres, int rdt,
+                                  float* part, float* dw, int64_t M, int D, hipStream_t st) {
+  const int g = bwd_grid(M);
+  const size_t lds = 4 * (size_t)D * sizeof(float);
+  NCH_SWITCH(D, hipLaunchKernelGGL((add_rmsnorm_bwd_k<NCH>), dim3(g), dim3(256), lds, st, dy, ydt, dro, drodt, ro,
+                                   rodt, w, rstd, dx, xdt, dres, rdt, part, M, D));
+  MAMBA_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(sum_rows_k, dim3((D + 255) / 256), dim3(256), 0, st, part, g, D, dw);
+  return hipGetLastError();
+}
+
+hipError_t launch_gated_rmsnorm_fwd(const void* x, int xdt, int64_t sx, const void* z, int zdt, int64_t sz,
+                                    const float* w, void* y, int ydt, float* rstd, int64_t M, int D, int G,
+                                    float eps, bool nbg, hipStream_t st) {
+  if (M == 0) return hipSuccess;
+  dim3 grid((unsigned)((M + 3) / 4)), block(256);
+  if (nbg) {
+    NCH_SWITCH(D, hipLaunchKernelGGL((gated_rmsnorm_fwd_k<NCH, true>), grid, block, 0, st, x, xdt, sx, z, zdt, sz,
+                                     w, y, ydt, rstd, M, D, G, eps));
+  } else {
+    NCH_SWITCH(D, hipLaunchKernelGGL((gated_rmsnorm_fwd_k<NCH, false>), grid, block, 0, st, x, xdt, sx, z, zdt,
+                                     sz, w, y, ydt, rstd, M, D, G, eps));
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_gated_rmsnorm_bwd(const void* dy, int ydt, const void* x, int xdt, int64_t sx, const void* z,
+                                    int zdt, int64_t sz, const float* w, const float* rstd, void* dx, int64_t sdx,
+                                    void* dz, int64_t sdz, float* part, float* dw, int64_t M, int D, int G,
+                                    bool nbg, hipStream_t st) {
+  const int g = bwd_grid(M);
+  const size_t lds = 4 * (size_t)D * sizeof(float);
+  if (nbg) {
+    NCH_SWITCH(D, hipLaunchKernelGGL((gated_rmsnorm_bwd_k<NCH, true>), dim3(g), dim3(256), lds, st, dy, ydt, x,
+                                     xdt, sx, z, zdt, sz, w, rstd, dx, sdx, dz, sdz, part, M, D, G));
+  } else {
+    NCH_SWITCH(D, hipLaunchKernelGGL((gated_rmsnorm_bwd_k<NCH, false>), dim3(g), dim3(256), lds, st, dy, ydt, x,
+                                     xdt, sx, z, zdt, sz, w, rstd, dx, sdx, dz, sdz, part, M, D, G));
+  }
+  MAMBA_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(sum_rows_k, dim3((D + 255) / 256), dim3(256), 0, st, part, g, D, dw);
+  return hipGetLastError();
+}
+
+int norm_bwd_partial_rows(int64_t M) { return bwd_grid(M); }
+
+}  // namespace mamba_amd

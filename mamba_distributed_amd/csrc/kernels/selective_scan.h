@@ -1,0 +1,51 @@
+// Argument blocks for kernels/selective_scan.hip (Mamba-1 scan + decode state update).
+#pragma once
+#include "types.h"
+
+namespace mamba_amd {
+
+struct SelScanArgs {
+  int B, D, L, N, G, Kc;  // Kc = channels per workgroup (<= 64)
+  int dtype;              // dtype of u / delta / z / B / C / out (kBF16 or kF32)
+  bool softplus, vec, vecbc, vecg, vecz;
+  const void* u_; const void* delta_;
+  int64_t sub, sud, sdb, sdd;                       // (b, d, l) strides, unit l
+  const float* A;                                   // (D, N)
+  const void* Bm_; int64_t sBb, sBg, sBn;           // (b, g, n, l)
+  const void* Cm_; int64_t sCb, sCg, sCn;
+  const float* D_; const float* delta_bias;
+  const void* z_; int64_t szb, szd;
+  void* out_; int64_t sob, sod;
+  float* carries;                                   // (B, D, ntiles, N) state at each tile start
+  float* last_state;                                // (B, D, N) or null
+  // backward
+  const void* dout_; int64_t sgb, sgd;
+  void* du_; int64_t sdub, sdud;
+  void* ddelta_; int64_t sddb, sddd;
+  void* dz_; int64_t sdzb, sdzd;
+  void* dB_; int64_t sdBb, sdBg, sdBn;
+  void* dC_; int64_t sdCb, sdCg, sdCn;
+  float* part_dB; float* part_dC;                   // (B, ndg, N, L)
+  float* part_dA;                                   // (B, D, N)   zero-initialised
+  float* part_dD; float* part_dbias;                // (B, D)      zero-initialised
+};
+
+struct SSMUpdateArgs {
+  int B, H, P, N, G, dtype;
+  bool softplus, A_per_n, D_per_p, dt_bias_per_p;
+  float* state;                                     // (B, H, P, N) fp32, updated in place
+  const void* x_; int64_t sxb, sxh;                 // (B, H, P) unit p
+  const void* dt_; int64_t sdtb, sdth, sdtp;
+  const float* A; const float* D; const float* dt_bias;
+  const void* Bm_; int64_t sBb, sBg;                // (B, G, N) unit n
+  const void* Cm_; int64_t sCb, sCg;
+  const void* z_; int64_t szb, szh;
+  void* out_;                                       // (B, H, P) contiguous
+};
+
+hipError_t launch_selscan_fwd(const SelScanArgs& a, hipStream_t st);
+hipError_t launch_selscan_bwd(const SelScanArgs& a, hipStream_t st);
+int selscan_ntiles(int L);
+hipError_t launch_ssm_update(const SSMUpdateArgs& a, hipStream_t st);
+
+}  // namespace mamba_amd

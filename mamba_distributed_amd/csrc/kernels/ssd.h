@@ -1,0 +1,41 @@
+// Argument block shared by the SSD kernels (kernels/ssd.hip) and the torch binding.
+#pragma once
+#include "types.h"
+
+namespace mamba_amd {
+
+struct SSDArgs {
+  int B, L, H, G, N, nc, Lp;  // Lp = nc * 64
+  int HG, nhg;                // heads per workgroup in the chunk kernels, nhg = H / HG
+  // forward inputs
+  const bf16_t* x; int64_t sxb, sxl, sxh;  // (b, l, h, p) unit p stride
+  const void* dt; int dt_dtype; int64_t sdtb, sdtl, sdth;
+  const float* A; const float* D; const float* dt_bias;
+  const bf16_t* Bm; int64_t sBb, sBl, sBg;  // (b, l, g, n) unit n stride
+  const bf16_t* Cm; int64_t sCb, sCl, sCg;
+  bool softplus; float dt_min, dt_max;
+  const float* init;      // (b, h, p, n) or null
+  // forward outputs / saved
+  float* dtp; float* cum; // (b, h, Lp)
+  bf16_t* states;         // (b, nc, h, p, n) state entering each chunk
+  float* final_state;     // (b, h, p, n) or null
+  bf16_t* y; int64_t syb, syl, syh;
+  // backward
+  const bf16_t* dy; int64_t sdyb, sdyl, sdyh;
+  const float* dfinal;    // (b, h, p, n) or null
+  bf16_t* dstates;        // (b, nc, h, p, n) workspace
+  float* dinit;           // or null
+  bf16_t* dx; int64_t sdxb, sdxl, sdxh;
+  void* ddt; int ddt_dtype; int64_t sddtb, sddtl, sddth;
+  bf16_t* dB; int64_t sdBb, sdBl, sdBg;
+  bf16_t* dC; int64_t sdCb, sdCl, sdCg;
+  float* part_dcb;        // (b, nc, nhg, 64, 64)
+  float* part_db;         // (b, nc, nhg, 64, N)
+  float* part_dc;         // (b, nc, nhg, 64, N)
+  float* part_dA; float* part_dD; float* part_dbias;  // (b, nc, h)
+};
+
+hipError_t launch_ssd_fwd(const SSDArgs& a, hipStream_t st);
+hipError_t launch_ssd_bwd(const SSDArgs& a, hipStream_t st);
+
+}  // namespace mamba_amd

@@ -1,0 +1,108 @@
+"""Token-shard data loading (reference dataloader.py:7-52).
+
+``DataLoaderLite`` keeps the reference's semantics exactly — sorted shards whose names contain
+the split, rank r starts at B*T*r and strides B*T*world, x = buf[:-1], y = buf[1:], rollover to
+the next shard (mod #shards) when the next global window would overflow, ``reset()`` rewinds.
+
+Differences: shards are memory-mapped (``np.load(mmap_mode='r')``) instead of
+materialised as int64 in host RAM, and batches can be produced straight into pinned memory by
+the native prefetcher (``native_loader.py``) so the H2D copy is asynchronous.
+``SyntheticTokens`` is the no-dataset source used by bench.py / tests (BASELINE: synthetic data).
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+
+def load_tokens(filename: str) -> torch.Tensor:
+    npt = np.load(filename, mmap_mode="r")
+    return torch.from_numpy(np.ascontiguousarray(npt).astype(np.int64, copy=False))
+
+
+def _load_tokens_np(filename: str) -> np.ndarray:
+    return np.load(filename, mmap_mode="r")
+
+
+class DataLoaderLite:
+    def __init__(self, B, T, process_rank, num_processes, split, master_process=True,
+                 data_root: str = "edu_fineweb10B", verbose: bool = True):
+        self.B = B
+        self.T = T
+        self.process_rank = process_rank
+        self.num_processes = num_processes
+        assert split in {"train", "val"}
+        shards = sorted(s for s in os.listdir(data_root) if split in s)
+        self.shards: List[str] = [os.path.join(data_root, s) for s in shards]
+        assert len(self.shards) > 0, f"no shards found for split {split}"
+        if master_process and verbose:
+            print(f"found {len(self.shards)} shards for split {split}")
+        self.reset()
+
+    def reset(self):
+        self.current_shard = 0
+        self.tokens = _load_tokens_np(self.shards[self.current_shard])
+        self.current_position = self.B * self.T * self.process_rank
+
+    def state_dict(self):
+        return {"current_shard": self.current_shard, "current_position": self.current_position}
+
+    def load_state_dict(self, s):
+        self.current_shard = s["current_shard"]
+        self.tokens = _load_tokens_np(self.shards[self.current_shard])
+        self.current_position = s["current_position"]
+
+    def next_batch(self):
+        B, T = self.B, self.T
+        buf = torch.from_numpy(np.asarray(
+            self.tokens[self.current_position: self.current_position + B * T + 1]).astype(np.int64))
+        x = buf[:-1].view(B, T)
+        y = buf[1:].view(B, T)
+        self.current_position += B * T * self.num_processes
+        if self.current_position + (B * T * self.num_processes + 1) > len(self.tokens):
+            self.current_shard = (self.current_shard + 1) % len(self.shards)
+            self.tokens = _load_tokens_np(self.shards[self.current_shard])
+            self.current_position = B * T * self.process_rank
+        return x, y
+
+
+class SyntheticTokens:
+    """Deterministic random tokens with the DataLoaderLite interface (no dataset on the box).
+
+    Batches are generated on ``device`` directly (no H2D copy) from a per-rank seeded generator.
+    """
+
+    def __init__(self, B, T, vocab_size, process_rank=0, num_processes=1, device="cpu", seed=1234):
+        self.B, self.T, self.V = B, T, vocab_size
+        self.process_rank, self.num_processes = process_rank, num_processes
+        self.device = torch.device(device)
+        self.seed = seed
+        self.reset()
+
+    def reset(self):
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(self.seed + 7919 * self.process_rank)
+
+    def next_batch(self):
+        buf = torch.randint(0, self.V, (self.B * self.T + 1,), generator=self.gen, device=self.device)
+        return buf[:-1].view(self.B, self.T), buf[1:].view(self.B, self.T)
+
+
+def write_synthetic_shards(root: str, n_train: int = 2, n_val: int = 1, tokens_per_shard: int = 1 << 16,
+                           vocab_size: int = 50304, seed: int = 0, dtype=np.uint16) -> List[str]:
+    """Write edu_fineweb-style ``*_train_XXXXXX.npy`` / ``*_val_XXXXXX.npy`` shards."""
+    os.makedirs(root, exist_ok=True)
+    rng = np.random.default_rng(seed)
+    paths = []
+    for split, n in (("val", n_val), ("train", n_train)):
+        for i in range(n):
+            p = os.path.join(root, f"edufineweb_{split}_{i:06d}.npy")
+            np.save(p, rng.integers(0, vocab_size, size=tokens_per_shard, dtype=np.int64).astype(dtype))
+            paths.append(p)
+    return paths
+
+
+_ = Optional

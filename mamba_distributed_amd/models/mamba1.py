@@ -1,0 +1,232 @@
+"""Mamba-1 (S6) mixer.
+
+Parameter names, shapes and init follow upstream ``mamba_ssm/modules/mamba_simple.py::Mamba``
+so checkpoints are interchangeable with the reference.
+
+Layout choice (MI355X-first, not upstream's): the whole inner path runs channel-major with the
+batch folded inside, i.e. tensors of logical shape (b, d, l) live in memory as (d, b, l).  Every
+projection is then ONE plain 2-D GEMM on hipBLASLt —
+  xz    = W_in  @ h^T           (2di, b*l)
+  x_dbl = W_x   @ conv_out      (R+2N, b*l)
+  delta = W_dt  @ x_dbl[:R]     (di, b*l)
+  out   = y^T   @ W_out^T       (b*l, d)
+— and the HIP conv / scan kernels see unit stride along time, which is what their time-tiled
+wavefront layout wants.  The backward writes d(xz) as one buffer (no slice-gradient
+materialisation), like upstream's MambaInnerFn.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops import _ext
+from ..ops.conv1d import causal_conv1d_update
+from ..ops.reference import causal_conv1d_ref, selective_scan_ref, softplus_inverse
+from ..ops.selective_scan import selective_state_update
+
+
+def _cm(t2d: torch.Tensor, b: int, l: int) -> torch.Tensor:
+    """(d, b*l) -> logical (b, d, l) view over the same memory."""
+    return t2d.view(t2d.shape[0], b, l).permute(1, 0, 2)
+
+
+def _flat(t: torch.Tensor) -> torch.Tensor:
+    """logical (b, d, l) stored (d, b, l) -> (d, b*l) view."""
+    return t.permute(1, 0, 2).reshape(t.shape[1], -1)
+
+
+class _Mamba1InnerFn(torch.autograd.Function):
+    """conv1d+SiLU -> x_proj -> dt_proj -> selective scan(+D, *silu(z)) ; returns y as (di, b*l)."""
+
+    @staticmethod
+    def forward(ctx, xz, conv_w, conv_b, W_x, W_dt, dt_bias, A, D, b, l, compute_dtype):
+        ops = _ext.ops()
+        di = xz.shape[0] // 2
+        R = W_dt.shape[1]
+        N = A.shape[1]
+        cd = compute_dtype
+        xz3 = _cm(xz, b, l)
+        x, z = xz3[:, :di], xz3[:, di:]
+        w2 = conv_w.reshape(di, -1)
+        conv_out = ops.conv1d_cf_fwd(x, w2, conv_b, True)                  # (b,di,l) in (di,b,l) memory
+        co2 = _flat(conv_out)
+        Wx, Wdt = W_x.to(cd), W_dt.to(cd)
+        x_dbl = torch.mm(Wx, co2)                                           # (R+2N, b*l)
+        delta = torch.mm(Wdt, x_dbl[:R])                                    # (di, b*l)
+        Bm = _cm(x_dbl[R:R + N], b, l).unsqueeze(1)                         # (b,1,N,l)
+        Cm = _cm(x_dbl[R + N:], b, l).unsqueeze(1)
+        y, carries, _ = ops.selscan_fwd(conv_out, _cm(delta, b, l), A, Bm, Cm, D, z, dt_bias, True)
+        ctx.save_for_backward(xz, w2, conv_b, Wx, Wdt, dt_bias, A, D, conv_out, x_dbl, delta, carries)
+        ctx.meta = (b, l, conv_w.shape, W_x.dtype, W_dt.dtype)
+        return _flat(y)
+
+    @staticmethod
+    def backward(ctx, dy2):
+        xz, w2, conv_b, Wx, Wdt, dt_bias, A, D, conv_out, x_dbl, delta, carries = ctx.saved_tensors
+        b, l, wshape, wx_dtype, wdt_dtype = ctx.meta
+        ops = _ext.ops()
+        di = xz.shape[0] // 2
+        R = Wdt.shape[1]
+        N = A.shape[1]
+        xz3 = _cm(xz, b, l)
+        x, z = xz3[:, :di], xz3[:, di:]
+        dxz = torch.empty_like(xz)
+        dxz3 = _cm(dxz, b, l)
+        Bm = _cm(x_dbl[R:R + N], b, l).unsqueeze(1)
+        Cm = _cm(x_dbl[R + N:], b, l).unsqueeze(1)
+        dx_dbl = torch.empty_like(x_dbl)
+        du, ddelta, dA, dB, dC, dD, dz, ddt_bias = ops.selscan_bwd_into(
+            _cm(dy2.contiguous() if dy2.stride(-1) != 1 else dy2, b, l), conv_out, _cm(delta, b, l), A,
+            Bm, Cm, D, z, dt_bias, carries, True,
+            dxz3[:, di:], _cm(dx_dbl[R:R + N], b, l).unsqueeze(1), _cm(dx_dbl[R + N:], b, l).unsqueeze(1))
+        dd2 = _flat(ddelta)
+        dWdt = torch.mm(dd2, x_dbl[:R].t())                                  # (di, R)
+        torch.mm(Wdt.t(), dd2, out=dx_dbl[:R])                              # d x_dbl[:R]
+        dWx = torch.mm(dx_dbl, _flat(conv_out).t())                         # (R+2N, di)
+        dco2 = _flat(du)
+        dco2.addmm_(Wx.t(), dx_dbl)                                         # du + W_x^T dx_dbl
+        _, dw, db = ops.conv1d_cf_bwd(x, w2, conv_b, _cm(dco2, b, l), True, dxz3[:, :di])
+        return (dxz, dw.view(wshape).to(w2.dtype), db.to(conv_b.dtype) if conv_b is not None else None,
+                dWx.to(wx_dtype), dWdt.to(wdt_dtype), ddt_bias, dA, dD, None, None, None)
+
+
+def mamba1_inner_ref(xz3, conv_w, conv_b, W_x, W_dt, dt_bias, A, D):
+    """Pure-torch composition of the same path (CPU / oracle).  xz3: (b, 2di, l)."""
+    di = xz3.shape[1] // 2
+    R = W_dt.shape[1]
+    N = A.shape[1]
+    x, z = xz3[:, :di], xz3[:, di:]
+    conv_out = causal_conv1d_ref(x, conv_w.reshape(di, -1), conv_b, "silu")
+    x_dbl = torch.einsum("rd,bdl->brl", W_x.to(conv_out.dtype), conv_out)
+    delta = torch.einsum("dr,brl->bdl", W_dt.to(x_dbl.dtype), x_dbl[:, :R])
+    Bm = x_dbl[:, R:R + N].unsqueeze(1)
+    Cm = x_dbl[:, R + N:].unsqueeze(1)
+    return selective_scan_ref(conv_out, delta, A, Bm, Cm, D, z, dt_bias, True)
+
+
+class Mamba(nn.Module):
+    def __init__(self, d_model, d_state=16, d_conv=4, expand=2, dt_rank="auto", dt_min=0.001,
+                 dt_max=0.1, dt_init="random", dt_scale=1.0, dt_init_floor=1e-4, conv_bias=True,
+                 bias=False, use_fast_path=True, layer_idx=None, device=None, dtype=None):
+        factory = {"device": device, "dtype": dtype}
+        super().__init__()
+        self.d_model = d_model
+        self.d_state = d_state
+        self.d_conv = d_conv
+        self.expand = expand
+        self.d_inner = int(expand * d_model)
+        self.dt_rank = math.ceil(d_model / 16) if dt_rank == "auto" else dt_rank
+        self.use_fast_path = use_fast_path
+        self.layer_idx = layer_idx
+
+        self.in_proj = nn.Linear(d_model, self.d_inner * 2, bias=bias, **factory)
+        self.conv1d = nn.Conv1d(self.d_inner, self.d_inner, bias=conv_bias, kernel_size=d_conv,
+                                groups=self.d_inner, padding=d_conv - 1, **factory)
+        self.activation = "silu"
+        self.act = nn.SiLU()
+        self.x_proj = nn.Linear(self.d_inner, self.dt_rank + d_state * 2, bias=False, **factory)
+        self.dt_proj = nn.Linear(self.dt_rank, self.d_inner, bias=True, **factory)
+
+        dt_init_std = self.dt_rank ** -0.5 * dt_scale
+        with torch.no_grad():
+            if dt_init == "constant":
+                nn.init.constant_(self.dt_proj.weight, dt_init_std)
+            elif dt_init == "random":
+                nn.init.uniform_(self.dt_proj.weight, -dt_init_std, dt_init_std)
+            else:
+                raise NotImplementedError(dt_init)
+            dt = torch.exp(torch.rand(self.d_inner, **factory) * (math.log(dt_max) - math.log(dt_min))
+                           + math.log(dt_min)).clamp(min=dt_init_floor)
+            self.dt_proj.bias.copy_(softplus_inverse(dt))
+        self.dt_proj.bias._no_reinit = True
+
+        A = torch.arange(1, d_state + 1, dtype=torch.float32, device=device).repeat(self.d_inner, 1)
+        self.A_log = nn.Parameter(torch.log(A))
+        self.A_log._no_weight_decay = True
+        self.D = nn.Parameter(torch.ones(self.d_inner, device=device))
+        self.D._no_weight_decay = True
+        self.out_proj = nn.Linear(self.d_inner, d_model, bias=bias, **factory)
+
+    # ------------------------------------------------------------------
+    def forward(self, hidden_states, inference_params=None):
+        b, l, _ = hidden_states.shape
+        if inference_params is not None:
+            conv_state, ssm_state = self._get_states_from_cache(inference_params, b)
+            if inference_params.seqlen_offset > 0:
+                out, _, _ = self.step(hidden_states, conv_state, ssm_state)
+                return out
+        else:
+            conv_state = ssm_state = None
+        cd = torch.get_autocast_dtype("cuda") if (hidden_states.is_cuda and torch.is_autocast_enabled("cuda")) else hidden_states.dtype
+        A = -torch.exp(self.A_log.float())
+        h2 = hidden_states.reshape(b * l, -1).to(cd)
+        xz = torch.mm(self.in_proj.weight.to(cd), h2.t())                  # (2di, b*l)
+        if self.in_proj.bias is not None:
+            xz = xz + self.in_proj.bias.to(cd)[:, None]
+        if conv_state is None and self.use_fast_path and _ext.use_native(xz):
+            y2 = _Mamba1InnerFn.apply(xz, self.conv1d.weight, self.conv1d.bias, self.x_proj.weight,
+                                      self.dt_proj.weight, self.dt_proj.bias.float(), A, self.D.float(),
+                                      b, l, cd)
+            out = F.linear(y2.t().to(cd), self.out_proj.weight.to(cd),
+                           None if self.out_proj.bias is None else self.out_proj.bias.to(cd))
+            return out.view(b, l, -1)
+        xz3 = _cm(xz, b, l)
+        if conv_state is not None:  # prefill: remember the last d_conv-1 inputs for decoding
+            x = xz3[:, :self.d_inner]
+            conv_state.copy_(F.pad(x, (max(0, self.d_conv - 1 - l), 0))[..., -(self.d_conv - 1):])
+            y, last = self._inner_ref_with_state(xz3, A)
+            ssm_state.copy_(last)
+        else:
+            y = mamba1_inner_ref(xz3, self.conv1d.weight, self.conv1d.bias, self.x_proj.weight,
+                                 self.dt_proj.weight, self.dt_proj.bias.float(), A, self.D.float())
+        out = F.linear(y.transpose(1, 2).to(cd), self.out_proj.weight.to(cd),
+                       None if self.out_proj.bias is None else self.out_proj.bias.to(cd))
+        return out
+
+    def _inner_ref_with_state(self, xz3, A):
+        di = self.d_inner
+        R, N = self.dt_rank, self.d_state
+        x, z = xz3[:, :di], xz3[:, di:]
+        conv_out = causal_conv1d_ref(x, self.conv1d.weight.reshape(di, -1), self.conv1d.bias, "silu")
+        x_dbl = torch.einsum("rd,bdl->brl", self.x_proj.weight.to(conv_out.dtype), conv_out)
+        delta = torch.einsum("dr,brl->bdl", self.dt_proj.weight.to(x_dbl.dtype), x_dbl[:, :R])
+        return selective_scan_ref(conv_out, delta, A, x_dbl[:, R:R + N].unsqueeze(1),
+                                  x_dbl[:, R + N:].unsqueeze(1), self.D.float(), z,
+                                  self.dt_proj.bias.float(), True, return_last_state=True)
+
+    @torch.no_grad()
+    def step(self, hidden_states, conv_state, ssm_state):
+        """One decode token.  hidden_states (b, 1, d)."""
+        dtype = hidden_states.dtype
+        h = hidden_states.squeeze(1)
+        xz = F.linear(h, self.in_proj.weight.to(h.dtype),
+                      None if self.in_proj.bias is None else self.in_proj.bias.to(h.dtype))
+        x, z = xz.chunk(2, dim=-1)
+        x = causal_conv1d_update(x, conv_state, self.conv1d.weight, self.conv1d.bias, "silu")
+        x_db = F.linear(x, self.x_proj.weight.to(x.dtype))
+        dt, B, C = torch.split(x_db, [self.dt_rank, self.d_state, self.d_state], dim=-1)
+        dt = F.linear(dt, self.dt_proj.weight.to(dt.dtype))
+        A = -torch.exp(self.A_log.float())
+        y = selective_state_update(ssm_state, x, dt, A, B, C, self.D.float(), z=z,
+                                   dt_bias=self.dt_proj.bias.float(), dt_softplus=True)
+        out = F.linear(y, self.out_proj.weight.to(y.dtype),
+                       None if self.out_proj.bias is None else self.out_proj.bias.to(y.dtype))
+        return out.unsqueeze(1).to(dtype), conv_state, ssm_state
+
+    def allocate_inference_cache(self, batch_size, max_seqlen, dtype=None, **kwargs):
+        device = self.out_proj.weight.device
+        conv_dtype = self.conv1d.weight.dtype if dtype is None else dtype
+        conv_state = torch.zeros(batch_size, self.d_inner, self.d_conv - 1, device=device, dtype=conv_dtype)
+        ssm_state = torch.zeros(batch_size, self.d_inner, self.d_state, device=device, dtype=torch.float32)
+        return conv_state, ssm_state
+
+    def _get_states_from_cache(self, inference_params, batch_size):
+        assert self.layer_idx is not None
+        if self.layer_idx not in inference_params.key_value_memory_dict:
+            inference_params.key_value_memory_dict[self.layer_idx] = self.allocate_inference_cache(
+                batch_size, inference_params.max_seqlen)
+        return inference_params.key_value_memory_dict[self.layer_idx]

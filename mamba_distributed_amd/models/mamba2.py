@@ -1,0 +1,153 @@
+"""Mamba-2 (SSD) mixer.
+
+Parameter names, shapes and init follow upstream ``mamba_ssm/modules/mamba2.py::Mamba2``
+ so checkpoints interchange.  Training forward:
+
+    zxbcdt = in_proj(u)                      hipBLASLt, (b, l, 2di + 2GN + H), token-major
+    y      = mamba2_inner_fn(zxbcdt, ...)    HIP: conv1d(xBC)+SiLU -> SSD -> gated RMSNorm
+    out    = out_proj(y)                     hipBLASLt
+
+The conv, SSD and norm kernels read their operands straight out of the strided zxbcdt buffer
+and the backward writes d(zxbcdt) as one buffer (ops/ssd.py).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops.conv1d import causal_conv1d_update
+from ..ops.norm import RMSNormGated
+from ..ops.reference import causal_conv1d_ref, ssd_chunked_ref, softplus_inverse
+from ..ops.selective_scan import selective_state_update
+from ..ops.ssd import mamba2_inner_fn
+
+
+class Mamba2(nn.Module):
+    def __init__(self, d_model, d_state=128, d_conv=4, conv_init=None, expand=2, headdim=64,
+                 d_ssm=None, ngroups=1, A_init_range=(1, 16), D_has_hdim=False, rmsnorm=True,
+                 norm_before_gate=False, dt_min=0.001, dt_max=0.1, dt_init_floor=1e-4,
+                 dt_limit=(0.0, float("inf")), bias=False, conv_bias=True, chunk_size=256,
+                 use_mem_eff_path=True, layer_idx=None, process_group=None, sequence_parallel=True,
+                 device=None, dtype=None):
+        factory = {"device": device, "dtype": dtype}
+        super().__init__()
+        assert process_group is None, "use parallel.tensor_parallel.Mamba2TP for head-sharded TP"
+        assert not D_has_hdim, "D_has_hdim is not supported"
+        assert rmsnorm, "the gated RMSNorm output path is the only supported one"
+        self.d_model = d_model
+        self.d_state = d_state
+        self.d_conv = d_conv
+        self.conv_init = conv_init
+        self.expand = expand
+        self.d_inner = int(expand * d_model)
+        self.headdim = headdim
+        self.d_ssm = self.d_inner if d_ssm is None else d_ssm
+        assert self.d_ssm == self.d_inner, "d_ssm < d_inner (extra MLP branch) not supported"
+        self.ngroups = ngroups
+        assert self.d_ssm % headdim == 0
+        self.nheads = self.d_ssm // headdim
+        self.D_has_hdim = D_has_hdim
+        self.rmsnorm = rmsnorm
+        self.norm_before_gate = norm_before_gate
+        self.dt_limit = dt_limit
+        self.activation = "silu"
+        self.chunk_size = chunk_size
+        self.use_mem_eff_path = use_mem_eff_path
+        self.layer_idx = layer_idx
+
+        d_in_proj = 2 * self.d_inner + 2 * ngroups * d_state + self.nheads
+        self.in_proj = nn.Linear(d_model, d_in_proj, bias=bias, **factory)
+        conv_dim = self.d_ssm + 2 * ngroups * d_state
+        self.conv1d = nn.Conv1d(conv_dim, conv_dim, bias=conv_bias, kernel_size=d_conv, groups=conv_dim,
+                                padding=d_conv - 1, **factory)
+        if conv_init is not None:
+            nn.init.uniform_(self.conv1d.weight, -conv_init, conv_init)
+        self.act = nn.SiLU()
+
+        dt = torch.exp(torch.rand(self.nheads, **factory) * (math.log(dt_max) - math.log(dt_min))
+                       + math.log(dt_min)).clamp(min=dt_init_floor)
+        self.dt_bias = nn.Parameter(softplus_inverse(dt))
+        self.dt_bias._no_weight_decay = True
+
+        assert A_init_range[0] > 0 and A_init_range[1] >= A_init_range[0]
+        A = torch.empty(self.nheads, dtype=torch.float32, device=device).uniform_(*A_init_range)
+        self.A_log = nn.Parameter(torch.log(A).to(dtype=dtype or torch.float32))
+        self.A_log._no_weight_decay = True
+        self.D = nn.Parameter(torch.ones(self.nheads, device=device))
+        self.D._no_weight_decay = True
+        self.norm = RMSNormGated(self.d_ssm, eps=1e-5, norm_before_gate=norm_before_gate,
+                                 group_size=self.d_ssm // ngroups, **factory)
+        self.out_proj = nn.Linear(self.d_inner, d_model, bias=bias, **factory)
+
+    # ------------------------------------------------------------------
+    def forward(self, u, seqlen=None, seq_idx=None, cu_seqlens=None, inference_params=None):
+        b, l, _ = u.shape
+        conv_state = ssm_state = None
+        if inference_params is not None:
+            conv_state, ssm_state = self._get_states_from_cache(inference_params, b)
+            if inference_params.seqlen_offset > 0:
+                out, _, _ = self.step(u, conv_state, ssm_state)
+                return out
+        zxbcdt = self.in_proj(u)
+        A = -torch.exp(self.A_log.float())
+        if conv_state is None:
+            y = mamba2_inner_fn(zxbcdt, self.conv1d.weight, self.conv1d.bias, self.dt_bias, A, self.D,
+                                self.norm.weight, self.norm.eps, self.headdim, self.ngroups, self.d_state,
+                                self.dt_limit, self.norm_before_gate, ref_chunk_size=min(64, self.chunk_size))
+        else:
+            y = self._prefill(zxbcdt, A, conv_state, ssm_state)
+        return self.out_proj(y)
+
+    def _prefill(self, zxbcdt, A, conv_state, ssm_state):
+        """Prompt pass that also fills the decode cache (conv window + final SSM state)."""
+        di, gn, H = self.d_ssm, self.ngroups * self.d_state, self.nheads
+        z, xBC, dt = torch.split(zxbcdt, [di, di + 2 * gn, H], dim=-1)
+        xt = xBC.transpose(1, 2)
+        w = self.d_conv
+        conv_state.copy_(F.pad(xt, (max(0, w - 1 - xt.shape[-1]), 0))[..., -(w - 1):])
+        xBC = causal_conv1d_ref(xt, self.conv1d.weight.reshape(xt.shape[1], -1), self.conv1d.bias,
+                                "silu").transpose(1, 2)
+        x, Bm, Cm = torch.split(xBC, [di, gn, gn], dim=-1)
+        y, last = ssd_chunked_ref(x.unflatten(-1, (H, self.headdim)), dt, A,
+                                  Bm.unflatten(-1, (self.ngroups, self.d_state)),
+                                  Cm.unflatten(-1, (self.ngroups, self.d_state)), min(64, self.chunk_size),
+                                  D=self.D, dt_bias=self.dt_bias, dt_softplus=True, dt_limit=self.dt_limit,
+                                  return_final_states=True)
+        ssm_state.copy_(last)
+        return self.norm(y.flatten(-2), z)
+
+    @torch.no_grad()
+    def step(self, hidden_states, conv_state, ssm_state):
+        dtype = hidden_states.dtype
+        zxbcdt = self.in_proj(hidden_states.squeeze(1))
+        di, gn, H = self.d_ssm, self.ngroups * self.d_state, self.nheads
+        z, xBC, dt = torch.split(zxbcdt, [di, di + 2 * gn, H], dim=-1)
+        xBC = causal_conv1d_update(xBC, conv_state, self.conv1d.weight, self.conv1d.bias, "silu")
+        x, B, C = torch.split(xBC, [di, gn, gn], dim=-1)
+        A = -torch.exp(self.A_log.float())
+        y = selective_state_update(ssm_state, x.unflatten(-1, (H, self.headdim)), dt, A,
+                                   B.unflatten(-1, (self.ngroups, self.d_state)),
+                                   C.unflatten(-1, (self.ngroups, self.d_state)), self.D,
+                                   z=None, dt_bias=self.dt_bias, dt_softplus=True)
+        y = self.norm(y.flatten(-2), z)
+        out = self.out_proj(y)
+        return out.unsqueeze(1).to(dtype), conv_state, ssm_state
+
+    def allocate_inference_cache(self, batch_size, max_seqlen, dtype=None, **kwargs):
+        device = self.out_proj.weight.device
+        conv_dtype = self.conv1d.weight.dtype if dtype is None else dtype
+        conv_state = torch.zeros(batch_size, self.conv1d.weight.shape[0], self.d_conv - 1, device=device,
+                                 dtype=conv_dtype)
+        ssm_state = torch.zeros(batch_size, self.nheads, self.headdim, self.d_state, device=device,
+                                dtype=torch.float32)
+        return conv_state, ssm_state
+
+    def _get_states_from_cache(self, inference_params, batch_size):
+        assert self.layer_idx is not None
+        if self.layer_idx not in inference_params.key_value_memory_dict:
+            inference_params.key_value_memory_dict[self.layer_idx] = self.allocate_inference_cache(
+                batch_size, inference_params.max_seqlen)
+        return inference_params.key_value_memory_dict[self.layer_idx]

@@ -1,0 +1,74 @@
+"""Causal depthwise conv1d (+SiLU), both memory layouts.
+
+Same call surface as causal-conv1d's ``causal_conv1d_fn(x, weight, bias, activation)`` with x
+given as (batch, dim, seqlen) — SURVEY.md D15, K3-K6.  The layout is taken from the strides:
+
+  * channel-first  (x.stride(2) == 1): Mamba-1 path (x is a slice of the (b, 2di, l) in_proj output)
+      -> HIP ``conv1d_cf_fwd/bwd``: one wavefront per (b, channel-block) walks time with a 3-tap
+         register window; 16-byte loads along l.
+  * channel-last   (x.stride(1) == 1): Mamba-2 path (xBC is a column slice of the (b, l, d_in_proj)
+      in_proj output) -> HIP ``conv1d_cl_fwd/bwd``: lanes over channels (8 bf16 per lane, 16 B),
+      a block owns a time tile, the w-1 halo rows are re-read (cheap, L2 hits).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import _ext
+from .reference import causal_conv1d_ref, causal_conv1d_update_ref
+
+
+def _is_channel_last(x: torch.Tensor) -> bool:
+    return x.stride(1) == 1 and x.stride(2) != 1
+
+
+class _CausalConv1dFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, silu):
+        ops = _ext.ops()
+        w2 = weight.reshape(weight.shape[0], -1)
+        if _is_channel_last(x):
+            xt = x.transpose(1, 2)  # (b, l, d) with unit channel stride
+            out = ops.conv1d_cl_fwd(xt, w2, bias, silu).transpose(1, 2)
+            ctx.cl = True
+        else:
+            if x.stride(2) != 1:
+                x = x.contiguous()
+            out = ops.conv1d_cf_fwd(x, w2, bias, silu)
+            ctx.cl = False
+        ctx.save_for_backward(x, w2, bias)
+        ctx.silu = silu
+        ctx.wshape = weight.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, w2, bias = ctx.saved_tensors
+        ops = _ext.ops()
+        if ctx.cl:
+            dx, dw, db = ops.conv1d_cl_bwd(x.transpose(1, 2), w2, bias, dout.transpose(1, 2), ctx.silu, None)
+            dx = dx.transpose(1, 2)
+        else:
+            dx, dw, db = ops.conv1d_cf_bwd(x, w2, bias, dout, ctx.silu, None)
+        return dx, dw.view(ctx.wshape).to(w2.dtype), (db.to(bias.dtype) if bias is not None else None), None
+
+
+def causal_conv1d_fn(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None,
+                     activation: Optional[str] = None, initial_states=None, return_final_states=False):
+    """x: (b, d, l) in either memory layout; weight (d, w) or (d, 1, w)."""
+    silu = activation in ("silu", "swish")
+    assert activation in (None, "silu", "swish")
+    if initial_states is None and not return_final_states and _ext.use_native(x):
+        return _CausalConv1dFn.apply(x, weight, bias, silu)
+    w2 = weight.reshape(weight.shape[0], -1)
+    return causal_conv1d_ref(x, w2, bias, activation, initial_states, return_final_states)
+
+
+def causal_conv1d_update(x, conv_state, weight, bias=None, activation=None):
+    """Single-token decode step (K6).  conv_state (b, d, w-1) is updated in place."""
+    w2 = weight.reshape(weight.shape[0], -1)
+    if _ext.use_native(x):
+        return _ext.ops().conv1d_update(x, conv_state, w2, bias, activation in ("silu", "swish"))
+    return causal_conv1d_update_ref(x, conv_state, w2, bias, activation)

@@ -1,0 +1,190 @@
+"""Mamba-2 SSD (state-space duality) chunked scan — the Mamba-2 hot op.
+
+Call surface mirrors upstream ``mamba_chunk_scan_combined`` / ``mamba_split_conv1d_scan_combined``
+(SURVEY.md D11/D12, T1-T5, T8); the reference reaches them through ``Mamba2.forward``.
+
+GPU implementation (csrc/kernels/ssd.hip), MI355X-first decomposition:
+  fwd  1. ``ssd_chunk_state``  grid (chunk, head, batch): dt = softplus(dt+bias), in-chunk cumsum of
+          dt*A (wave prefix scan), local chunk state  X^T (w*B)  on MFMA 32x32x16 bf16.
+       2. ``ssd_state_pass``   grid (pn-slice, head, batch): sequential over chunks in fp32 registers,
+          writes the state entering every chunk (bf16) + final state.
+       3. ``ssd_chunk_scan``   grid (chunk, head, batch): CB = C B^T, causal decay mask, y_diag,
+          y_off = e^cum C S_in^T, +D x, all on MFMA, CB tile kept in LDS.
+  bwd  mirrors it: dstate pass (reverse, fp32), chunk-parallel dX/ddt/dcum with head-summed dCB
+       tiles, then one dB/dC GEMM kernel over the head-concatenated K dimension.
+CPU: ``reference.ssd_chunked_ref`` under autograd.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from . import _ext
+from .reference import ssd_chunked_ref, gated_rms_norm_ref, causal_conv1d_ref
+
+_INF = float("inf")
+
+# chunk length used by the HIP kernels (a pure implementation detail: results are identical up to
+# fp rounding for any chunk size); 64 keeps every per-chunk tile MFMA/LDS friendly on gfx950.
+NATIVE_CHUNK = 64
+
+
+class _SSDFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, dt, A, B, C, D, dt_bias, initial_states, dt_softplus, dt_min, dt_max,
+                return_final_states):
+        ops = _ext.ops()
+        y, cum, dtp, states, final = ops.ssd_fwd(x, dt, A, B, C, D, dt_bias, initial_states,
+                                                  NATIVE_CHUNK, dt_softplus, dt_min, dt_max)
+        ctx.save_for_backward(x, dt, A, B, C, D, dt_bias, initial_states, cum, dtp, states)
+        ctx.flags = (dt_softplus, dt_min, dt_max)
+        ctx.return_final = return_final_states
+        if return_final_states:
+            return y, final
+        return y
+
+    @staticmethod
+    def backward(ctx, dy, *rest):
+        x, dt, A, B, C, D, dt_bias, init, cum, dtp, states = ctx.saved_tensors
+        dfinal = rest[0] if ctx.return_final and len(rest) else None
+        softplus, dt_min, dt_max = ctx.flags
+        g = _ext.ops().ssd_bwd(dy.contiguous(), x, dt, A, B, C, D, dt_bias, init, cum, dtp, states,
+                               dfinal, NATIVE_CHUNK, softplus, dt_min, dt_max, None, None, None, None)
+        dx, ddt, dA, dB, dC, dD, ddt_bias, dinit = g
+        return (dx, ddt, dA, dB, dC,
+                dD if D is not None else None,
+                ddt_bias if dt_bias is not None else None,
+                dinit if init is not None else None,
+                None, None, None, None)
+
+
+def mamba_chunk_scan_combined(x, dt, A, B, C, chunk_size=256, D=None, z=None, dt_bias=None,
+                              initial_states=None, seq_idx=None, dt_softplus=False,
+                              dt_limit=(0.0, _INF), return_final_states=False):
+    """x (b,l,h,p), dt (b,l,h), A (h), B/C (b,l,g,n) -> y (b,l,h,p) [, final_states (b,h,p,n)]."""
+    assert seq_idx is None, "seq_idx (packed variable-length) is not supported yet"
+    if _ext.use_native(x) and z is None and (D is None or D.dim() == 1):
+        out = _SSDFn.apply(x, dt, A, B, C, D, dt_bias, initial_states, dt_softplus,
+                           float(dt_limit[0]), float(dt_limit[1]), return_final_states)
+        return out
+    return ssd_chunked_ref(x, dt, A, B, C, chunk_size, D=D, z=z, dt_bias=dt_bias,
+                           dt_softplus=dt_softplus, dt_limit=dt_limit, initial_states=initial_states,
+                           return_final_states=return_final_states)
+
+
+# ----------------------------------------------------------------------------------------
+# Fused Mamba-2 inner path: conv1d(xBC)+SiLU -> SSD -> gated RMSNorm   (out_proj stays outside,
+# on hipBLASLt, so autocast handles it)
+# ----------------------------------------------------------------------------------------
+class _Mamba2InnerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, zxbcdt, conv_w, conv_b, dt_bias, A, D, norm_w, eps, headdim, ngroups, d_state,
+                dt_min, dt_max, norm_before_gate):
+        ops = _ext.ops()
+        b, l, dproj = zxbcdt.shape
+        H = dt_bias.shape[0]
+        di = H * headdim
+        conv_dim = di + 2 * ngroups * d_state
+        assert dproj == 2 * di + 2 * ngroups * d_state + H, "only d_mlp == 0 layouts are supported"
+        if zxbcdt.stride(-1) != 1:
+            zxbcdt = zxbcdt.contiguous()
+        z = zxbcdt[..., :di]
+        xBC = zxbcdt[..., di:di + conv_dim]
+        dt = zxbcdt[..., di + conv_dim:]
+        w2 = conv_w.reshape(conv_dim, -1)
+        xBC_c = ops.conv1d_cl_fwd(xBC, w2, conv_b, True)                # (b, l, conv_dim)
+        x = xBC_c[..., :di].unflatten(-1, (H, headdim))
+        Bm = xBC_c[..., di:di + ngroups * d_state].unflatten(-1, (ngroups, d_state))
+        Cm = xBC_c[..., di + ngroups * d_state:].unflatten(-1, (ngroups, d_state))
+        y, cum, dtp, states, _ = ops.ssd_fwd(x, dt, A, Bm, Cm, D, dt_bias, None, NATIVE_CHUNK,
+                                             True, dt_min, dt_max)
+        y2 = y.view(b * l, di)
+        yn, rstd = ops.gated_rmsnorm_fwd(y2, z.flatten(0, 1), norm_w, eps, di // ngroups, norm_before_gate)
+        ctx.save_for_backward(zxbcdt, w2, conv_b, dt_bias, A, D, norm_w, xBC_c, y, rstd, cum, dtp, states)
+        ctx.meta = (eps, headdim, ngroups, d_state, dt_min, dt_max, norm_before_gate)
+        ctx.wshape = conv_w.shape
+        return yn.view(b, l, di)
+
+    @staticmethod
+    def backward(ctx, dyn):
+        (zxbcdt, w2, conv_b, dt_bias, A, D, norm_w, xBC_c, y, rstd, cum, dtp, states) = ctx.saved_tensors
+        eps, headdim, ngroups, d_state, dt_min, dt_max, nbg = ctx.meta
+        ops = _ext.ops()
+        b, l, dproj = zxbcdt.shape
+        H = dt_bias.shape[0]
+        di = H * headdim
+        gn = ngroups * d_state
+        conv_dim = di + 2 * gn
+        dz_all = torch.empty_like(zxbcdt)
+        z = zxbcdt[..., :di]
+        # gated norm backward writes dz straight into its slice of d(zxbcdt)
+        dy, _, dnorm_w = ops.gated_rmsnorm_bwd(dyn.reshape(b * l, di), y.view(b * l, di),
+                                               z.flatten(0, 1), norm_w, rstd, di // ngroups, nbg,
+                                               None, dz_all[..., :di].flatten(0, 1))
+        x = xBC_c[..., :di].unflatten(-1, (H, headdim))
+        Bm = xBC_c[..., di:di + gn].unflatten(-1, (ngroups, d_state))
+        Cm = xBC_c[..., di + gn:].unflatten(-1, (ngroups, d_state))
+        dt = zxbcdt[..., di + conv_dim:]
+        dxBC_c = torch.empty_like(xBC_c)
+        g = ops.ssd_bwd(dy.view(b, l, H, headdim), x, dt, A, Bm, Cm, D, dt_bias, None, cum, dtp, states,
+                        None, NATIVE_CHUNK, True, dt_min, dt_max,
+                        dxBC_c[..., :di].unflatten(-1, (H, headdim)),
+                        dz_all[..., di + conv_dim:],
+                        dxBC_c[..., di:di + gn].unflatten(-1, (ngroups, d_state)),
+                        dxBC_c[..., di + gn:].unflatten(-1, (ngroups, d_state)))
+        _, _, dA, _, _, dD, ddt_bias, _ = g
+        xBC = zxbcdt[..., di:di + conv_dim]
+        _, dw, db = ops.conv1d_cl_bwd(xBC, w2, conv_b, dxBC_c, True, dz_all[..., di:di + conv_dim])
+        return (dz_all, dw.view(ctx.wshape).to(w2.dtype), db.to(conv_b.dtype) if conv_b is not None else None,
+                ddt_bias, dA, dD, dnorm_w, None, None, None, None, None, None, None)
+
+
+def mamba2_inner_ref(zxbcdt, conv_w, conv_b, dt_bias, A, D, norm_w, eps, headdim, ngroups, d_state,
+                     dt_limit=(0.0, _INF), norm_before_gate=False, chunk_size=64):
+    b, l, dproj = zxbcdt.shape
+    H = dt_bias.shape[0]
+    di = H * headdim
+    gn = ngroups * d_state
+    conv_dim = di + 2 * gn
+    z, xBC, dt = torch.split(zxbcdt, [di, conv_dim, H], dim=-1)
+    xBC = causal_conv1d_ref(xBC.transpose(1, 2), conv_w.reshape(conv_dim, -1), conv_b, "silu").transpose(1, 2)
+    x, Bm, Cm = torch.split(xBC, [di, gn, gn], dim=-1)
+    y = ssd_chunked_ref(x.unflatten(-1, (H, headdim)), dt, A, Bm.unflatten(-1, (ngroups, d_state)),
+                        Cm.unflatten(-1, (ngroups, d_state)), chunk_size, D=D, dt_bias=dt_bias,
+                        dt_softplus=True, dt_limit=dt_limit)
+    y = y.flatten(-2)
+    return gated_rms_norm_ref(y, z, norm_w, eps, di // ngroups, norm_before_gate)
+
+
+def mamba2_inner_fn(zxbcdt, conv_w, conv_b, dt_bias, A, D, norm_w, eps, headdim, ngroups, d_state,
+                    dt_limit=(0.0, _INF), norm_before_gate=False, ref_chunk_size=64):
+    """conv1d+SiLU -> SSD -> gated RMSNorm on the in_proj output; returns (b, l, d_inner)."""
+    if _ext.use_native(zxbcdt):
+        return _Mamba2InnerFn.apply(zxbcdt, conv_w, conv_b, dt_bias, A, D, norm_w, eps, headdim,
+                                    ngroups, d_state, float(dt_limit[0]), float(dt_limit[1]),
+                                    norm_before_gate)
+    return mamba2_inner_ref(zxbcdt, conv_w, conv_b, dt_bias, A, D, norm_w, eps, headdim, ngroups,
+                            d_state, dt_limit, norm_before_gate, ref_chunk_size)
+
+
+def mamba_split_conv1d_scan_combined(zxbcdt, conv1d_weight, conv1d_bias, dt_bias, A, D, chunk_size,
+                                     initial_states=None, seq_idx=None, dt_limit=(0.0, _INF),
+                                     return_final_states=False, activation="silu",
+                                     rmsnorm_weight=None, rmsnorm_eps=1e-6, outproj_weight=None,
+                                     outproj_bias=None, headdim=None, ngroups=1, norm_before_gate=True):
+    """Upstream-compatible entry point (D11).  Requires rmsnorm_weight (the Mamba2 default)."""
+    assert initial_states is None and seq_idx is None and not return_final_states
+    assert activation in ("silu", "swish") and rmsnorm_weight is not None
+    H = dt_bias.shape[0]
+    d_state = (zxbcdt.shape[-1] - H - 2 * H * headdim) // (2 * ngroups)
+    y = mamba2_inner_fn(zxbcdt, conv1d_weight, conv1d_bias, dt_bias, A, D, rmsnorm_weight, rmsnorm_eps,
+                        headdim, ngroups, d_state, dt_limit, norm_before_gate, chunk_size)
+    if outproj_weight is not None:
+        y = F.linear(y, outproj_weight, outproj_bias)
+    return y
+
+
+_ = math

@@ -1,0 +1,66 @@
+"""Data parallelism over RCCL / xGMI (reference train.py:86, 209-221).
+
+The reference wraps the model in torch DDP with defaults (25 MB buckets).  On one 8x MI355X node
+the GPUs form a fully connected xGMI mesh (7 links x ~153 GB/s per GPU).  RCCL's ring
+all-reduce is per-link bound, so for the 1.12 GB fp32 gradient of the 280M model the
+all-reduce itself costs ~6-13 ms — small next to a 300+ ms step — and what matters is (a) that it
+overlaps the LAST micro-step's backward and (b) that the per-collective launch latency is
+amortised.  Defaults chosen for that regime:
+
+  * ``bucket_cap_mb=100``  (4x fewer collectives than 25 MB; a 100 MB bucket moves in
+    ~0.5-1 ms over xGMI, still much shorter than the backward of the 64 layers it overlaps)
+  * ``gradient_as_bucket_view=True``  (grads live in the buckets: no copy in / copy out)
+  * ``static_graph=True`` when the model's graph is fixed (Mamba LMs are)
+  * optional bf16 compression hook (``grad_comm_dtype="bf16"``) halves the bytes on the links.
+
+Gradient accumulation uses ``require_backward_grad_sync`` exactly like the reference
+(train.py:209-210): only the last micro-step's backward launches the bucketed all-reduce.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+from torch.nn.parallel import DistributedDataParallel as DDP
+
+from .dist import DistInfo
+
+
+def wrap_ddp(model: torch.nn.Module, info: DistInfo, bucket_cap_mb: float = 100.0,
+             grad_comm_dtype: str = "fp32", static_graph: bool = True,
+             gradient_as_bucket_view: bool = True):
+    if not info.ddp:
+        return model
+    device_ids = [info.local_rank] if info.device.startswith("cuda") else None
+    m = DDP(model, device_ids=device_ids, bucket_cap_mb=bucket_cap_mb,
+            gradient_as_bucket_view=gradient_as_bucket_view, static_graph=static_graph,
+            broadcast_buffers=False)
+    if grad_comm_dtype == "bf16":
+        from torch.distributed.algorithms.ddp_comm_hooks import default_hooks
+        m.register_comm_hook(dist.group.WORLD, default_hooks.bf16_compress_hook)
+    elif grad_comm_dtype == "fp16":
+        from torch.distributed.algorithms.ddp_comm_hooks import default_hooks
+        m.register_comm_hook(dist.group.WORLD, default_hooks.fp16_compress_hook)
+    return m
+
+
+def unwrap(model):
+    return model.module if isinstance(model, DDP) else model
+
+
+def set_grad_sync(model, enabled: bool):
+    if isinstance(model, DDP):
+        model.require_backward_grad_sync = enabled
+
+
+def params_in_sync(model, atol: float = 0.0) -> bool:
+    """Debug / test helper: every rank holds bit-identical parameters (max-abs-diff over ranks)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return True
+    ok = torch.ones(1, device=next(model.parameters()).device)
+    for p in unwrap(model).parameters():
+        ref = p.detach().clone()
+        dist.broadcast(ref, src=0)
+        if (ref - p.detach()).abs().max().item() > atol:
+            ok.zero_()
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    return bool(ok.item() == 1)

@@ -1,0 +1,267 @@
+"""The training loop of the reference (train.py:24-244) as a library.
+
+Zero-flag ``TrainArgs()`` reproduces the reference hyper-parameters:
+B=32, T=1024, 524,288 tokens/step, lr 6e-4 -> 6e-5 (warmup 715, cosine to 19,073), wd 0.1,
+AdamW(0.9, 0.95, 1e-8, fused), clip 1.0, bf16 autocast, seed 1337, val 20x every 250 steps,
+checkpoint every 1000, samples every 250, ``MambaConfig(d_model=768, vocab_size=50304)``.
+
+Log formats are kept byte-compatible (train.py:151, 237-241): ``"{step} val {:.4f}"``,
+``"{step} train {:.6f}"`` and the ``step {:5d} | loss: ... | tok/sec: ...`` stdout line.
+Additions: flags (model preset, Mamba1/Mamba2, sizes, synthetic data, steps, DDP knobs), resume
+(optimizer + loader + RNG in the checkpoint), steady-state tok/s excluding eval steps (A10),
+optional JSONL metrics.
+"""
+from __future__ import annotations
+
+import contextlib
+import json
+import math
+import os
+import time
+from dataclasses import asdict, dataclass, field
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from .config import MambaConfig, preset
+from .data.loader import DataLoaderLite, SyntheticTokens
+from .lm import LMHeadModel
+from .parallel import ddp as ddp_mod
+from .parallel.dist import all_reduce_avg, destroy, init_distributed
+from .utils.checkpoint import latest_checkpoint, load_checkpoint, save_checkpoint, set_rng_state
+from .utils.lr import get_lr
+
+
+@dataclass
+class TrainArgs:
+    total_batch_size: int = 524288
+    B: int = 32
+    T: int = 1024
+    model: Optional[str] = None          # preset name; None -> reference MambaConfig(768, 50304)
+    layer: Optional[str] = None          # override ssm_cfg["layer"]: Mamba1 | Mamba2
+    n_layer: Optional[int] = None
+    d_model: Optional[int] = None
+    max_lr: float = 6e-4
+    min_lr_ratio: float = 0.1
+    warmup_steps: int = 715
+    max_steps: int = 19073               # schedule length (reference)
+    steps: Optional[int] = None          # stop after this many steps (default: max_steps)
+    weight_decay: float = 0.1
+    grad_clip: float = 1.0
+    val_every: int = 250
+    val_steps: int = 20
+    ckpt_every: int = 1000
+    sample_every: int = 250
+    data_root: str = "edu_fineweb10B"
+    synthetic: bool = False
+    log_dir: str = "log"
+    seed: int = 1337
+    backend: str = "auto"
+    bucket_cap_mb: float = 100.0
+    grad_comm_dtype: str = "fp32"
+    resume: bool = False
+    fused_ce: bool = True
+    save_optimizer: bool = True
+    metrics_jsonl: Optional[str] = None
+    sample_prompt: str = "Hello, I'm a language model,"
+    device_type: str = "auto"
+
+
+def build_config(a: TrainArgs) -> MambaConfig:
+    cfg = preset(a.model) if a.model else MambaConfig(d_model=768, vocab_size=50304)
+    if a.layer:
+        cfg.ssm_cfg = dict(cfg.ssm_cfg, layer=a.layer)
+    if a.n_layer:
+        cfg.n_layer = a.n_layer
+    if a.d_model:
+        cfg.d_model = a.d_model
+    return cfg
+
+
+class Trainer:
+    def __init__(self, args: TrainArgs):
+        self.a = a = args
+        self.info = init_distributed(a.backend, a.device_type)
+        self.device = self.info.device
+        self.device_type = "cuda" if self.device.startswith("cuda") else "cpu"
+        self.master = self.info.master
+        torch.manual_seed(a.seed)
+        if torch.cuda.is_available():
+            torch.cuda.manual_seed(a.seed)
+        world = self.info.world_size
+        assert a.total_batch_size % (a.B * a.T * world) == 0, \
+            "make sure total_batch_size is divisible by B * T * ddp_world_size"
+        self.grad_accum_steps = a.total_batch_size // (a.B * a.T * world)
+        if self.master:
+            print(f"total desired batch size: {a.total_batch_size}")
+            print(f"=> calculated gradient accumulation steps: {self.grad_accum_steps}")
+        self.config = build_config(a)
+        if a.synthetic:
+            self.train_loader = SyntheticTokens(a.B, a.T, self.config.vocab_size, self.info.rank, world,
+                                                device=self.device, seed=a.seed)
+            self.val_loader = SyntheticTokens(a.B, a.T, self.config.vocab_size, self.info.rank, world,
+                                              device=self.device, seed=a.seed + 1)
+        else:
+            self.train_loader = DataLoaderLite(a.B, a.T, self.info.rank, world, "train", self.master, a.data_root)
+            self.val_loader = DataLoaderLite(a.B, a.T, self.info.rank, world, "val", self.master, a.data_root)
+        if self.device_type == "cuda":
+            torch.set_float32_matmul_precision("high")
+        self.raw_model = LMHeadModel(self.config, device=self.device)
+        self.raw_model.to(self.device)
+        if self.master:
+            total = int(sum(p.numel() for p in self.raw_model.parameters()) // 1e6)
+            print(f"Total number of parameters: {total}M")
+        self.model = ddp_mod.wrap_ddp(self.raw_model, self.info, a.bucket_cap_mb, a.grad_comm_dtype)
+        self.optimizer = self.raw_model.configure_optimizers(a.weight_decay, a.max_lr, self.device_type, self.master)
+        os.makedirs(a.log_dir, exist_ok=True)
+        self.log_file = os.path.join(a.log_dir, "log.txt")
+        self.start_step = 0
+        if a.resume:
+            self._resume()
+        if self.master and self.start_step == 0:
+            with open(self.log_file, "w"):
+                pass
+        self.enc = self.raw_model.enc
+        self.step_times = []
+
+    # ------------------------------------------------------------------
+    def lr(self, it):
+        a = self.a
+        return get_lr(it, a.max_lr, a.max_lr * a.min_lr_ratio, a.warmup_steps, a.max_steps)
+
+    def _autocast(self):
+        return torch.autocast(device_type=self.device_type, dtype=torch.bfloat16)
+
+    def _batch(self, loader):
+        x, y = loader.next_batch()
+        return x.to(self.device, non_blocking=True), y.to(self.device, non_blocking=True)
+
+    def _resume(self):
+        path = latest_checkpoint(self.a.log_dir)
+        if path is None:
+            return
+        ck = load_checkpoint(path, map_location=self.device)
+        self.raw_model.load_state_dict(ck["model"])
+        if "optimizer" in ck:
+            self.optimizer.load_state_dict(ck["optimizer"])
+        if "loader" in ck and hasattr(self.train_loader, "load_state_dict"):
+            loaders = ck["loader"]
+            st = loaders[self.info.rank] if isinstance(loaders, list) and self.info.rank < len(loaders) else None
+            if st is not None:
+                self.train_loader.load_state_dict(st)
+        if "rng" in ck:
+            set_rng_state(ck["rng"])
+        self.start_step = int(ck["step"]) + 1
+        if self.master:
+            print(f"resumed from {path} at step {self.start_step}")
+
+    # ------------------------------------------------------------------
+    @torch.no_grad()
+    def validate(self):
+        self.model.eval()
+        self.val_loader.reset()
+        val_loss_accum = torch.zeros((), device=self.device)
+        for _ in range(self.a.val_steps):
+            x, y = self._batch(self.val_loader)
+            with self._autocast():
+                _, loss = self.model(x, y, return_logits=False)
+            val_loss_accum += loss.detach().float() / self.a.val_steps
+        all_reduce_avg(val_loss_accum)
+        return val_loss_accum.item()
+
+    @torch.no_grad()
+    def sample(self, num_return_sequences=4, max_length=32):
+        self.model.eval()
+        tokens = torch.tensor(self.enc.encode(self.a.sample_prompt), dtype=torch.long)
+        xgen = tokens.unsqueeze(0).repeat(num_return_sequences, 1).to(self.device)
+        sample_rng = torch.Generator(device=self.device)
+        sample_rng.manual_seed(42 + self.info.rank)
+        while xgen.size(1) < max_length:
+            with self._autocast():
+                logits, _ = self.model(xgen)
+            probs = F.softmax(logits[:, -1, :].float(), dim=-1)
+            topk_probs, topk_indices = torch.topk(probs, 50, dim=-1)
+            ix = torch.multinomial(topk_probs, 1, generator=sample_rng)
+            xgen = torch.cat((xgen, torch.gather(topk_indices, -1, ix)), dim=1)
+        for i in range(num_return_sequences):
+            print(f"rank {self.info.rank} sample {i}: {self.enc.decode(xgen[i, :max_length].tolist())}")
+
+    def train_step(self, step):
+        self.model.train()
+        self.optimizer.zero_grad(set_to_none=True)
+        loss_accum = torch.zeros((), device=self.device)
+        for micro_step in range(self.grad_accum_steps):
+            x, y = self._batch(self.train_loader)
+            ddp_mod.set_grad_sync(self.model, micro_step == self.grad_accum_steps - 1)
+            with self._autocast():
+                _, loss = self.model(x, y, return_logits=not self.a.fused_ce)
+            loss = loss / self.grad_accum_steps
+            loss_accum += loss.detach().float()
+            loss.backward()
+        all_reduce_avg(loss_accum)
+        norm = torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.a.grad_clip)
+        lr = self.lr(step)
+        for g in self.optimizer.param_groups:
+            g["lr"] = lr
+        self.optimizer.step()
+        return loss_accum, norm, lr
+
+    def save(self, step, val_loss):
+        path = os.path.join(self.a.log_dir, f"model_{step:05d}.pt")
+        opt = self.optimizer if self.a.save_optimizer else None
+        loader_state = self.train_loader.state_dict() if hasattr(self.train_loader, "state_dict") else None
+        save_checkpoint(path, self.raw_model, step, val_loss, optimizer=opt,
+                        loader_state=[loader_state] if loader_state is not None else None)
+        return path
+
+    def run(self):
+        a = self.a
+        last = (a.steps if a.steps is not None else a.max_steps)
+        metrics = open(a.metrics_jsonl, "a") if (a.metrics_jsonl and self.master) else None
+        for step in range(self.start_step, last):
+            t0 = time.time()
+            last_step = step == last - 1
+            eval_step = False
+            if step % a.val_every == 0 or last_step:
+                eval_step = True
+                val_loss = self.validate()
+                if self.master:
+                    print(f"validation loss: {val_loss:.4f}")
+                    with open(self.log_file, "a") as f:
+                        f.write(f"{step} val {val_loss:.4f}\n")
+                    if step > 0 and (step % a.ckpt_every == 0 or last_step):
+                        self.save(step, val_loss)
+            if (step > 0 and step % a.sample_every == 0) or last_step:
+                eval_step = True
+                self.sample()
+            loss_accum, norm, lr = self.train_step(step)
+            if self.device_type == "cuda":
+                torch.cuda.synchronize()
+            dt = time.time() - t0
+            tokens_processed = a.B * a.T * self.grad_accum_steps * self.info.world_size
+            tps = tokens_processed / dt
+            if not eval_step:
+                self.step_times.append(dt)
+            if self.master:
+                print(f"step {step:5d} | loss: {loss_accum.item():.6f} | lr {lr:.4e} | norm: {norm:.4f} | "
+                      f"dt: {dt*1000:.2f}ms | tok/sec: {tps:.2f}")
+                with open(self.log_file, "a") as f:
+                    f.write(f"{step} train {loss_accum.item():.6f}\n")
+                if metrics:
+                    metrics.write(json.dumps({"step": step, "loss": loss_accum.item(), "lr": lr,
+                                              "norm": float(norm), "dt_ms": dt * 1000, "tok_s": tps,
+                                              "eval_step": eval_step}) + "\n")
+                    metrics.flush()
+        if self.master and self.step_times:
+            ts = sorted(self.step_times[1:] or self.step_times)
+            med = ts[len(ts) // 2]
+            print(f"steady-state median step {med*1000:.1f} ms, "
+                  f"{a.B * a.T * self.grad_accum_steps * self.info.world_size / med:.1f} tok/s "
+                  f"(excluding eval/sample steps)")
+        if metrics:
+            metrics.close()
+        destroy()
+
+
+_ = (asdict, field, contextlib, math)

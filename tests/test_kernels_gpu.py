@@ -1,0 +1,294 @@
+"""Native HIP kernels vs the PyTorch fp32 references (SURVEY.md §4 'Op oracles' / 'Autograd').
+
+Every test runs the same bf16 inputs through (a) the gfx950 kernel path and (b) the reference
+path (ops/reference.py, fp32 math), forward and backward, and compares with bf16 tolerances:
+relative L2 error of the whole tensor, plus a max-abs bound.
+"""
+import math
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from mamba_distributed_amd.ops import reference as R
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def leaf(t):
+    return t.detach().clone().requires_grad_(True)
+
+
+def run_both(fn_native, fn_ref, inputs, grad_seed=0):
+    """Run fwd+bwd on cloned leaves; returns (out_n, out_r, grads_n, grads_r)."""
+    xn = [leaf(t) if (t is not None and t.is_floating_point()) else t for t in inputs]
+    xr = [leaf(t) if (t is not None and t.is_floating_point()) else t for t in inputs]
+    on = fn_native(*xn)
+    os.environ["MAMBA_AMD_FORCE_REFERENCE"] = "1"
+    try:
+        orf = fn_ref(*xr)
+    finally:
+        os.environ.pop("MAMBA_AMD_FORCE_REFERENCE")
+    on_t = on if isinstance(on, torch.Tensor) else on[0]
+    or_t = orf if isinstance(orf, torch.Tensor) else orf[0]
+    g = torch.Generator(device=on_t.device).manual_seed(grad_seed)
+    go = torch.randn(on_t.shape, generator=g, device=on_t.device, dtype=torch.float32).to(on_t.dtype)
+    on_t.backward(go)
+    or_t.backward(go.to(or_t.dtype))
+    gn = [t.grad if isinstance(t, torch.Tensor) and t.requires_grad else None for t in xn]
+    gr = [t.grad if isinstance(t, torch.Tensor) and t.requires_grad else None for t in xr]
+    return on, orf, gn, gr
+
+
+# ------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("D", [256, 768, 1040])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_add_rmsnorm(cuda, D, with_res):
+    from mamba_distributed_amd.ops.norm import rms_norm_fn
+    torch.manual_seed(0)
+    M = 333
+    x = torch.randn(M, D, device=cuda, dtype=torch.bfloat16)
+    r = torch.randn(M, D, device=cuda, dtype=torch.float32) if with_res else None
+    w = torch.rand(D, device=cuda) + 0.5
+
+    def f(x, w, r):
+        y, res = rms_norm_fn(x, w, None, residual=r, prenorm=True, residual_in_fp32=True, eps=1e-5)
+        return y.float() * 1.0 + res * 0.37
+
+    on, orf, gn, gr = run_both(f, f, [x, w, r])
+    assert rel(on, orf) < 1e-2
+    for a, b in zip(gn, gr):
+        if b is not None:
+            assert rel(a, b) < 2e-2, (rel(a, b))
+
+
+@pytest.mark.parametrize("nbg", [False, True])
+@pytest.mark.parametrize("D,G", [(1536, 1536), (512, 256)])
+def test_gated_rmsnorm(cuda, nbg, D, G):
+    from mamba_distributed_amd.ops.norm import rmsnorm_gated_fn
+    torch.manual_seed(1)
+    M = 257
+    big = torch.randn(M, 2 * D + 64, device=cuda, dtype=torch.bfloat16)
+    x = torch.randn(M, D, device=cuda, dtype=torch.bfloat16)
+    w = torch.rand(D, device=cuda) + 0.5
+
+    def f(x, zbig, w):
+        return rmsnorm_gated_fn(x, zbig[:, 64:64 + D], w, 1e-5, G, nbg)
+
+    on, orf, gn, gr = run_both(f, f, [x, big, w])
+    assert rel(on, orf) < 1e-2
+    for a, b in zip(gn, gr):
+        assert rel(a, b) < 2e-2
+
+
+@pytest.mark.parametrize("layout", ["cf", "cl"])
+@pytest.mark.parametrize("L", [1024, 77])
+def test_conv1d(cuda, layout, L):
+    from mamba_distributed_amd.ops.conv1d import causal_conv1d_fn
+    torch.manual_seed(2)
+    b, d, W = 3, 384, 4
+    if layout == "cf":
+        base = torch.randn(b, 2 * d, L, device=cuda, dtype=torch.bfloat16)   # x = first half of channels
+    else:
+        base = torch.randn(b, L, 2 * d + 40, device=cuda, dtype=torch.bfloat16)  # x = column slice
+    w = torch.randn(d, 1, W, device=cuda) * 0.5
+    bias = torch.randn(d, device=cuda) * 0.1
+
+    def f(base, w, bias):
+        x = base[:, :d] if layout == "cf" else base[:, :, 40:40 + d].transpose(1, 2)
+        return causal_conv1d_fn(x, w, bias, "silu")
+
+    on, orf, gn, gr = run_both(f, f, [base, w, bias])
+    assert rel(on, orf) < 1e-2
+    for a, b_ in zip(gn, gr):
+        assert rel(a, b_) < 2e-2
+
+
+def test_cross_entropy(cuda):
+    from mamba_distributed_amd.ops.cross_entropy import cross_entropy, fused_linear_cross_entropy
+    torch.manual_seed(3)
+    M, V, d = 300, 50304, 64
+    logits = (torch.randn(M, V, device=cuda) * 3).to(torch.bfloat16)
+    t = torch.randint(0, V, (M,), device=cuda)
+    t[::7] = -100
+    on, orf, gn, gr = run_both(lambda l: cross_entropy(l, t), lambda l: cross_entropy(l, t), [logits])
+    assert abs(on.item() - orf.item()) < 2e-3 * abs(orf.item())
+    assert rel(gn[0], gr[0]) < 2e-2
+    h = torch.randn(M, d, device=cuda, dtype=torch.bfloat16)
+    W = torch.randn(V, d, device=cuda) * 0.05
+    on, orf, gn, gr = run_both(lambda h, W: fused_linear_cross_entropy(h, W, t),
+                               lambda h, W: fused_linear_cross_entropy(h, W, t), [h, W])
+    assert abs(on.item() - orf.item()) < 5e-3 * abs(orf.item())
+    assert rel(gn[0], gr[0]) < 3e-2 and rel(gn[1], gr[1]) < 3e-2
+
+
+def _ssd_inputs(cuda, b, L, H, G, N, seed=0, strided=True):
+    g = torch.Generator(device=cuda).manual_seed(seed)
+    P = 64
+    width = H * P + 2 * G * N + (24 if strided else 0)
+    buf = torch.randn(b, L, width, generator=g, device=cuda).to(torch.bfloat16)
+    off = 24 if strided else 0
+    x = buf[..., off:off + H * P].unflatten(-1, (H, P))
+    Bm = buf[..., off + H * P: off + H * P + G * N].unflatten(-1, (G, N)) * 0.5
+    Cm = buf[..., off + H * P + G * N:].unflatten(-1, (G, N)) * 0.5
+    dt = (torch.randn(b, L, H, generator=g, device=cuda) * 0.5 - 1.0).to(torch.bfloat16)
+    A = -torch.rand(H, generator=g, device=cuda) * 8 - 0.5
+    D = torch.randn(H, generator=g, device=cuda)
+    dt_bias = torch.randn(H, generator=g, device=cuda) * 0.3
+    return x.contiguous() if not strided else x, dt, A, Bm, Cm, D, dt_bias
+
+
+@pytest.mark.parametrize("b,L,H,G,N", [(2, 256, 4, 1, 128), (1, 200, 8, 2, 64), (2, 70, 6, 1, 128)])
+def test_ssd_fwd_bwd(cuda, b, L, H, G, N):
+    from mamba_distributed_amd.ops.ssd import mamba_chunk_scan_combined
+    x, dt, A, Bm, Cm, D, dt_bias = _ssd_inputs(cuda, b, L, H, G, N)
+
+    def f(x, dt, A, Bm, Cm, D, dt_bias):
+        return mamba_chunk_scan_combined(x, dt, A, Bm, Cm, 64, D=D, dt_bias=dt_bias, dt_softplus=True)
+
+    on, orf, gn, gr = run_both(f, f, [x, dt, A, Bm, Cm, D, dt_bias])
+    assert rel(on, orf) < 2e-2, rel(on, orf)
+    names = ["x", "dt", "A", "B", "C", "D", "dt_bias"]
+    for nm, a, b_ in zip(names, gn, gr):
+        assert rel(a, b_) < 3e-2, (nm, rel(a, b_))
+
+
+def test_ssd_initial_and_final_states(cuda):
+    from mamba_distributed_amd.ops.ssd import mamba_chunk_scan_combined
+    x, dt, A, Bm, Cm, D, dt_bias = _ssd_inputs(cuda, 2, 192, 4, 1, 128, seed=5)
+    init = torch.randn(2, 4, 64, 128, device=cuda) * 0.2
+
+    def f(x, dt, Bm, Cm, init):
+        y, fin = mamba_chunk_scan_combined(x, dt, A, Bm, Cm, 64, D=D, dt_bias=dt_bias, dt_softplus=True,
+                                           initial_states=init, return_final_states=True)
+        return y.float().sum(-1) * 0 + y.float().mean(-1) + fin.sum((-1, -2))[:, None, :].float() * 1e-2
+
+    on, orf, gn, gr = run_both(f, f, [x, dt, Bm, Cm, init])
+    assert rel(on, orf) < 2e-2
+    for a, b_ in zip(gn, gr):
+        assert rel(a, b_) < 3e-2
+
+
+def test_ssd_deterministic(cuda):
+    from mamba_distributed_amd.ops.ssd import mamba_chunk_scan_combined
+    x, dt, A, Bm, Cm, D, dt_bias = _ssd_inputs(cuda, 2, 256, 8, 1, 128, seed=7)
+    outs = []
+    for _ in range(2):
+        xs = [leaf(t) for t in (x, dt, Bm, Cm)]
+        y = mamba_chunk_scan_combined(xs[0], xs[1], A, xs[2], xs[3], 64, D=D, dt_bias=dt_bias, dt_softplus=True)
+        y.float().square().sum().backward()
+        outs.append([y] + [t.grad for t in xs])
+    for a, b_ in zip(*outs):
+        assert torch.equal(a, b_)
+
+
+def test_mamba2_inner(cuda):
+    from mamba_distributed_amd.ops.ssd import mamba2_inner_fn
+    torch.manual_seed(4)
+    b, L, H, P, N, G = 2, 300, 8, 64, 128, 1
+    di = H * P
+    dproj = 2 * di + 2 * G * N + H
+    zx = torch.randn(b, L, dproj, device=cuda).to(torch.bfloat16)
+    conv_w = torch.randn(di + 2 * G * N, 1, 4, device=cuda) * 0.3
+    conv_b = torch.randn(di + 2 * G * N, device=cuda) * 0.1
+    dt_bias = torch.randn(H, device=cuda) * 0.3
+    A = -torch.rand(H, device=cuda) * 8 - 0.5
+    D = torch.randn(H, device=cuda)
+    nw = torch.rand(di, device=cuda) + 0.5
+
+    def f(zx, conv_w, conv_b, dt_bias, A, D, nw):
+        return mamba2_inner_fn(zx, conv_w, conv_b, dt_bias, A, D, nw, 1e-5, P, G, N)
+
+    on, orf, gn, gr = run_both(f, f, [zx, conv_w, conv_b, dt_bias, A, D, nw])
+    assert rel(on, orf) < 2e-2
+    for i, (a, b_) in enumerate(zip(gn, gr)):
+        assert rel(a, b_) < 3e-2, (i, rel(a, b_))
+
+
+@pytest.mark.parametrize("L", [512, 700])
+@pytest.mark.parametrize("with_z", [True, False])
+def test_selective_scan(cuda, L, with_z):
+    from mamba_distributed_amd.ops.selective_scan import selective_scan_fn
+    torch.manual_seed(5)
+    b, d, n = 2, 96, 16
+    u = torch.randn(b, d, L, device=cuda).to(torch.bfloat16)
+    delta = (torch.randn(b, d, L, device=cuda) * 0.5 - 1).to(torch.bfloat16)
+    A = -torch.rand(d, n, device=cuda) * 4 - 0.1
+    Bm = torch.randn(b, 1, n, L, device=cuda).to(torch.bfloat16)
+    Cm = torch.randn(b, 1, n, L, device=cuda).to(torch.bfloat16)
+    D = torch.randn(d, device=cuda)
+    z = torch.randn(b, d, L, device=cuda).to(torch.bfloat16) if with_z else None
+    db = torch.randn(d, device=cuda) * 0.3
+
+    def f(u, delta, A, Bm, Cm, D, z, db):
+        return selective_scan_fn(u, delta, A, Bm, Cm, D, z=z, delta_bias=db, delta_softplus=True)
+
+    on, orf, gn, gr = run_both(f, f, [u, delta, A, Bm, Cm, D, z, db])
+    assert rel(on, orf) < 2e-2, rel(on, orf)
+    names = ["u", "delta", "A", "B", "C", "D", "z", "db"]
+    for nm, a, b_ in zip(names, gn, gr):
+        if b_ is not None:
+            assert rel(a, b_) < 3e-2, (nm, rel(a, b_))
+
+
+@pytest.mark.parametrize("layer", ["Mamba1", "Mamba2"])
+def test_model_native_vs_reference(cuda, layer):
+    from mamba_distributed_amd import LMHeadModel, MambaConfig
+    torch.manual_seed(0)
+    cfg = MambaConfig(d_model=256, n_layer=2, vocab_size=1024, ssm_cfg={"layer": layer})
+    m = LMHeadModel(cfg, device=cuda)
+    x = torch.randint(0, 1024, (2, 192), device=cuda)
+    y = torch.randint(0, 1024, (2, 192), device=cuda)
+
+    def lossgrad(force_ref):
+        if force_ref:
+            os.environ["MAMBA_AMD_FORCE_REFERENCE"] = "1"
+        try:
+            m.zero_grad(set_to_none=True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                _, loss = m(x, y)
+            loss.backward()
+            return loss.item(), {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+        finally:
+            os.environ.pop("MAMBA_AMD_FORCE_REFERENCE", None)
+
+    ln, gn = lossgrad(False)
+    lr, gr = lossgrad(True)
+    assert abs(ln - lr) < 1e-2 * abs(lr), (ln, lr)
+    bad = {n: rel(gn[n], gr[n]) for n in gr if rel(gn[n], gr[n]) > 5e-2}
+    assert not bad, bad
+
+
+def test_decode_update_ops(cuda):
+    from mamba_distributed_amd.ops.conv1d import causal_conv1d_update
+    from mamba_distributed_amd.ops.selective_scan import selective_state_update
+    torch.manual_seed(6)
+    b, c = 3, 96
+    x = torch.randn(b, c, device=cuda).to(torch.bfloat16)
+    st = torch.randn(b, c, 3, device=cuda).to(torch.bfloat16)
+    w = torch.randn(c, 1, 4, device=cuda)
+    bias = torch.randn(c, device=cuda)
+    st_r = st.clone()
+    o = causal_conv1d_update(x, st, w, bias, "silu")
+    o_r = R.causal_conv1d_update_ref(x, st_r, w.view(c, 4), bias, "silu")
+    assert rel(o, o_r) < 1e-2 and torch.equal(st, st_r)
+    # Mamba-2 form
+    H, P, N, G = 4, 64, 128, 1
+    s = torch.randn(b, H, P, N, device=cuda)
+    s_r = s.clone()
+    xx = torch.randn(b, H, P, device=cuda).to(torch.bfloat16)
+    dt = torch.randn(b, H, device=cuda).to(torch.bfloat16)
+    A = -torch.rand(H, device=cuda) * 4
+    Bm = torch.randn(b, G, N, device=cuda).to(torch.bfloat16)
+    Cm = torch.randn(b, G, N, device=cuda).to(torch.bfloat16)
+    D = torch.randn(H, device=cuda)
+    dtb = torch.randn(H, device=cuda)
+    y = selective_state_update(s, xx, dt, A, Bm, Cm, D, None, dtb, True)
+    y_r = R.selective_state_update_ref(s_r, xx, dt, A, Bm, Cm, D, None, dtb, True)
+    assert rel(y, y_r) < 1e-2 and rel(s, s_r) < 1e-4
