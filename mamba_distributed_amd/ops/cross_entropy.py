@@ -85,6 +85,6 @@ class _FusedLinearCEFn(torch.autograd.Function):
 def fused_linear_cross_entropy(h, weight, targets, ignore_index=-100, compute_dtype=torch.bfloat16):
     if _ext.use_native(h):
         return _FusedLinearCEFn.apply(h, weight, targets, ignore_index, compute_dtype)
-    logits = F.linear(h, weight)
+    logits = F.linear(h, weight.to(h.dtype))
     return F.cross_entropy(logits.float().view(-1, logits.size(-1)), targets.view(-1),
                            ignore_index=ignore_index)

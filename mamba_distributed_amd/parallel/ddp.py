@@ -10,7 +10,7 @@ amortised.  Defaults chosen for that regime:
   * ``bucket_cap_mb=100``  (4x fewer collectives than 25 MB; a 100 MB bucket moves in
     ~0.5-1 ms over xGMI, still much shorter than the backward of the 64 layers it overlaps)
   * ``gradient_as_bucket_view=True``  (grads live in the buckets: no copy in / copy out)
-  * ``static_graph=True`` when the model's graph is fixed (Mamba LMs are)
+  * ``static_graph`` off: validation / sampling run no-grad forwards through the same wrapper
   * optional bf16 compression hook (``grad_comm_dtype="bf16"``) halves the bytes on the links.
 
 Gradient accumulation uses ``require_backward_grad_sync`` exactly like the reference
@@ -26,7 +26,7 @@ from .dist import DistInfo
 
 
 def wrap_ddp(model: torch.nn.Module, info: DistInfo, bucket_cap_mb: float = 100.0,
-             grad_comm_dtype: str = "fp32", static_graph: bool = True,
+             grad_comm_dtype: str = "fp32", static_graph: bool = False,
              gradient_as_bucket_view: bool = True):
     if not info.ddp:
         return model

@@ -1,0 +1,66 @@
+"""DataLoaderLite semantics (reference dataloader.py:14-52) and checkpoint compatibility (§5.4)."""
+import os
+
+import numpy as np
+import torch
+
+from mamba_distributed_amd import LMHeadModel, MambaConfig, preset
+from mamba_distributed_amd.data.loader import DataLoaderLite, write_synthetic_shards
+from mamba_distributed_amd.utils.checkpoint import (config_from_checkpoint, latest_checkpoint, load_checkpoint,
+                                                    save_checkpoint)
+
+
+def test_loader_rank_striding_and_rollover(tmp_path):
+    root = str(tmp_path / "shards")
+    write_synthetic_shards(root, n_train=2, n_val=1, tokens_per_shard=1000, vocab_size=500)
+    shards = sorted(p for p in os.listdir(root) if "train" in p)
+    toks = [np.load(os.path.join(root, s)).astype(np.int64) for s in shards]
+    B, T, W = 2, 8, 3
+    loaders = [DataLoaderLite(B, T, r, W, "train", r == 0, data_root=root, verbose=False) for r in range(W)]
+    for r, ld in enumerate(loaders):
+        x, y = ld.next_batch()
+        start = B * T * r
+        assert torch.equal(x.flatten(), torch.from_numpy(toks[0][start:start + B * T]))
+        assert torch.equal(y.flatten(), torch.from_numpy(toks[0][start + 1:start + B * T + 1]))
+    # step until rollover: position advances by B*T*W per call; shard switches when the next window overflows
+    ld = loaders[1]
+    seen_shard1 = False
+    for _ in range(30):
+        x, y = ld.next_batch()
+        if ld.current_shard == 1:
+            seen_shard1 = True
+            break
+    assert seen_shard1
+    x, _ = ld.next_batch()
+    assert torch.equal(x.flatten(), torch.from_numpy(toks[1][B * T * 1:B * T * 2]))
+    ld.reset()
+    assert ld.current_shard == 0 and ld.current_position == B * T * 1
+
+
+def test_checkpoint_roundtrip_default_torch_load(tmp_path):
+    torch.manual_seed(0)
+    cfg = preset("mamba2-tiny")
+    m = LMHeadModel(cfg, device="cpu", enc=object())
+    opt = m.configure_optimizers(0.1, 1e-3, "cpu", False)
+    path = str(tmp_path / "log" / "model_00010.pt")
+    save_checkpoint(path, m, 10, 3.21, optimizer=opt, loader_state=[{"current_shard": 0, "current_position": 5}])
+    ck = torch.load(path)  # torch >= 2.6 default weights_only=True must work (reference A5)
+    assert set(["model", "config", "step", "val_loss"]) <= set(ck)
+    assert isinstance(ck["config"], dict) and ck["step"] == 10
+    cfg2 = config_from_checkpoint(ck)
+    assert cfg2 == cfg
+    m2 = LMHeadModel(cfg2, device="cpu", enc=object())
+    m2.load_state_dict(ck["model"])
+    for (k, a), (_, b) in zip(m.state_dict().items(), m2.state_dict().items()):
+        assert torch.equal(a, b), k
+    assert latest_checkpoint(str(tmp_path / "log")) == path
+    assert load_checkpoint(path)["val_loss"] == 3.21
+
+
+def test_reference_default_config_checkpoint_keys(tmp_path):
+    """A checkpoint of MambaConfig(d_model=768, vocab_size=50304) has exactly the §2.8 keys."""
+    with torch.device("meta"):
+        m = LMHeadModel(MambaConfig(d_model=768, vocab_size=50304), device="meta", enc=object())
+    keys = list(m.state_dict().keys())
+    assert keys[0] == "backbone.embedding.weight" and keys[-1] == "lm_head.weight"
+    assert len(keys) == 1 + 64 * 10 + 1 + 1

@@ -1,0 +1,91 @@
+"""Multi-process data parallelism on CPU with gloo (SURVEY.md §4 'Distributed (fake multi-node)').
+
+torchrun --nproc-per-node 2 (gloo) on the tiny Mamba-2 config (the BASELINE 'CPU/gloo world_size=2'
+plumbing config) must produce the same parameters as a single process that sees the same global
+batch (DDP averages gradients; DataLoaderLite's rank striding splits the global batch exactly).
+A second test runs two torchrun "nodes" on localhost (--nnodes 2 --node-rank i).
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from mamba_distributed_amd.data.loader import write_synthetic_shards
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.slow
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+COMMON = ["--model", "mamba2-tiny", "--n-layer", "2", "--T", "32", "--total-batch-size", "256", "--steps", "3",
+          "--val-every", "100", "--val-steps", "1", "--ckpt-every", "1000", "--sample-every", "1000",
+          "--warmup-steps", "2", "--device-type", "cpu", "--backend", "gloo"]
+
+
+def _env():
+    return dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2", MAMBA_AMD_FORCE_REFERENCE="1")
+
+
+def _run_single(tmp, data, B):
+    log = str(tmp / "single")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "train.py"), *COMMON, "--B", str(B),
+                        "--data-root", data, "--log-dir", log], capture_output=True, text=True, env=_env(), timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return torch.load(os.path.join(log, "model_00002.pt"))["model"], r.stdout
+
+
+def _assert_close_sd(a, b):
+    # AdamW turns fp-roundoff-sized gradient differences on (near-)zero-gradient entries into
+    # O(lr) updates, so parameters agree to a few lr (6e-4) after 3 steps, not to fp32 epsilon;
+    # the loss trajectories (compared separately) agree to ~1e-5 relative.
+    for k in a:
+        torch.testing.assert_close(a[k], b[k], rtol=0, atol=3e-3, msg=k)
+
+
+def _losses(stdout):
+    return [float(l.split("loss: ")[1].split(" ")[0]) for l in stdout.splitlines() if l.startswith("step ")]
+
+
+def test_ddp_gloo_world2_matches_single_process(tmp_path):
+    data = str(tmp_path / "data")
+    write_synthetic_shards(data, n_train=1, n_val=1, tokens_per_shard=1 << 14, vocab_size=50304)
+    sd_single, out_single = _run_single(tmp_path, data, B=4)
+    log = str(tmp_path / "ddp")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "train.py"), *COMMON,
+           "--B", "2", "--data-root", data, "--log-dir", log]
+    r = subprocess.run(cmd, capture_output=True, text=True, env=_env(), timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "=> calculated gradient accumulation steps: 2" in r.stdout
+    sd_ddp = torch.load(os.path.join(log, "model_00002.pt"))["model"]
+    _assert_close_sd(sd_ddp, sd_single)
+    la, lb = _losses(r.stdout), _losses(out_single)
+    assert len(la) == 3 and all(abs(x - y) < 1e-4 * abs(y) for x, y in zip(la, lb)), (la, lb)
+
+
+def test_two_node_rendezvous_on_localhost(tmp_path):
+    data = str(tmp_path / "data")
+    write_synthetic_shards(data, n_train=1, n_val=1, tokens_per_shard=1 << 14, vocab_size=50304)
+    port = _port()
+    log = str(tmp_path / "nodes")
+    procs = []
+    for node in range(2):
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "2", "--node-rank", str(node),
+               "--nproc-per-node", "1", "--master-addr", "127.0.0.1", "--master-port", str(port),
+               os.path.join(ROOT, "train.py"), *COMMON, "--B", "2", "--data-root", data, "--log-dir", log]
+        procs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=_env()))
+    outs = [p.communicate(timeout=600) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-3000:]
+    sd_single, _ = _run_single(tmp_path, data, B=4)
+    _assert_close_sd(torch.load(os.path.join(log, "model_00002.pt"))["model"], sd_single)
