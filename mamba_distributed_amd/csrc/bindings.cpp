@@ -206,13 +206,12 @@ std::tuple<Tensor, Tensor, Tensor> conv1d_cf_bwd(Tensor x, Tensor weight, option
               dx.scalar_type() == x.scalar_type(), "dx_out layout");
   const int W = (int)w.size(1);
   auto part = at::empty({B, D, W + 1}, x.options().dtype(at::kFloat));
-  auto dw = at::empty({D, W}, x.options().dtype(at::kFloat));
-  auto db = at::empty({D}, x.options().dtype(at::kFloat));
+  auto dwb = at::empty({D, W + 1}, x.options().dtype(at::kFloat));  // [taps | bias] per channel
   HIPCHK(mamba_amd::launch_conv_cf_bwd(x.data_ptr(), dcode(x.scalar_type()), x.stride(0), x.stride(1), w.data_ptr<float>(),
                                        fptr(bb), dout.data_ptr(), dout.stride(0), dout.stride(1), dx.data_ptr(),
-                                       dx.stride(0), dx.stride(1), part.data_ptr<float>(), dw.data_ptr<float>(),
-                                       db.data_ptr<float>(), (int)B, (int)D, (int)L, W, silu, cur_stream()));
-  return {dx, dw, db};
+                                       dx.stride(0), dx.stride(1), part.data_ptr<float>(), dwb.data_ptr<float>(),
+                                       nullptr, (int)B, (int)D, (int)L, W, silu, cur_stream()));
+  return {dx, dwb.narrow(1, 0, W), dwb.select(1, W)};
 }
 
 Tensor conv1d_cl_fwd(Tensor x, Tensor weight, optional<Tensor> bias, bool silu) {
@@ -246,13 +245,12 @@ std::tuple<Tensor, Tensor, Tensor> conv1d_cl_bwd(Tensor x, Tensor weight, option
               dx.scalar_type() == x.scalar_type(), "dx_out layout");
   const int W = (int)w.size(1);
   auto part = at::empty({mamba_amd::conv_cl_bwd_partial_rows((int)B, (int)L), C, W + 1}, x.options().dtype(at::kFloat));
-  auto dw = at::empty({C, W}, x.options().dtype(at::kFloat));
-  auto db = at::empty({C}, x.options().dtype(at::kFloat));
+  auto dwb = at::empty({C, W + 1}, x.options().dtype(at::kFloat));  // [taps | bias] per channel
   HIPCHK(mamba_amd::launch_conv_cl_bwd(x.data_ptr(), dcode(x.scalar_type()), x.stride(0), x.stride(1), w.data_ptr<float>(),
                                        fptr(bb), dout.data_ptr(), dout.stride(0), dout.stride(1), dx.data_ptr(),
-                                       dx.stride(0), dx.stride(1), part.data_ptr<float>(), dw.data_ptr<float>(),
-                                       db.data_ptr<float>(), (int)B, (int)L, (int)C, W, silu, cur_stream()));
-  return {dx, dw, db};
+                                       dx.stride(0), dx.stride(1), part.data_ptr<float>(), dwb.data_ptr<float>(),
+                                       nullptr, (int)B, (int)L, (int)C, W, silu, cur_stream()));
+  return {dx, dwb.narrow(1, 0, W), dwb.select(1, W)};
 }
 
 Tensor conv1d_update(Tensor x, Tensor conv_state, Tensor weight, optional<Tensor> bias, bool silu) {

@@ -191,18 +191,6 @@ __global__ __launch_bounds__(256) void conv_cf_bwd_k(const T* __restrict__ x, in
   }
 }
 
-// part: (B, D, W+1) -> dw (D, W), db (D): sum over batch in fixed order
-__global__ void conv_reduce_batch_k(const float* __restrict__ part, int Bn, int Dn, int W, float* __restrict__ dw,
-                                    float* __restrict__ db) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // over D*(W+1)
-  if (i >= Dn * (W + 1)) return;
-  float s = 0.f;
-  for (int b = 0; b < Bn; ++b) s += part[(int64_t)b * Dn * (W + 1) + i];
-  const int d = i / (W + 1), k = i % (W + 1);
-  if (k < W) dw[d * W + k] = s;
-  else if (db) db[d] = s;
-}
-
 // =========================== channel-last ================================================
 constexpr int CL_T = 16;  // timesteps per wave tile
 
@@ -447,9 +435,7 @@ static hipError_t cf_bwd(const T* x, int64_t sxb, int64_t sxd, const float* w, c
                             sdb, sdd, part, Bn, Dn, L, silu);
   });
   MAMBA_HIP_CHECK(hipGetLastError());
-  const int n = Dn * (Wd + 1);
-  hipLaunchKernelGGL(conv_reduce_batch_k, dim3((n + 255) / 256), dim3(256), 0, st, part, Bn, Dn, Wd, dw, db);
-  return hipGetLastError();
+  return launch_colsum(part, Bn, Dn * (Wd + 1), dw, st);  // dw buffer holds (D, W+1): [w taps | bias]
 }
 
 hipError_t launch_conv_cf_bwd(const void* x, int dt, int64_t sxb, int64_t sxd, const float* w, const float* bias,
@@ -492,17 +478,6 @@ hipError_t launch_conv_cl_fwd(const void* x, int dt, int64_t sxb, int64_t sxl, c
 
 int conv_cl_bwd_partial_rows(int Bn, int L) { return Bn * ((L + 4 * CLB_T - 1) / (4 * CLB_T)); }
 
-__global__ void conv_reduce_rows_k(const float* __restrict__ part, int nrows, int C, int W, float* __restrict__ dw,
-                                   float* __restrict__ db) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // over C*(W+1)
-  if (i >= C * (W + 1)) return;
-  float s = 0.f;
-  for (int r = 0; r < nrows; ++r) s += part[(int64_t)r * C * (W + 1) + i];
-  const int c = i / (W + 1), k = i % (W + 1);
-  if (k < W) dw[c * W + k] = s;
-  else if (db) db[c] = s;
-}
-
 template <typename T>
 static hipError_t cl_bwd(const T* x, int64_t sxb, int64_t sxl, const float* w, const float* bias, const T* g,
                          int64_t sgb, int64_t sgl, T* dx, int64_t sdb, int64_t sdl, float* part, float* dw, float* db,
@@ -518,10 +493,7 @@ static hipError_t cl_bwd(const T* x, int64_t sxb, int64_t sxl, const float* w, c
                             sdb, sdl, part, Bn, L, C, silu);
   });
   MAMBA_HIP_CHECK(hipGetLastError());
-  const int n = C * (Wd + 1);
-  hipLaunchKernelGGL(conv_reduce_rows_k, dim3((n + 255) / 256), dim3(256), 0, st, part,
-                     conv_cl_bwd_partial_rows(Bn, L), C, Wd, dw, db);
-  return hipGetLastError();
+  return launch_colsum(part, conv_cl_bwd_partial_rows(Bn, L), C * (Wd + 1), dw, st);  // (C, W+1)
 }
 
 hipError_t launch_conv_cl_bwd(const void* x, int dt, int64_t sxb, int64_t sxl, const float* w, const float* bias,

@@ -121,4 +121,28 @@ __device__ __forceinline__ void store_tile(bf16_t* g, int64_t gs, const bf16_t* 
   }
 }
 
+// ---- cross-lane reductions without LDS: DPP butterflies inside a 16-lane row --------------------
+#define MAMBA_DPP(v, ctrl) __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, (v)), (ctrl), 0xF, 0xF, false))
+// sum over the 16 lanes of each row (lanes 16r..16r+15); every lane of the row gets the sum
+__device__ __forceinline__ float row_sum16(float v) {
+  v += MAMBA_DPP(v, 0xB1);   // quad_perm [1,0,3,2]
+  v += MAMBA_DPP(v, 0x4E);   // quad_perm [2,3,0,1]
+  v += MAMBA_DPP(v, 0x141);  // row_half_mirror
+  v += MAMBA_DPP(v, 0x140);  // row_mirror
+  return v;
+}
+// sum over the 4 rows (lanes l, l^16, l^32, l^48)
+__device__ __forceinline__ float rows_sum4(float v) {
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
+// read 4 consecutive rows r0+4g..+3 of column c0 + (l&15) from a [rows][ld] bf16 LDS tile (the rows /
+// column an MFMA accumulator lane owns) with one ds_read_b64_tr_b16
+__device__ __forceinline__ bf16x4 acc_rows4(const bf16_t* T, int ld, int r0, int c0) {
+  const int l = threadIdx.x & 63, g = l >> 4, li = l & 15;
+  return tr4(T + (r0 + 4 * g + (li >> 2)) * ld + c0 + 4 * (li & 3));
+}
+
 }  // namespace mamba_amd

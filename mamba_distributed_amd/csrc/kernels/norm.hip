@@ -143,13 +143,37 @@ __global__ __launch_bounds__(256) void add_rmsnorm_bwd_k(
   block_dw_partial<NCH>(acc, part, D, lds);
 }
 
-__global__ __launch_bounds__(256) void sum_rows_k(const float* __restrict__ part, int nrows, int D,
-                                                  float* __restrict__ out) {
-  const int col = blockIdx.x * blockDim.x + threadIdx.x;
-  if (col >= D) return;
+// out[c] = sum_r part[r][c] in a fixed order.  Block = 64 columns x 16 row-groups (1024 threads);
+// each thread sums a strided row subset (independent loads -> deep memory-level parallelism), the
+// 16 group sums are combined through LDS in index order -> bitwise deterministic.
+__global__ __launch_bounds__(1024) void colsum_k(const float* __restrict__ part, int nrows, int ncols,
+                                                 float* __restrict__ out) {
+  __shared__ float red[16][65];
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   float s = 0.f;
-  for (int r = 0; r < nrows; ++r) s += part[(int64_t)r * D + col];
-  out[col] = s;
+  if (c < ncols) {
+    int r = rg;
+    for (; r + 48 < nrows; r += 64) {
+      const float a0 = part[(int64_t)r * ncols + c], a1 = part[(int64_t)(r + 16) * ncols + c];
+      const float a2 = part[(int64_t)(r + 32) * ncols + c], a3 = part[(int64_t)(r + 48) * ncols + c];
+      s += (a0 + a1) + (a2 + a3);
+    }
+    for (; r < nrows; r += 16) s += part[(int64_t)r * ncols + c];
+  }
+  red[rg][cl] = s;
+  __syncthreads();
+  if (rg == 0 && c < ncols) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][cl];
+    out[c] = t;
+  }
+}
+
+hipError_t launch_colsum(const float* part, int nrows, int ncols, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(colsum_k, dim3((ncols + 63) / 64), dim3(1024), 0, st, part, nrows, ncols, out);
+  return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------
@@ -300,6 +324,109 @@ __global__ __launch_bounds__(256) void gated_rmsnorm_bwd_k(
   block_dw_partial<NCH>(acc, part, D, lds);
 }
 
+// bf16 fast path of the gated backward: x / z / dy stay PACKED (4 bf16 = 2 VGPRs per chunk) between
+// the statistics pass and the output pass and every derived value is recomputed -> ~1/2 the VGPRs of
+// the generic kernel, 2x the resident waves for this HBM-bound kernel.
+__device__ __forceinline__ void unpack4(uint2 v, float (&o)[4]) {
+  o[0] = __uint_as_float(v.x << 16); o[1] = __uint_as_float(v.x & 0xffff0000u);
+  o[2] = __uint_as_float(v.y << 16); o[3] = __uint_as_float(v.y & 0xffff0000u);
+}
+template <int NCH, bool NBG>
+__global__ __launch_bounds__(256) void gated_rmsnorm_bwd_bf16_k(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, int64_t sx, const bf16_t* __restrict__ z,
+    int64_t sz, const float* __restrict__ w, const float* __restrict__ rstd, bf16_t* __restrict__ dx, int64_t sdx,
+    bf16_t* __restrict__ dz, int64_t sdz, float* __restrict__ part, int64_t M, int D, int G) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int lane = threadIdx.x & 63;
+  const int ngroups = D / G;
+  float acc[NCH][4];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[c][k] = 0.f;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < M; row += (int64_t)gridDim.x * 4) {
+    uint2 px[NCH], pz[NCH], pg[NCH];
+    float dotc[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = (lane + 64 * c) * 4;
+      dotc[c] = 0.f;
+      if (col < D) {
+        px[c] = *reinterpret_cast<const uint2*>(x + row * sx + col);
+        pz[c] = *reinterpret_cast<const uint2*>(z + row * sz + col);
+        pg[c] = *reinterpret_cast<const uint2*>(dy + row * D + col);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = (lane + 64 * c) * 4;
+      if (col < D) {
+        float xv[4], zv[4], g[4], wv[4];
+        unpack4(px[c], xv); unpack4(pz[c], zv); unpack4(pg[c], g);
+        ld4<float>(w + col, wv);
+        const float rs = rstd[row * ngroups + col / G];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float s = siluf_(zv[k]);
+          const float xh = (NBG ? xv[k] : xv[k] * s) * rs;
+          const float dyn = NBG ? g[k] * s : g[k];
+          dotc[c] += dyn * wv[k] * xh;
+          acc[c][k] += dyn * xh;
+        }
+      }
+    }
+    // make the packed inputs opaque here so the compiler recomputes pass-1 values in pass 2 instead of
+    // keeping ~6 unpacked fp32 copies per element live across the reduction (register pressure)
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+      asm volatile("" : "+v"(px[c].x), "+v"(px[c].y), "+v"(pz[c].x), "+v"(pz[c].y), "+v"(pg[c].x), "+v"(pg[c].y));
+    float dotg[NCH];
+    for (int gi = 0; gi < ngroups; ++gi) {
+      float sacc = 0.f;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const int col = (lane + 64 * c) * 4;
+        if (col < D && col / G == gi) sacc += dotc[c];
+      }
+      sacc = wave_sum(sacc) / (float)G;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const int col = (lane + 64 * c) * 4;
+        if (col / G == gi) dotg[c] = sacc;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = (lane + 64 * c) * 4;
+      if (col < D) {
+        float xv[4], zv[4], g[4], wv[4], ox[4], oz[4];
+        unpack4(px[c], xv); unpack4(pz[c], zv); unpack4(pg[c], g);
+        ld4<float>(w + col, wv);
+        const float rs = rstd[row * ngroups + col / G];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float sg = sigmoidf_(zv[k]);
+          const float s = zv[k] * sg;
+          const float dsilu = sg * (1.f + zv[k] * (1.f - sg));
+          const float xh = (NBG ? xv[k] : xv[k] * s) * rs;
+          const float dyn = NBG ? g[k] * s : g[k];
+          const float dbase = (dyn * wv[k] - xh * dotg[c]) * rs;
+          if (NBG) {
+            ox[k] = dbase;
+            oz[k] = g[k] * xh * wv[k] * dsilu;
+          } else {
+            ox[k] = dbase * s;
+            oz[k] = dbase * xv[k] * dsilu;
+          }
+        }
+        st4<bf16_t>(dx + row * sdx + col, ox);
+        st4<bf16_t>(dz + row * sdz + col, oz);
+      }
+    }
+  }
+  block_dw_partial<NCH>(acc, part, D, lds);
+}
+
 // ------------------------------------------------------------------------------------------
 // host launchers
 #define NCH_SWITCH(D, ...)                                               \
@@ -320,7 +447,7 @@ __global__ __launch_bounds__(256) void gated_rmsnorm_bwd_k(
 
 static int bwd_grid(int64_t M) {
   int64_t g = (M + 3) / 4;
-  return (int)(g < 1024 ? (g < 1 ? 1 : g) : 1024);
+  return (int)(g < 2048 ? (g < 1 ? 1 : g) : 2048);
 }
 
 hipError_t launch_add_rmsnorm_fwd(const void* x, int xdt, int64_t sx, const void* res, int rdt, int64_t sr,
@@ -343,8 +470,7 @@ hipError_t launch_add_rmsnorm_bwd(const void* dy, int ydt, const void* dro, int 
   NCH_SWITCH(D, hipLaunchKernelGGL((add_rmsnorm_bwd_k<NCH>), dim3(g), dim3(256), lds, st, dy, ydt, dro, drodt, ro,
                                    rodt, w, rstd, dx, xdt, dres, rdt, part, M, D));
   MAMBA_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(sum_rows_k, dim3((D + 255) / 256), dim3(256), 0, st, part, g, D, dw);
-  return hipGetLastError();
+  return launch_colsum(part, g, D, dw, st);
 }
 
 hipError_t launch_gated_rmsnorm_fwd(const void* x, int xdt, int64_t sx, const void* z, int zdt, int64_t sz,
@@ -368,7 +494,16 @@ hipError_t launch_gated_rmsnorm_bwd(const void* dy, int ydt, const void* x, int 
                                     bool nbg, hipStream_t st) {
   const int g = bwd_grid(M);
   const size_t lds = 4 * (size_t)D * sizeof(float);
-  if (nbg) {
+  const bool fast = ydt == kBF16 && xdt == kBF16 && zdt == kBF16;
+  if (fast && nbg) {
+    NCH_SWITCH(D, hipLaunchKernelGGL((gated_rmsnorm_bwd_bf16_k<NCH, true>), dim3(g), dim3(256), lds, st,
+                                     (const bf16_t*)dy, (const bf16_t*)x, sx, (const bf16_t*)z, sz, w, rstd,
+                                     (bf16_t*)dx, sdx, (bf16_t*)dz, sdz, part, M, D, G));
+  } else if (fast) {
+    NCH_SWITCH(D, hipLaunchKernelGGL((gated_rmsnorm_bwd_bf16_k<NCH, false>), dim3(g), dim3(256), lds, st,
+                                     (const bf16_t*)dy, (const bf16_t*)x, sx, (const bf16_t*)z, sz, w, rstd,
+                                     (bf16_t*)dx, sdx, (bf16_t*)dz, sdz, part, M, D, G));
+  } else if (nbg) {
     NCH_SWITCH(D, hipLaunchKernelGGL((gated_rmsnorm_bwd_k<NCH, true>), dim3(g), dim3(256), lds, st, dy, ydt, x,
                                      xdt, sx, z, zdt, sz, w, rstd, dx, sdx, dz, sdz, part, M, D, G));
   } else {
@@ -376,8 +511,7 @@ hipError_t launch_gated_rmsnorm_bwd(const void* dy, int ydt, const void* x, int 
                                      xdt, sx, z, zdt, sz, w, rstd, dx, sdx, dz, sdz, part, M, D, G));
   }
   MAMBA_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(sum_rows_k, dim3((D + 255) / 256), dim3(256), 0, st, part, g, D, dw);
-  return hipGetLastError();
+  return launch_colsum(part, g, D, dw, st);
 }
 
 int norm_bwd_partial_rows(int64_t M) { return bwd_grid(M); }

@@ -63,6 +63,50 @@ __global__ __launch_bounds__(256) void ssd_cumsum_k(SSDArgs a) {
   a.cum[o] = x;
 }
 
+// ---- register-staged tile loads (issue early, write to LDS late: latency hides under the MFMAs) ----
+// one 64 x 64 bf16 tile = 512 16-B chunks; with NT threads each thread owns 512/NT chunks
+template <int NT>
+struct Tile64 {
+  static constexpr int K = 512 / NT;
+  uint4 v[K];
+  __device__ __forceinline__ void load(const bf16_t* g, int64_t gs, int valid) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int idx = threadIdx.x + k * NT, r = idx >> 3, c = (idx & 7) * 8;
+      v[k] = r < valid ? *reinterpret_cast<const uint4*>(g + (int64_t)r * gs + c) : make_uint4(0, 0, 0, 0);
+    }
+  }
+  __device__ __forceinline__ void store(bf16_t* lds, int ld, const float* rowscale = nullptr) const {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int idx = threadIdx.x + k * NT, r = idx >> 3, c = (idx & 7) * 8;
+      uint4 d = v[k];
+      if (rowscale) {
+        float f[8];
+        ld8bf(reinterpret_cast<const bf16_t*>(&d), f);
+        const float s = rowscale[r];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] *= s;
+        st8bf(reinterpret_cast<bf16_t*>(&d), f);
+      }
+      *reinterpret_cast<uint4*>(lds + r * ld + c) = d;
+    }
+  }
+};
+// a 64 x N bf16 state tile (P x N) as N/64 column blocks of Tile64
+template <int NT, int N>
+struct TileState {
+  Tile64<NT> t[N / 64];
+  __device__ __forceinline__ void load(const bf16_t* g) {
+#pragma unroll
+    for (int i = 0; i < N / 64; ++i) t[i].load(g + 64 * i, N, 64);
+  }
+  __device__ __forceinline__ void store(bf16_t* lds, int ld) const {
+#pragma unroll
+    for (int i = 0; i < N / 64; ++i) t[i].store(lds + 64 * i, ld);
+  }
+};
+
 // ============================== K1: chunk states + state passing (forward) =================
 template <int N>
 __global__ __launch_bounds__(256) void ssd_state_fwd_k(SSDArgs a) {
@@ -75,6 +119,8 @@ __global__ __launch_bounds__(256) void ssd_state_fwd_k(SSDArgs a) {
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const float* cumbh = a.cum + ((int64_t)b * a.H + h) * a.Lp;
   const float* dtbh = a.dtp + ((int64_t)b * a.H + h) * a.Lp;
+  const bf16_t* xg = a.x + (int64_t)b * a.sxb + (int64_t)h * a.sxh;
+  const bf16_t* bg = a.Bm + (int64_t)b * a.sBb + (int64_t)g * a.sBg + ns * 64;
   f32x4 acc[4];
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) {
@@ -87,22 +133,30 @@ __global__ __launch_bounds__(256) void ssd_state_fwd_k(SSDArgs a) {
       }
     }
   }
+  Tile64<256> px, pb;
+  float pw = 0.f, pcl = 0.f;
+  px.load(xg, a.sxl, min(Q, a.L));
+  pb.load(bg, a.sBl, min(Q, a.L));
+  if (threadIdx.x < Q) { pw = cumbh[threadIdx.x] ; pcl = cumbh[Q - 1]; pw = __expf(pcl - pw) * dtbh[threadIdx.x]; }
   for (int c = 0; c < a.nc; ++c) {
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) acc_to_lds(Os, LD64, 16 * w, 16 * nt, acc[nt]);
-    if (threadIdx.x < Q) {
-      const int t = c * Q + threadIdx.x;
-      wrow[threadIdx.x] = __expf(cumbh[c * Q + Q - 1] - cumbh[t]) * dtbh[t];
-    }
+    if (threadIdx.x < Q) wrow[threadIdx.x] = pw;
+    const float decay = __expf(cumbh[c * Q + Q - 1]);
     __syncthreads();
     store_tile<P, 64>(a.states + ((((int64_t)b * a.nc + c) * a.H + h) * P) * N + ns * 64, N, Os, LD64, P);
-    const int valid = min(Q, a.L - c * Q);
-    stage_tile<Q, 64>(Xs, LD64, a.x + (int64_t)b * a.sxb + (int64_t)c * Q * a.sxl + (int64_t)h * a.sxh, a.sxl, valid,
-                      wrow);
-    stage_tile<Q, 64>(Bs, LD64, a.Bm + (int64_t)b * a.sBb + (int64_t)c * Q * a.sBl + (int64_t)g * a.sBg + ns * 64,
-                      a.sBl, valid);
+    px.store(Xs, LD64, wrow);
+    pb.store(Bs, LD64);
+    if (c + 1 < a.nc) {  // prefetch chunk c+1 while this chunk's MFMAs run
+      const int valid = min(Q, a.L - (c + 1) * Q);
+      px.load(xg + (int64_t)(c + 1) * Q * a.sxl, a.sxl, valid);
+      pb.load(bg + (int64_t)(c + 1) * Q * a.sBl, a.sBl, valid);
+      if (threadIdx.x < Q) {
+        const int t = (c + 1) * Q + threadIdx.x;
+        pw = __expf(cumbh[(c + 1) * Q + Q - 1] - cumbh[t]) * dtbh[t];
+      }
+    }
     __syncthreads();
-    const float decay = __expf(cumbh[c * Q + Q - 1]);
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) acc[nt] *= decay;
 #pragma unroll
@@ -111,7 +165,6 @@ __global__ __launch_bounds__(256) void ssd_state_fwd_k(SSDArgs a) {
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) acc[nt] = mfma16(A, frag_tr(Bs, LD64, 32 * ks, 16 * nt), acc[nt]);
     }
-    __syncthreads();
   }
   if (a.final_state) {
 #pragma unroll
@@ -139,6 +192,20 @@ __global__ __launch_bounds__(256) void ssd_scan_fwd_k(SSDArgs a) {
   const int h0 = hgi * a.HG, g = h0 / (a.H / a.G);
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int valid = min(Q, a.L - c * Q);
+  // prefetch head h0's tiles before the shared C/B work
+  Tile64<256> px;
+  TileState<256, N> ps;
+  float pc = 0.f, pd = 0.f;
+  auto prefetch = [&](int h) {
+    px.load(a.x + (int64_t)b * a.sxb + (int64_t)c * Q * a.sxl + (int64_t)h * a.sxh, a.sxl, valid);
+    ps.load(a.states + ((((int64_t)b * a.nc + c) * a.H + h) * P) * N);
+    if (threadIdx.x < Q) {
+      const int64_t bh = ((int64_t)b * a.H + h) * a.Lp + (int64_t)c * Q + threadIdx.x;
+      pc = a.cum[bh];
+      pd = a.dtp[bh];
+    }
+  };
+  prefetch(h0);
   stage_tile<Q, N>(Cs, LDN, a.Cm + (int64_t)b * a.sCb + (int64_t)c * Q * a.sCl + (int64_t)g * a.sCg, a.sCl, valid);
   stage_tile<Q, N>(Bs, LDN, a.Bm + (int64_t)b * a.sBb + (int64_t)c * Q * a.sBl + (int64_t)g * a.sBg, a.sBl, valid);
   __syncthreads();
@@ -153,18 +220,20 @@ __global__ __launch_bounds__(256) void ssd_scan_fwd_k(SSDArgs a) {
         cbt[jt] = mfma16(frag_kc(Bs, LDN, 16 * jt, 32 * ks), frag_kc(Cs, LDN, 16 * w, 32 * ks), cbt[jt]);
     }
   }
+  const float Dh0 = 0.f;
+  (void)Dh0;
   for (int hh = 0; hh < a.HG; ++hh) {
     const int h = h0 + hh;
-    const int64_t bh = ((int64_t)b * a.H + h) * a.Lp + (int64_t)c * Q;
+    __syncthreads();  // previous head's readers of Xs / XDs(Os) / Ss / cumr are done
     if (threadIdx.x < Q) {
-      cumr[threadIdx.x] = a.cum[bh + threadIdx.x];
-      dtr[threadIdx.x] = a.dtp[bh + threadIdx.x];
+      cumr[threadIdx.x] = pc;
+      dtr[threadIdx.x] = pd;
     }
+    px.store(Xs, LD64);
+    ps.store(Ss, LDN);
     __syncthreads();
-    const bf16_t* xg = a.x + (int64_t)b * a.sxb + (int64_t)c * Q * a.sxl + (int64_t)h * a.sxh;
-    stage_tile<Q, 64>(Xs, LD64, xg, a.sxl, valid);
-    stage_tile<Q, 64>(XDs, LD64, xg, a.sxl, valid, dtr);
-    stage_tile<P, N>(Ss, LDN, a.states + ((((int64_t)b * a.nc + c) * a.H + h) * P) * N, N, P);
+    px.store(XDs, LD64, dtr);
+    if (hh + 1 < a.HG) prefetch(h + 1);
     __syncthreads();
     f32x4 acc[4];
     // y_off = e^{cum_i} C_i . S^T
@@ -202,17 +271,19 @@ __global__ __launch_bounds__(256) void ssd_scan_fwd_k(SSDArgs a) {
       }
     }
     const float Dh = a.D ? a.D[h] : 0.f;
+    bf16x4 xr[4];
+#pragma unroll
+    for (int pt = 0; pt < 4; ++pt) xr[pt] = acc_rows4(Xs, LD64, 16 * w, 16 * pt);
     __syncthreads();  // every wave is done reading XDs before it becomes the output tile
 #pragma unroll
     for (int pt = 0; pt < 4; ++pt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int i = 16 * w + 4 * (l >> 4) + r, p = 16 * pt + (l & 15);
-        Os[i * LD64 + p] = f2bf(acc[pt][r] + Dh * bf2f(Xs[i * LD64 + p]));
+        Os[i * LD64 + p] = f2bf(acc[pt][r] + Dh * (float)xr[pt][r]);
       }
     __syncthreads();
     store_tile<Q, 64>(a.y + (int64_t)b * a.syb + (int64_t)c * Q * a.syl + (int64_t)h * a.syh, a.syl, Os, LD64, valid);
-    __syncthreads();
   }
 }
 
@@ -227,6 +298,8 @@ __global__ __launch_bounds__(256) void ssd_dstate_bwd_k(SSDArgs a) {
   const int g = h / (a.H / a.G);
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const float* cumbh = a.cum + ((int64_t)b * a.H + h) * a.Lp;
+  const bf16_t* yg = a.dy + (int64_t)b * a.sdyb + (int64_t)h * a.sdyh;
+  const bf16_t* cg = a.Cm + (int64_t)b * a.sCb + (int64_t)g * a.sCg + ns * 64;
   f32x4 acc[4];
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) {
@@ -239,19 +312,30 @@ __global__ __launch_bounds__(256) void ssd_dstate_bwd_k(SSDArgs a) {
       }
     }
   }
+  Tile64<256> py, pcs;
+  float pe = 0.f;
+  {
+    const int c = a.nc - 1, valid = min(Q, a.L - c * Q);
+    py.load(yg + (int64_t)c * Q * a.sdyl, a.sdyl, valid);
+    pcs.load(cg + (int64_t)c * Q * a.sCl, a.sCl, valid);
+    if (threadIdx.x < Q) pe = __expf(cumbh[c * Q + threadIdx.x]);
+  }
   for (int c = a.nc - 1; c >= 0; --c) {
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) acc_to_lds(Os, LD64, 16 * w, 16 * nt, acc[nt]);
-    if (threadIdx.x < Q) er[threadIdx.x] = __expf(cumbh[c * Q + threadIdx.x]);
+    if (threadIdx.x < Q) er[threadIdx.x] = pe;
+    const float decay = __expf(cumbh[c * Q + Q - 1]);
     __syncthreads();
     store_tile<P, 64>(a.dstates + ((((int64_t)b * a.nc + c) * a.H + h) * P) * N + ns * 64, N, Os, LD64, P);
-    const int valid = min(Q, a.L - c * Q);
-    stage_tile<Q, 64>(Ys, LD64, a.dy + (int64_t)b * a.sdyb + (int64_t)c * Q * a.sdyl + (int64_t)h * a.sdyh, a.sdyl,
-                      valid, er);
-    stage_tile<Q, 64>(Cs, LD64, a.Cm + (int64_t)b * a.sCb + (int64_t)c * Q * a.sCl + (int64_t)g * a.sCg + ns * 64,
-                      a.sCl, valid);
+    py.store(Ys, LD64, er);
+    pcs.store(Cs, LD64);
+    if (c > 0) {
+      const int cn = c - 1, valid = min(Q, a.L - cn * Q);
+      py.load(yg + (int64_t)cn * Q * a.sdyl, a.sdyl, valid);
+      pcs.load(cg + (int64_t)cn * Q * a.sCl, a.sCl, valid);
+      if (threadIdx.x < Q) pe = __expf(cumbh[cn * Q + threadIdx.x]);
+    }
     __syncthreads();
-    const float decay = __expf(cumbh[c * Q + Q - 1]);
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) acc[nt] *= decay;
 #pragma unroll
@@ -260,7 +344,6 @@ __global__ __launch_bounds__(256) void ssd_dstate_bwd_k(SSDArgs a) {
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) acc[nt] = mfma16(A, frag_tr(Cs, LD64, 32 * ks, 16 * nt), acc[nt]);
     }
-    __syncthreads();
   }
   if (a.dinit) {
 #pragma unroll
@@ -274,23 +357,15 @@ __global__ __launch_bounds__(256) void ssd_dstate_bwd_k(SSDArgs a) {
 }
 
 // ============================== K4: per-chunk backward =======================================
-__device__ __forceinline__ float sum16(float v) {  // over the 16 lanes l&15 of a lane group
-  v += __shfl_xor(v, 1, 64);
-  v += __shfl_xor(v, 2, 64);
-  v += __shfl_xor(v, 4, 64);
-  v += __shfl_xor(v, 8, 64);
-  return v;
-}
-__device__ __forceinline__ float sum_groups(float v) {  // over the 4 lane groups l>>4
-  v += __shfl_xor(v, 16, 64);
-  v += __shfl_xor(v, 32, 64);
-  return v;
-}
-
+// 512 threads: wave w4 = wid & 3 owns row/column tile w4 of the 64x64 chunk matrices; the two
+// halves (wid >> 2) split the p-tiles (dX, BdS, Yoff) and the n-tiles (dB/dC accumulators).  The
+// M / dM tiles of column w4 are computed by both halves (cheap: 2 MFMAs per tile) so neither has to
+// wait for the other; only half 0 accumulates dCB and the G row/col sums.
 template <int N>
-__global__ __launch_bounds__(256) void ssd_chunk_bwd_k(SSDArgs a) {
+__global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
   constexpr int LDN = N + 8;
   constexpr int NT = N / 16;
+  constexpr int NTH = NT / 2;
   __shared__ __attribute__((aligned(16))) bf16_t Cs[Q * LDN];
   __shared__ __attribute__((aligned(16))) bf16_t Bs[Q * LDN];
   __shared__ __attribute__((aligned(16))) bf16_t Ss[P * LDN];
@@ -298,16 +373,34 @@ __global__ __launch_bounds__(256) void ssd_chunk_bwd_k(SSDArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t Xs[Q * LD64];
   __shared__ __attribute__((aligned(16))) bf16_t dYs[Q * LD64];
   __shared__ __attribute__((aligned(16))) bf16_t Os[Q * LD64];
-  __shared__ float cumr[Q], dtr[Q], dcum[Q], ddtd[Q], red[4];
+  __shared__ float cumr[Q], dtr[Q], dcum[Q], ddtd[Q], red[16];
   const int c = blockIdx.x, hgi = blockIdx.y, b = blockIdx.z;
   const int h0 = hgi * a.HG, g = h0 / (a.H / a.G);
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int w = wid & 3, half = wid >> 2;
+  const int li = l & 15, lg = l >> 4;
   const int valid = min(Q, a.L - c * Q);
+  Tile64<512> px, py;
+  TileState<512, N> ps, pds;
+  float pc = 0.f, pd = 0.f;
+  auto prefetch = [&](int h) {
+    px.load(a.x + (int64_t)b * a.sxb + (int64_t)c * Q * a.sxl + (int64_t)h * a.sxh, a.sxl, valid);
+    py.load(a.dy + (int64_t)b * a.sdyb + (int64_t)c * Q * a.sdyl + (int64_t)h * a.sdyh, a.sdyl, valid);
+    const int64_t soff = ((((int64_t)b * a.nc + c) * a.H + h) * P) * N;
+    ps.load(a.states + soff);
+    pds.load(a.dstates + soff);
+    if (threadIdx.x < Q) {
+      const int64_t bh = ((int64_t)b * a.H + h) * a.Lp + (int64_t)c * Q + threadIdx.x;
+      pc = a.cum[bh];
+      pd = a.dtp[bh];
+    }
+  };
+  prefetch(h0);
   stage_tile<Q, N>(Cs, LDN, a.Cm + (int64_t)b * a.sCb + (int64_t)c * Q * a.sCl + (int64_t)g * a.sCg, a.sCl, valid);
   stage_tile<Q, N>(Bs, LDN, a.Bm + (int64_t)b * a.sBb + (int64_t)c * Q * a.sBl + (int64_t)g * a.sBg, a.sBl, valid);
   __syncthreads();
-  // CB tiles for the wave's column tile (j in tile w): rows i in tile I >= w
-  f32x4 cb[4], dcb[4], dBa[NT], dCa[NT];
+  // CB tiles for the column tile w: rows i in tile I >= w
+  f32x4 cb[4], dcb[4], dBa[NTH], dCa[NTH];
 #pragma unroll
   for (int I = 0; I < 4; ++I) {
     cb[I] = zero4();
@@ -319,33 +412,32 @@ __global__ __launch_bounds__(256) void ssd_chunk_bwd_k(SSDArgs a) {
     }
   }
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) {
+  for (int nt = 0; nt < NTH; ++nt) {
     dBa[nt] = zero4();
     dCa[nt] = zero4();
   }
-  const int jl = 16 * w + (l & 15);  // this lane's column index in the M / dM tiles
+  const int jl = 16 * w + li;  // this lane's column index in the M / dM tiles
   for (int hh = 0; hh < a.HG; ++hh) {
     const int h = h0 + hh;
-    const int64_t bh = ((int64_t)b * a.H + h) * a.Lp + (int64_t)c * Q;
+    __syncthreads();  // previous head fully consumed (LDS tiles, dcum, Os)
     if (threadIdx.x < Q) {
-      cumr[threadIdx.x] = a.cum[bh + threadIdx.x];
-      dtr[threadIdx.x] = a.dtp[bh + threadIdx.x];
+      cumr[threadIdx.x] = pc;
+      dtr[threadIdx.x] = pd;
       dcum[threadIdx.x] = 0.f;
       ddtd[threadIdx.x] = 0.f;
     }
-    if (threadIdx.x < 4) red[threadIdx.x] = 0.f;
-    stage_tile<Q, 64>(Xs, LD64, a.x + (int64_t)b * a.sxb + (int64_t)c * Q * a.sxl + (int64_t)h * a.sxh, a.sxl, valid);
-    stage_tile<Q, 64>(dYs, LD64, a.dy + (int64_t)b * a.sdyb + (int64_t)c * Q * a.sdyl + (int64_t)h * a.sdyh, a.sdyl,
-                      valid);
-    const int64_t soff = ((((int64_t)b * a.nc + c) * a.H + h) * P) * N;
-    stage_tile<P, N>(Ss, LDN, a.states + soff, N, P);
-    stage_tile<P, N>(dSs, LDN, a.dstates + soff, N, P);
+    if (threadIdx.x < 16) red[threadIdx.x] = 0.f;
+    px.store(Xs, LD64);
+    py.store(dYs, LD64);
+    ps.store(Ss, LDN);
+    pds.store(dSs, LDN);
     __syncthreads();
+    if (hh + 1 < a.HG) prefetch(h + 1);
     const float cl = cumr[Q - 1];
     const float Ah = a.A[h];
     const float Dh = a.D ? a.D[h] : 0.f;
     const float dtj = dtr[jl], cumj = cumr[jl];
-    // ---- (1)(2) dM, M, dCB, G row/col sums
+    // ---- (1)(2) dM, M; half 0: dCB and the G row/col sums
     f32x4 m[4];
     float colG = 0.f;
 #pragma unroll
@@ -356,122 +448,124 @@ __global__ __launch_bounds__(256) void ssd_chunk_bwd_k(SSDArgs a) {
 #pragma unroll
         for (int ks = 0; ks < P / 32; ++ks)
           dm = mfma16(frag_kc(dYs, LD64, 16 * I, 32 * ks), frag_kc(Xs, LD64, 16 * w, 32 * ks), dm);
+        float gr[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int i = 16 * I + 4 * (l >> 4) + r;
+          const int i = 16 * I + 4 * lg + r;
           const float Lij = (jl <= i) ? __expf(cumr[i] - cumj) : 0.f;
           const float dmv = dm[r] * dtj;
           const float mv = cb[I][r] * Lij;
           m[I][r] = mv;
           dcb[I][r] += dmv * Lij;
-          const float G = dmv * mv;
-          colG += G;
-          const float rs = sum16(G);
-          if ((l & 15) == 0) atomicAdd(&dcum[i], rs);
+          gr[r] = dmv * mv;
+          colG += gr[r];
+        }
+        if (half == 0) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float rs = row_sum16(gr[r]);
+            if (li == 0) atomicAdd(&dcum[16 * I + 4 * lg + r], rs);
+          }
         }
       }
     }
-    colG = sum_groups(colG);
-    if (l < 16) atomicAdd(&dcum[jl], -colG);
-    // ---- (3) dXdt = M^T dY   and (4) BdS = B dS^T     (rows j of tile w, cols p)
-    f32x4 dxd[4], bds[4];
+    if (half == 0) {
+      colG = rows_sum4(colG);
+      if (l < 16) atomicAdd(&dcum[jl], -colG);
+    }
+    // ---- (3) dXdt = M^T dY, (4) BdS = B dS^T, (6) Yoff = C S^T  for this half's p-tiles
+    f32x4 dxd[2], bds[2], yo[2];
 #pragma unroll
-    for (int pt = 0; pt < 4; ++pt) {
-      dxd[pt] = zero4();
-      bds[pt] = zero4();
+    for (int q = 0; q < 2; ++q) {
+      dxd[q] = zero4();
+      bds[q] = zero4();
+      yo[q] = zero4();
     }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       if (2 * ks + 1 >= w) {
         const bf16x8 Af = acc_frag(m[2 * ks], m[2 * ks + 1]);
 #pragma unroll
-        for (int pt = 0; pt < 4; ++pt) dxd[pt] = mfma16(Af, frag_tr_perm(dYs, LD64, 32 * ks, 16 * pt), dxd[pt]);
+        for (int q = 0; q < 2; ++q)
+          dxd[q] = mfma16(Af, frag_tr_perm(dYs, LD64, 32 * ks, 16 * (2 * half + q)), dxd[q]);
       }
     }
 #pragma unroll
     for (int ks = 0; ks < N / 32; ++ks) {
-      const bf16x8 Af = frag_kc(Bs, LDN, 16 * w, 32 * ks);
+      const bf16x8 Ab = frag_kc(Bs, LDN, 16 * w, 32 * ks);
+      const bf16x8 Ac = frag_kc(Cs, LDN, 16 * w, 32 * ks);
 #pragma unroll
-      for (int pt = 0; pt < 4; ++pt) bds[pt] = mfma16(Af, frag_kc(dSs, LDN, 16 * pt, 32 * ks), bds[pt]);
+      for (int q = 0; q < 2; ++q) {
+        bds[q] = mfma16(Ab, frag_kc(dSs, LDN, 16 * (2 * half + q), 32 * ks), bds[q]);
+        yo[q] = mfma16(Ac, frag_kc(Ss, LDN, 16 * (2 * half + q), 32 * ks), yo[q]);
+      }
     }
-    // ---- (5) dX, ddt_direct, U, dD
-    float ddp[4] = {0.f, 0.f, 0.f, 0.f}, up[4] = {0.f, 0.f, 0.f, 0.f}, dDp = 0.f;
+    // ---- (5) dX, ddt_direct, U, dD ; (6) dcum Yoff term   (rows j = i = 16w + 4lg + r)
+    bf16x4 xr[2], yr[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      xr[q] = acc_rows4(Xs, LD64, 16 * w, 16 * (2 * half + q));
+      yr[q] = acc_rows4(dYs, LD64, 16 * w, 16 * (2 * half + q));
+    }
+    float dDp = 0.f, usum = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int j = 16 * w + 4 * (l >> 4) + r;
+      const int j = 16 * w + 4 * lg + r;
       const float dt_ = dtr[j];
       const float ej = __expf(cl - cumr[j]);
       const float wj = ej * dt_;
+      const float ei = __expf(cumr[j]);
+      float ddp = 0.f, up = 0.f, yp = 0.f;
 #pragma unroll
-      for (int pt = 0; pt < 4; ++pt) {
-        const int p = 16 * pt + (l & 15);
-        const float xv = bf2f(Xs[j * LD64 + p]);
-        const float dyv = bf2f(dYs[j * LD64 + p]);
-        Os[j * LD64 + p] = f2bf(dt_ * dxd[pt][r] + wj * bds[pt][r] + Dh * dyv);
-        ddp[r] += xv * (dxd[pt][r] + ej * bds[pt][r]);
-        up[r] += wj * xv * bds[pt][r];
+      for (int q = 0; q < 2; ++q) {
+        const int p = 16 * (2 * half + q) + li;
+        const float xv = (float)xr[q][r];
+        const float dyv = (float)yr[q][r];
+        Os[j * LD64 + p] = f2bf(dt_ * dxd[q][r] + wj * bds[q][r] + Dh * dyv);
+        ddp += xv * (dxd[q][r] + ej * bds[q][r]);
+        up += xv * bds[q][r];
+        yp += yo[q][r] * dyv;
         dDp += xv * dyv;
       }
-    }
-    float usum = 0.f;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int j = 16 * w + 4 * (l >> 4) + r;
-      const float dd = sum16(ddp[r]);
-      const float uu = sum16(up[r]);
-      if ((l & 15) == 0) {
-        ddtd[j] = dd;
-        atomicAdd(&dcum[j], -uu);
+      ddp = row_sum16(ddp);
+      up = row_sum16(up) * wj;
+      yp = row_sum16(yp) * ei;
+      if (li == 0) {
+        atomicAdd(&ddtd[j], ddp);
+        atomicAdd(&dcum[j], yp - up);
       }
-      usum += uu;
+      usum += up;
     }
-    usum = sum_groups(usum);  // every lane now holds the wave's total U over its 16 rows
+    usum = rows_sum4(usum);  // the wave's U total over its 16 rows (x its p-half)
     if (l == 0) atomicAdd(&dcum[Q - 1], usum);
     dDp = wave_sum(dDp);
     if (l == 0) atomicAdd(&red[0], dDp);
-    // ---- (6) Yoff term of dcum: rows i of tile w
+    // ---- (7) dC_off += (e^{cum_i} dY) S , (8) dB_off += (w_j x) dS   for this half's n-tiles
     {
-      float yp[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int pt = 0; pt < 4; ++pt) {
-        f32x4 yo = zero4();
-#pragma unroll
-        for (int ks = 0; ks < N / 32; ++ks)
-          yo = mfma16(frag_kc(Cs, LDN, 16 * w, 32 * ks), frag_kc(Ss, LDN, 16 * pt, 32 * ks), yo);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int i = 16 * w + 4 * (l >> 4) + r, p = 16 * pt + (l & 15);
-          yp[r] += yo[r] * bf2f(dYs[i * LD64 + p]);
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = 16 * w + 4 * (l >> 4) + r;
-        const float s = sum16(yp[r]);
-        if ((l & 15) == 0) atomicAdd(&dcum[i], s * __expf(cumr[i]));
-      }
-    }
-    // ---- (7) dC_off += (e^{cum_i} dY) S     (8) dB_off += (w_j x) dS
-    {
-      const float ei = __expf(cumr[jl]);  // A-operand row index = 16w + (l&15)
+      const float ei = __expf(cumr[jl]);
       const float wl = __expf(cl - cumr[jl]) * dtr[jl];
 #pragma unroll
       for (int ks = 0; ks < P / 32; ++ks) {
         const bf16x8 Ay = scale_frag(frag_kc(dYs, LD64, 16 * w, 32 * ks), ei);
         const bf16x8 Ax = scale_frag(frag_kc(Xs, LD64, 16 * w, 32 * ks), wl);
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
-          dCa[nt] = mfma16(Ay, frag_tr(Ss, LDN, 32 * ks, 16 * nt), dCa[nt]);
-          dBa[nt] = mfma16(Ax, frag_tr(dSs, LDN, 32 * ks, 16 * nt), dBa[nt]);
+        for (int nt = 0; nt < NTH; ++nt) {
+          const int n0 = 16 * (half * NTH + nt);
+          dCa[nt] = mfma16(Ay, frag_tr(Ss, LDN, 32 * ks, n0), dCa[nt]);
+          dBa[nt] = mfma16(Ax, frag_tr(dSs, LDN, 32 * ks, n0), dBa[nt]);
         }
       }
     }
-    // ---- (9) e^{cl} sum(dS o S) -> dcum[last]
+    // ---- (9) e^{cl} sum(dS o S) -> dcum[last]   (16-B LDS reads)
     {
       float s = 0.f;
-      for (int v = threadIdx.x; v < P * N; v += 256) {
-        const int p = v / N, n = v % N;
-        s += bf2f(Ss[p * LDN + n]) * bf2f(dSs[p * LDN + n]);
+      for (int v = threadIdx.x; v < P * N / 8; v += 512) {
+        const int p = v / (N / 8), n = (v % (N / 8)) * 8;
+        float fa[8], fb[8];
+        ld8bf(Ss + p * LDN + n, fa);
+        ld8bf(dSs + p * LDN + n, fb);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s += fa[k] * fb[k];
       }
       s = wave_sum(s);
       if (l == 0) atomicAdd(&dcum[Q - 1], s * __expf(cl));
@@ -480,7 +574,7 @@ __global__ __launch_bounds__(256) void ssd_chunk_bwd_k(SSDArgs a) {
     store_tile<Q, 64>(a.dx + (int64_t)b * a.sdxb + (int64_t)c * Q * a.sdxl + (int64_t)h * a.sdxh, a.sdxl, Os, LD64,
                       valid);
     // ---- (10) dt gradients for this head (wave 0; lane = local step)
-    if (w == 0) {
+    if (wid == 0) {
       float da = dcum[l];
 #pragma unroll
       for (int off = 1; off < 64; off <<= 1) {  // reverse inclusive scan: da_i = sum_{t>=i} dcum_t
@@ -507,22 +601,23 @@ __global__ __launch_bounds__(256) void ssd_chunk_bwd_k(SSDArgs a) {
         a.part_dD[pi] = red[0];
       }
     }
-    __syncthreads();
   }
   // ---- head-group partials
   const int64_t pbase = ((int64_t)b * a.nc + c) * a.nhg + hgi;
+  if (half == 0) {
 #pragma unroll
-  for (int I = 0; I < 4; ++I)
+    for (int I = 0; I < 4; ++I)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 16 * I + 4 * lg + r;
+        a.part_dcb[(pbase * Q + i) * Q + jl] = dcb[I][r];
+      }
+  }
+#pragma unroll
+  for (int nt = 0; nt < NTH; ++nt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int i = 16 * I + 4 * (l >> 4) + r;
-      a.part_dcb[(pbase * Q + i) * Q + jl] = dcb[I][r];
-    }
-#pragma unroll
-  for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = 16 * w + 4 * (l >> 4) + r, n = 16 * nt + (l & 15);
+      const int row = 16 * w + 4 * lg + r, n = 16 * (half * NTH + nt) + li;
       a.part_db[(pbase * Q + row) * N + n] = dBa[nt][r];
       a.part_dc[(pbase * Q + row) * N + n] = dCa[nt][r];
     }
@@ -608,7 +703,7 @@ hipError_t launch_ssd_fwd(const SSDArgs& a, hipStream_t st) {
 hipError_t launch_ssd_bwd(const SSDArgs& a, hipStream_t st) {
   N_SWITCH(a.N, hipLaunchKernelGGL(ssd_dstate_bwd_k<NN>, dim3(NN / 64, a.H, a.B), dim3(256), 0, st, a));
   MAMBA_HIP_CHECK(hipGetLastError());
-  N_SWITCH(a.N, hipLaunchKernelGGL(ssd_chunk_bwd_k<NN>, dim3(a.nc, a.nhg, a.B), dim3(256), 0, st, a));
+  N_SWITCH(a.N, hipLaunchKernelGGL(ssd_chunk_bwd_k<NN>, dim3(a.nc, a.nhg, a.B), dim3(512), 0, st, a));
   MAMBA_HIP_CHECK(hipGetLastError());
   N_SWITCH(a.N, hipLaunchKernelGGL(ssd_dbc_bwd_k<NN>, dim3(a.nc, a.G, a.B), dim3(256), 0, st, a));
   return hipGetLastError();

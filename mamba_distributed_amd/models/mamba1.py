@@ -90,7 +90,7 @@ class _Mamba1InnerFn(torch.autograd.Function):
         dco2 = _flat(du)
         dco2.addmm_(Wx.t(), dx_dbl)                                         # du + W_x^T dx_dbl
         _, dw, db = ops.conv1d_cf_bwd(x, w2, conv_b, _cm(dco2, b, l), True, dxz3[:, :di])
-        return (dxz, dw.view(wshape).to(w2.dtype), db.to(conv_b.dtype) if conv_b is not None else None,
+        return (dxz, dw.reshape(wshape).to(w2.dtype), db.to(conv_b.dtype) if conv_b is not None else None,
                 dWx.to(wx_dtype), dWdt.to(wdt_dtype), ddt_bias, dA, dD, None, None, None)
 
 

@@ -52,7 +52,7 @@ class _CausalConv1dFn(torch.autograd.Function):
             dx = dx.transpose(1, 2)
         else:
             dx, dw, db = ops.conv1d_cf_bwd(x, w2, bias, dout, ctx.silu, None)
-        return dx, dw.view(ctx.wshape).to(w2.dtype), (db.to(bias.dtype) if bias is not None else None), None
+        return dx, dw.reshape(ctx.wshape).to(w2.dtype), (db.to(bias.dtype) if bias is not None else None), None
 
 
 def causal_conv1d_fn(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None,

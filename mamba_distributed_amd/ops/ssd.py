@@ -138,7 +138,7 @@ class _Mamba2InnerFn(torch.autograd.Function):
         _, _, dA, _, _, dD, ddt_bias, _ = g
         xBC = zxbcdt[..., di:di + conv_dim]
         _, dw, db = ops.conv1d_cl_bwd(xBC, w2, conv_b, dxBC_c, True, dz_all[..., di:di + conv_dim])
-        return (dz_all, dw.view(ctx.wshape).to(w2.dtype), db.to(conv_b.dtype) if conv_b is not None else None,
+        return (dz_all, dw.reshape(ctx.wshape).to(w2.dtype), db.to(conv_b.dtype) if conv_b is not None else None,
                 ddt_bias, dA, dD, dnorm_w, None, None, None, None, None, None, None)
 
 
