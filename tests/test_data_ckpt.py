@@ -64,3 +64,13 @@ def test_reference_default_config_checkpoint_keys(tmp_path):
     keys = list(m.state_dict().keys())
     assert keys[0] == "backbone.embedding.weight" and keys[-1] == "lm_head.weight"
     assert len(keys) == 1 + 64 * 10 + 1 + 1
+
+
+def test_plot_loss_parses_reference_format(tmp_path):
+    from mamba_distributed_amd.utils.plot import parse_log, plot
+    log = tmp_path / "log.txt"
+    log.write_text("0 val 10.9911\n0 train 10.991953\n1 train 10.963361\n250 val 6.1\n")
+    d = parse_log(str(log))
+    assert d["val"] == ([0, 250], [10.9911, 6.1]) and d["train"][0] == [0, 1]
+    out = plot(str(log), str(tmp_path / "v.png"))
+    assert (tmp_path / "v.png").exists() and out.endswith("v.png")
