@@ -39,6 +39,7 @@ def main():
     p.add_argument("--grad-comm-dtype", default="fp32")
     p.add_argument("--reference-ops", action="store_true", help="A/B: run the PyTorch reference ops")
     p.add_argument("--no-fused-ce", action="store_true")
+    p.add_argument("--no-tuned-gemms", action="store_true", help="library-default GEMM solutions")
     p.add_argument("--profile-steps", type=int, default=0, help="torch.profiler trace of N extra steps")
     a = p.parse_args()
     if a.reference_ops:
@@ -54,6 +55,8 @@ def main():
     dev = info.device
     assert a.global_batch_tokens % (a.B * a.T * world) == 0
     accum = a.global_batch_tokens // (a.B * a.T * world)
+    from mamba_distributed_amd.utils.gemm_tuning import enable_tuned_gemms
+    tuned = False if a.no_tuned_gemms else enable_tuned_gemms()
     torch.manual_seed(1337)
     cfg = preset(a.model)
     model = LMHeadModel(cfg, device=dev)
@@ -126,6 +129,7 @@ def main():
                 "seq_len": a.T,
                 "parallelism": f"dp{world}",
                 "ops": "pytorch-reference" if a.reference_ops else "native-hip",
+                "gemm_table": "tunableop-gfx950" if tuned else "library-default",
                 "final_loss": round(loss_v, 4),
             },
         }

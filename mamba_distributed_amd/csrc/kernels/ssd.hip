@@ -382,9 +382,11 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
   const int valid = min(Q, a.L - c * Q);
   Tile64<512> px, py;
   TileState<512, N> ps, pds;
-  float pc = 0.f, pd = 0.f;
+  float pc = 0.f, pd = 0.f, praw = 0.f;
   auto prefetch = [&](int h) {
     px.load(a.x + (int64_t)b * a.sxb + (int64_t)c * Q * a.sxl + (int64_t)h * a.sxh, a.sxl, valid);
+    if (threadIdx.x < Q && c * Q + (int)threadIdx.x < a.L)
+      praw = ld_any(a.dt, a.dt_dtype, (int64_t)b * a.sdtb + (int64_t)(c * Q + threadIdx.x) * a.sdtl + (int64_t)h * a.sdth);
     py.load(a.dy + (int64_t)b * a.sdyb + (int64_t)c * Q * a.sdyl + (int64_t)h * a.sdyh, a.sdyl, valid);
     const int64_t soff = ((((int64_t)b * a.nc + c) * a.H + h) * P) * N;
     ps.load(a.states + soff);
@@ -420,6 +422,7 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
   for (int hh = 0; hh < a.HG; ++hh) {
     const int h = h0 + hh;
     __syncthreads();  // previous head fully consumed (LDS tiles, dcum, Os)
+    float rawdt = praw;  // lanes of wave 0 = local steps
     if (threadIdx.x < Q) {
       cumr[threadIdx.x] = pc;
       dtr[threadIdx.x] = pd;
@@ -586,7 +589,7 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
       const int t = c * Q + l;
       float gdt = 0.f;
       if (t < a.L) {
-        float raw = ld_any(a.dt, a.dt_dtype, (int64_t)b * a.sdtb + (int64_t)t * a.sdtl + (int64_t)h * a.sdth);
+        float raw = rawdt;
         if (a.dt_bias) raw += a.dt_bias[h];
         const float v = a.softplus ? softplusf_(raw) : raw;
         const bool inside = (v >= a.dt_min) && (v <= a.dt_max);
