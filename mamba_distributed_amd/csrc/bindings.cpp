@@ -309,11 +309,12 @@ void ssd_common(mamba_amd::SSDArgs& a, const Tensor& x, const Tensor& dt, const 
 std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> ssd_fwd(Tensor x, Tensor dt, Tensor A, Tensor Bm, Tensor Cm,
                                                            optional<Tensor> D, optional<Tensor> dt_bias,
                                                            optional<Tensor> init, int64_t chunk, bool softplus,
-                                                           double dt_min, double dt_max) {
+                                                           double dt_min, double dt_max, bool A_is_log) {
   check_cuda(x, "x");
   at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   mamba_amd::SSDArgs a{};
   ssd_common(a, x, dt, A, Bm, Cm, chunk, softplus, dt_min, dt_max);
+  a.a_log = A_is_log;
   Tensor Af = f32c(A), Df = f32c_opt(D), bf = f32c_opt(dt_bias), If = f32c_opt(init);
   if (Df.defined()) TORCH_CHECK(Df.numel() == a.H, "D must be (h,)");
   if (bf.defined()) TORCH_CHECK(bf.numel() == a.H, "dt_bias must be (h,)");
@@ -336,7 +337,7 @@ std::vector<Tensor> ssd_bwd(Tensor dy, Tensor x, Tensor dt, Tensor A, Tensor Bm,
                             optional<Tensor> dt_bias, optional<Tensor> init, Tensor cum, Tensor dtp, Tensor states,
                             optional<Tensor> dfinal, int64_t chunk, bool softplus, double dt_min, double dt_max,
                             optional<Tensor> dx_out, optional<Tensor> ddt_out, optional<Tensor> dB_out,
-                            optional<Tensor> dC_out) {
+                            optional<Tensor> dC_out, bool A_is_log) {
   check_cuda(x, "x");
   at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   mamba_amd::SSDArgs a{};
@@ -377,12 +378,14 @@ std::vector<Tensor> ssd_bwd(Tensor dy, Tensor x, Tensor dt, Tensor A, Tensor Bm,
   auto part_dcb = at::empty({a.B, a.nc, a.nhg, 64, 64}, fo);
   auto part_db = at::empty({a.B, a.nc, a.nhg, 64, a.N}, fo);
   auto part_dc = at::empty({a.B, a.nc, a.nhg, 64, a.N}, fo);
-  auto part_small = at::empty({3, a.B, a.nc, a.H}, fo);
+  auto part_small = at::empty({a.B * a.nc, 3, a.H}, fo);
   a.part_dcb = part_dcb.data_ptr<float>(); a.part_db = part_db.data_ptr<float>(); a.part_dc = part_dc.data_ptr<float>();
-  a.part_dA = part_small[0].data_ptr<float>(); a.part_dD = part_small[1].data_ptr<float>();
-  a.part_dbias = part_small[2].data_ptr<float>();
+  a.psl = 3 * a.H;
+  a.part_dA = part_small.data_ptr<float>(); a.part_dD = a.part_dA + a.H; a.part_dbias = a.part_dA + 2 * a.H;
+  a.a_log = A_is_log;
   HIPCHK(mamba_amd::launch_ssd_bwd(a, cur_stream()));
-  auto sums = part_small.sum({1, 2});  // (3, H), fixed-order reduction
+  auto sums = at::empty({3, a.H}, fo);  // deterministic column sums over the (b, chunk) rows
+  HIPCHK(mamba_amd::launch_colsum(part_small.data_ptr<float>(), a.B * a.nc, 3 * a.H, sums.data_ptr<float>(), cur_stream()));
   Tensor dA = sums[0].to(A.scalar_type());
   Tensor dD = D.has_value() && D->defined() ? sums[1].to(D->scalar_type()) : at::empty({0}, fo);
   Tensor dbias = dt_bias.has_value() && dt_bias->defined() ? sums[2].to(dt_bias->scalar_type()) : at::empty({0}, fo);
@@ -566,10 +569,11 @@ TORCH_LIBRARY(mamba_amd, m) {
         "-> (Tensor, Tensor, Tensor)");
   m.def("conv1d_update(Tensor x, Tensor(a!) conv_state, Tensor weight, Tensor? bias, bool silu) -> Tensor");
   m.def("ssd_fwd(Tensor x, Tensor dt, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? dt_bias, Tensor? init, "
-        "int chunk, bool softplus, float dt_min, float dt_max) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
+        "int chunk, bool softplus, float dt_min, float dt_max, bool A_is_log=False) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("ssd_bwd(Tensor dy, Tensor x, Tensor dt, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? dt_bias, "
         "Tensor? init, Tensor cum, Tensor dtp, Tensor states, Tensor? dfinal, int chunk, bool softplus, float dt_min, "
-        "float dt_max, Tensor(a!)? dx_out, Tensor(b!)? ddt_out, Tensor(c!)? dB_out, Tensor(d!)? dC_out) -> Tensor[]");
+        "float dt_max, Tensor(a!)? dx_out, Tensor(b!)? ddt_out, Tensor(c!)? dB_out, Tensor(d!)? dC_out, "
+        "bool A_is_log=False) -> Tensor[]");
   m.def("selscan_fwd(Tensor u, Tensor delta, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? z, Tensor? delta_bias, "
         "bool softplus) -> (Tensor, Tensor, Tensor)");
   m.def("selscan_bwd(Tensor dout, Tensor u, Tensor delta, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? z, "

@@ -15,6 +15,7 @@
 //   4 waves (4 time tiles) summed through LDS -> one partial row per block -> fixed-order sum.
 #include "common.h"
 #include "launchers.h"
+#include <type_traits>
 
 namespace mamba_amd {
 
@@ -365,6 +366,187 @@ __global__ __launch_bounds__(256) void conv_cl_bwd_k(const T* __restrict__ x, in
   }
 }
 
+// ---- bf16 fast path (16-B aligned rows, C % 8 == 0): the headline Mamba-2 shape -------------------
+// Same math as conv_cl_bwd_k, restructured for CDNA4 issue:
+//  * the W-row windows of x and dpre are register RINGS whose slots are compile-time indices of the
+//    W-step unrolled loop body, so advancing the window costs no moves;
+//  * each group of W steps issues its 2W 16-B row loads up front (kept packed as bf16 until used),
+//    so a wave waits for memory once per group instead of once per step;
+//  * channel pairs run on packed FP32 (v_pk_fma_f32 / v_pk_mul_f32).
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void unpack8(const uint4 v, f2v (&o)[4]) {
+  const unsigned u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) o[q] = f2v{__uint_as_float(u[q] << 16), __uint_as_float(u[q] & 0xffff0000u)};
+}
+__device__ __forceinline__ unsigned pack2(const f2v v) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf2v));
+}
+__device__ __forceinline__ uint4 pack8(const f2v (&o)[4]) {
+  return make_uint4(pack2(o[0]), pack2(o[1]), pack2(o[2]), pack2(o[3]));
+}
+
+template <int W, int TT>
+__global__ __launch_bounds__(256) void conv_cl_fwd_bf16_k(const bf16_t* __restrict__ x, int64_t sxb, int64_t sxl,
+                                                          const float* __restrict__ w, const float* __restrict__ bias,
+                                                          bf16_t* __restrict__ out, int64_t sob, int64_t sol, int L,
+                                                          int C, bool silu) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = (blockIdx.x * 64 + lane) * 8;
+  const int t0 = (blockIdx.y * 4 + wave) * TT;
+  const int b = blockIdx.z;
+  if (c >= C || t0 >= L) return;
+  f2v wk[W][4], bs[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+#pragma unroll
+    for (int k = 0; k < W; ++k) wk[k][q] = f2v{w[(c + 2 * q) * W + k], w[(c + 2 * q + 1) * W + k]};
+    bs[q] = bias ? f2v{bias[c + 2 * q], bias[c + 2 * q + 1]} : f2v{0.f, 0.f};
+  }
+  const bf16_t* xb = x + b * sxb + c;
+  bf16_t* ob = out + b * sob + c;
+  const int tend = min(t0 + TT, L);
+  auto ldrow = [&](int t) -> uint4 {
+    return (t >= 0 && t < tend) ? *reinterpret_cast<const uint4*>(xb + t * sxl) : make_uint4(0, 0, 0, 0);
+  };
+  f2v xr[W][4];
+#pragma unroll
+  for (int k = 0; k < W - 1; ++k) unpack8(ldrow(t0 - (W - 1) + k), xr[k]);
+  const int nsteps = tend - t0;
+  for (int i0 = 0; i0 < nsteps; i0 += W) {
+    uint4 rx[W];
+#pragma unroll
+    for (int u = 0; u < W; ++u) rx[u] = ldrow(t0 + i0 + u);
+#pragma unroll
+    for (int u = 0; u < W; ++u) {
+      const int i = i0 + u;
+      if (i < nsteps) {
+        const int sl = (u + W - 1) % W;
+        unpack8(rx[u], xr[sl]);
+        f2v o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          f2v a = bs[q];
+#pragma unroll
+          for (int k = 0; k < W; ++k) a += wk[k][q] * xr[(u + k) % W][q];
+          if (silu) a = a * f2v{sigmoidf_(a.x), sigmoidf_(a.y)};
+          o[q] = a;
+        }
+        *reinterpret_cast<uint4*>(ob + (t0 + i) * sol) = pack8(o);
+      }
+    }
+  }
+}
+
+template <int W, int TT>
+__global__ __launch_bounds__(256) void conv_cl_bwd_bf16_k(const bf16_t* __restrict__ x, int64_t sxb, int64_t sxl,
+                                                          const float* __restrict__ w, const float* __restrict__ bias,
+                                                          const bf16_t* __restrict__ dout, int64_t sgb, int64_t sgl,
+                                                          bf16_t* __restrict__ dx, int64_t sdb, int64_t sdl,
+                                                          float* __restrict__ part, int L, int C, bool silu) {
+  __shared__ float red[4][64 * 8 * (W + 1)];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = (blockIdx.x * 64 + lane) * 8;
+  const int t0 = (blockIdx.y * 4 + wave) * TT;
+  const int b = blockIdx.z;
+  f2v acc[W + 1][4];
+#pragma unroll
+  for (int k = 0; k < W + 1; ++k)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[k][q] = f2v{0.f, 0.f};
+  if (c < C && t0 < L) {
+    f2v wk[W][4], bs[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int k = 0; k < W; ++k) wk[k][q] = f2v{w[(c + 2 * q) * W + k], w[(c + 2 * q + 1) * W + k]};
+      bs[q] = bias ? f2v{bias[c + 2 * q], bias[c + 2 * q + 1]} : f2v{0.f, 0.f};
+    }
+    const bf16_t* xb = x + b * sxb + c;
+    const bf16_t* gb = dout + b * sgb + c;
+    bf16_t* db_ = dx + b * sdb + c;
+    const int tend = min(t0 + TT, L);
+    const int nsteps = tend + W - 1 - t0;  // main steps t = t0 .. t0+nsteps-1
+    const int tlim = min(L, t0 + nsteps);
+    auto ldrow = [&](const bf16_t* base, int64_t stride, int t) -> uint4 {
+      return (t >= 0 && t < tlim) ? *reinterpret_cast<const uint4*>(base + t * stride) : make_uint4(0, 0, 0, 0);
+    };
+    f2v xr[W][4], dp[W][4];
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dp[k][q] = f2v{0.f, 0.f};
+      if (k < W - 1) unpack8(ldrow(xb, sxl, t0 - (W - 1) + k), xr[k]);
+    }
+    for (int i0 = 0; i0 < nsteps; i0 += W) {
+      uint4 rx[W], rg[W];
+#pragma unroll
+      for (int u = 0; u < W; ++u) {
+        rx[u] = ldrow(xb, sxl, t0 + i0 + u);
+        rg[u] = ldrow(gb, sgl, t0 + i0 + u);
+      }
+#pragma unroll
+      for (int u = 0; u < W; ++u) {
+        const int i = i0 + u, t = t0 + i;
+        if (i < nsteps) {
+          const int sl = (u + W - 1) % W;  // slot of step t (compile-time after unrolling)
+          unpack8(rx[u], xr[sl]);
+          f2v g[4];
+          unpack8(rg[u], g);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            f2v a = bs[q];
+#pragma unroll
+            for (int k = 0; k < W; ++k) a += wk[k][q] * xr[(u + k) % W][q];
+            f2v d = g[q];
+            if (silu) {
+              const float s0 = sigmoidf_(a.x), s1 = sigmoidf_(a.y);
+              const f2v sv = f2v{s0, s1};
+              d = g[q] * sv * (1.f + a * (1.f - sv));
+            }
+            dp[sl][q] = (t < L) ? d : f2v{0.f, 0.f};
+          }
+          if (t < tend) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+#pragma unroll
+              for (int k = 0; k < W; ++k) acc[k][q] += dp[sl][q] * xr[(u + k) % W][q];
+              acc[W][q] += dp[sl][q];
+            }
+          }
+          if (i >= W - 1) {  // dx[s], s = t-(W-1) >= t0
+            f2v o[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              f2v v = f2v{0.f, 0.f};
+#pragma unroll
+              for (int m = 0; m < W; ++m) v += wk[W - 1 - m][q] * dp[(u + m) % W][q];
+              o[q] = v;
+            }
+            *reinterpret_cast<uint4*>(db_ + (t - (W - 1)) * sdl) = pack8(o);
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < W + 1; ++k)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      red[wave][(lane * 8 + 2 * q) * (W + 1) + k] = acc[k][q].x;
+      red[wave][(lane * 8 + 2 * q + 1) * (W + 1) + k] = acc[k][q].y;
+    }
+  __syncthreads();
+  const int64_t prow = (int64_t)blockIdx.z * gridDim.y + blockIdx.y;
+  for (int i = threadIdx.x; i < 64 * 8 * (W + 1); i += 256) {
+    const int ch = blockIdx.x * 512 + i / (W + 1);
+    if (ch < C) part[prow * (int64_t)C * (W + 1) + (int64_t)ch * (W + 1) + i % (W + 1)] =
+        red[0][i] + red[1][i] + red[2][i] + red[3][i];
+  }
+}
+
 // =========================== decode update ===============================================
 template <typename T, int W>
 __global__ void conv_update_k(const T* __restrict__ x, int64_t sxb, T* __restrict__ state, int64_t ssb,
@@ -456,6 +638,15 @@ static hipError_t cl_fwd(const T* x, int64_t sxb, int64_t sxl, const float* w, c
                          int64_t sob, int64_t sol, int Bn, int L, int C, int Wd, bool silu, hipStream_t st) {
   const bool vec = (C % 8 == 0) && (sxb % 8 == 0) && (sxl % 8 == 0) && (sob % 8 == 0) && (sol % 8 == 0) &&
                    ((uintptr_t)x % 16 == 0) && ((uintptr_t)out % 16 == 0);
+  if constexpr (std::is_same<T, bf16_t>::value) {
+    if (vec) {
+      constexpr int TF = 32;
+      dim3 g2((C + 511) / 512, (L + 4 * TF - 1) / (4 * TF), Bn);
+      W_SWITCH(Wd, hipLaunchKernelGGL((conv_cl_fwd_bf16_k<WW, TF>), g2, dim3(256), 0, st, x, sxb, sxl, w, bias, out,
+                                      sob, sol, L, C, silu));
+      return hipGetLastError();
+    }
+  }
   dim3 grid((C + 511) / 512, (L + 4 * CL_T - 1) / (4 * CL_T), Bn), block(256);
   W_SWITCH(Wd, {
     if (vec) hipLaunchKernelGGL((conv_cl_fwd_k<T, WW, true>), grid, block, 0, st, x, sxb, sxl, w, bias, out, sob,
@@ -486,6 +677,14 @@ static hipError_t cl_bwd(const T* x, int64_t sxb, int64_t sxl, const float* w, c
                    (sdb % 8 == 0) && (sdl % 8 == 0) && ((uintptr_t)x % 16 == 0) && ((uintptr_t)g % 16 == 0) &&
                    ((uintptr_t)dx % 16 == 0);
   dim3 grid((C + 511) / 512, (L + 4 * CLB_T - 1) / (4 * CLB_T), Bn), block(256);
+  if constexpr (std::is_same<T, bf16_t>::value) {
+    if (vec) {
+      W_SWITCH(Wd, hipLaunchKernelGGL((conv_cl_bwd_bf16_k<WW, CLB_T>), grid, block, 0, st, x, sxb, sxl, w, bias, g,
+                                      sgb, sgl, dx, sdb, sdl, part, L, C, silu));
+      MAMBA_HIP_CHECK(hipGetLastError());
+      return launch_colsum(part, conv_cl_bwd_partial_rows(Bn, L), C * (Wd + 1), dw, st);
+    }
+  }
   W_SWITCH(Wd, {
     if (vec) hipLaunchKernelGGL((conv_cl_bwd_k<T, WW, true>), grid, block, 0, st, x, sxb, sxl, w, bias, g, sgb, sgl,
                                 dx, sdb, sdl, part, Bn, L, C, silu);

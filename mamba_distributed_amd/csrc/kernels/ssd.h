@@ -14,6 +14,8 @@ struct SSDArgs {
   const bf16_t* Bm; int64_t sBb, sBl, sBg;  // (b, l, g, n) unit n stride
   const bf16_t* Cm; int64_t sCb, sCl, sCg;
   bool softplus; float dt_min, dt_max;
+  bool a_log;                 // A holds A_log: kernels use A = -exp(A_log), dA partials become dA_log
+  int psl;                    // row stride of the (b*nc, 3, H) small-partials block (= 3H)
   const float* init;      // (b, h, p, n) or null
   // forward outputs / saved
   float* dtp; float* cum; // (b, h, Lp)

@@ -52,7 +52,7 @@ __global__ __launch_bounds__(256) void ssd_cumsum_k(SSDArgs a) {
     v = a.softplus ? softplusf_(raw) : raw;
     v = fminf(fmaxf(v, a.dt_min), a.dt_max);
   }
-  float x = v * a.A[h];
+  float x = v * (a.a_log ? -__expf(a.A[h]) : a.A[h]);
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
     const float y = __shfl_up(x, off, 64);
@@ -437,7 +437,7 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
     __syncthreads();
     if (hh + 1 < a.HG) prefetch(h + 1);
     const float cl = cumr[Q - 1];
-    const float Ah = a.A[h];
+    const float Ah = a.a_log ? -__expf(a.A[h]) : a.A[h];
     const float Dh = a.D ? a.D[h] : 0.f;
     const float dtj = dtr[jl], cumj = cumr[jl];
     // ---- (1)(2) dM, M; half 0: dCB and the G row/col sums
@@ -598,8 +598,8 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
       }
       const float dbp = wave_sum(gdt);
       if (l == 0) {
-        const int64_t pi = ((int64_t)b * a.nc + c) * a.H + h;
-        a.part_dA[pi] = dAp;
+        const int64_t pi = ((int64_t)b * a.nc + c) * a.psl + h;
+        a.part_dA[pi] = a.a_log ? dAp * Ah : dAp;  // d/dA_log = dA * A
         a.part_dbias[pi] = dbp;
         a.part_dD[pi] = red[0];
       }

@@ -92,13 +92,13 @@ class Mamba2(nn.Module):
                 out, _, _ = self.step(u, conv_state, ssm_state)
                 return out
         zxbcdt = self.in_proj(u)
-        A = -torch.exp(self.A_log.float())
         if conv_state is None:
-            y = mamba2_inner_fn(zxbcdt, self.conv1d.weight, self.conv1d.bias, self.dt_bias, A, self.D,
+            y = mamba2_inner_fn(zxbcdt, self.conv1d.weight, self.conv1d.bias, self.dt_bias, self.A_log, self.D,
                                 self.norm.weight, self.norm.eps, self.headdim, self.ngroups, self.d_state,
-                                self.dt_limit, self.norm_before_gate, ref_chunk_size=min(64, self.chunk_size))
+                                self.dt_limit, self.norm_before_gate, ref_chunk_size=min(64, self.chunk_size),
+                                A_is_log=True)
         else:
-            y = self._prefill(zxbcdt, A, conv_state, ssm_state)
+            y = self._prefill(zxbcdt, -torch.exp(self.A_log.float()), conv_state, ssm_state)
         return self.out_proj(y)
 
     def _prefill(self, zxbcdt, A, conv_state, ssm_state):

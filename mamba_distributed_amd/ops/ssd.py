@@ -82,7 +82,7 @@ def mamba_chunk_scan_combined(x, dt, A, B, C, chunk_size=256, D=None, z=None, dt
 class _Mamba2InnerFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, zxbcdt, conv_w, conv_b, dt_bias, A, D, norm_w, eps, headdim, ngroups, d_state,
-                dt_min, dt_max, norm_before_gate):
+                dt_min, dt_max, norm_before_gate, A_is_log=False):
         ops = _ext.ops()
         b, l, dproj = zxbcdt.shape
         H = dt_bias.shape[0]
@@ -100,18 +100,18 @@ class _Mamba2InnerFn(torch.autograd.Function):
         Bm = xBC_c[..., di:di + ngroups * d_state].unflatten(-1, (ngroups, d_state))
         Cm = xBC_c[..., di + ngroups * d_state:].unflatten(-1, (ngroups, d_state))
         y, cum, dtp, states, _ = ops.ssd_fwd(x, dt, A, Bm, Cm, D, dt_bias, None, NATIVE_CHUNK,
-                                             True, dt_min, dt_max)
+                                             True, dt_min, dt_max, A_is_log)
         y2 = y.view(b * l, di)
         yn, rstd = ops.gated_rmsnorm_fwd(y2, z.flatten(0, 1), norm_w, eps, di // ngroups, norm_before_gate)
         ctx.save_for_backward(zxbcdt, w2, conv_b, dt_bias, A, D, norm_w, xBC_c, y, rstd, cum, dtp, states)
-        ctx.meta = (eps, headdim, ngroups, d_state, dt_min, dt_max, norm_before_gate)
+        ctx.meta = (eps, headdim, ngroups, d_state, dt_min, dt_max, norm_before_gate, A_is_log)
         ctx.wshape = conv_w.shape
         return yn.view(b, l, di)
 
     @staticmethod
     def backward(ctx, dyn):
         (zxbcdt, w2, conv_b, dt_bias, A, D, norm_w, xBC_c, y, rstd, cum, dtp, states) = ctx.saved_tensors
-        eps, headdim, ngroups, d_state, dt_min, dt_max, nbg = ctx.meta
+        eps, headdim, ngroups, d_state, dt_min, dt_max, nbg, a_log = ctx.meta
         ops = _ext.ops()
         b, l, dproj = zxbcdt.shape
         H = dt_bias.shape[0]
@@ -134,12 +134,12 @@ class _Mamba2InnerFn(torch.autograd.Function):
                         dxBC_c[..., :di].unflatten(-1, (H, headdim)),
                         dz_all[..., di + conv_dim:],
                         dxBC_c[..., di:di + gn].unflatten(-1, (ngroups, d_state)),
-                        dxBC_c[..., di + gn:].unflatten(-1, (ngroups, d_state)))
+                        dxBC_c[..., di + gn:].unflatten(-1, (ngroups, d_state)), a_log)
         _, _, dA, _, _, dD, ddt_bias, _ = g
         xBC = zxbcdt[..., di:di + conv_dim]
         _, dw, db = ops.conv1d_cl_bwd(xBC, w2, conv_b, dxBC_c, True, dz_all[..., di:di + conv_dim])
         return (dz_all, dw.reshape(ctx.wshape).to(w2.dtype), db.to(conv_b.dtype) if conv_b is not None else None,
-                ddt_bias, dA, dD, dnorm_w, None, None, None, None, None, None, None)
+                ddt_bias, dA, dD, dnorm_w, None, None, None, None, None, None, None, None)
 
 
 def mamba2_inner_ref(zxbcdt, conv_w, conv_b, dt_bias, A, D, norm_w, eps, headdim, ngroups, d_state,
@@ -160,12 +160,16 @@ def mamba2_inner_ref(zxbcdt, conv_w, conv_b, dt_bias, A, D, norm_w, eps, headdim
 
 
 def mamba2_inner_fn(zxbcdt, conv_w, conv_b, dt_bias, A, D, norm_w, eps, headdim, ngroups, d_state,
-                    dt_limit=(0.0, _INF), norm_before_gate=False, ref_chunk_size=64):
-    """conv1d+SiLU -> SSD -> gated RMSNorm on the in_proj output; returns (b, l, d_inner)."""
+                    dt_limit=(0.0, _INF), norm_before_gate=False, ref_chunk_size=64, A_is_log=False):
+    """conv1d+SiLU -> SSD -> gated RMSNorm on the in_proj output; returns (b, l, d_inner).
+    ``A_is_log``: ``A`` is the A_log parameter; the kernels apply A = -exp(A_log) and return dA_log
+    (saves the per-layer exp/neg launches and their backward)."""
     if _ext.use_native(zxbcdt):
         return _Mamba2InnerFn.apply(zxbcdt, conv_w, conv_b, dt_bias, A, D, norm_w, eps, headdim,
                                     ngroups, d_state, float(dt_limit[0]), float(dt_limit[1]),
-                                    norm_before_gate)
+                                    norm_before_gate, A_is_log)
+    if A_is_log:
+        A = -torch.exp(A.float())
     return mamba2_inner_ref(zxbcdt, conv_w, conv_b, dt_bias, A, D, norm_w, eps, headdim, ngroups,
                             d_state, dt_limit, norm_before_gate, ref_chunk_size)
 
