@@ -373,7 +373,14 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t Xs[Q * LD64];
   __shared__ __attribute__((aligned(16))) bf16_t dYs[Q * LD64];
   __shared__ __attribute__((aligned(16))) bf16_t Os[Q * LD64];
-  __shared__ float cumr[Q], dtr[Q], dcum[Q], ddtd[Q], red[16];
+  // per-head dt-gradient inputs, kept for all heads of the group so step (10) runs once at the end
+  // with one wave per head instead of serialising wave 0 inside the head loop
+  // Every cross-lane partial goes to a slot owned by ONE wave (plain read-modify-write in program
+  // order) and the slots are summed in a fixed order in (10): deterministic, no LDS float atomics.
+  __shared__ float cumr[Q], dtr[8][Q], rawl[8][Q];
+  __shared__ float dcw[8][8][Q];   // [head][wave][step]  dcum contributions
+  __shared__ float ddw[8][2][Q];   // [head][half][step]  direct ddt contributions
+  __shared__ float redw[8][8];     // [head][wave]        dD
   const int c = blockIdx.x, hgi = blockIdx.y, b = blockIdx.z;
   const int h0 = hgi * a.HG, g = h0 / (a.H / a.G);
   const int wid = threadIdx.x >> 6, l = threadIdx.x & 63;
@@ -398,6 +405,8 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
     }
   };
   prefetch(h0);
+  for (int v = threadIdx.x; v < 8 * 8 * Q; v += 512) (&dcw[0][0][0])[v] = 0.f;
+  for (int v = threadIdx.x; v < 8 * 2 * Q; v += 512) (&ddw[0][0][0])[v] = 0.f;
   stage_tile<Q, N>(Cs, LDN, a.Cm + (int64_t)b * a.sCb + (int64_t)c * Q * a.sCl + (int64_t)g * a.sCg, a.sCl, valid);
   stage_tile<Q, N>(Bs, LDN, a.Bm + (int64_t)b * a.sBb + (int64_t)c * Q * a.sBl + (int64_t)g * a.sBg, a.sBl, valid);
   __syncthreads();
@@ -422,14 +431,11 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
   for (int hh = 0; hh < a.HG; ++hh) {
     const int h = h0 + hh;
     __syncthreads();  // previous head fully consumed (LDS tiles, dcum, Os)
-    float rawdt = praw;  // lanes of wave 0 = local steps
     if (threadIdx.x < Q) {
       cumr[threadIdx.x] = pc;
-      dtr[threadIdx.x] = pd;
-      dcum[threadIdx.x] = 0.f;
-      ddtd[threadIdx.x] = 0.f;
+      dtr[hh][threadIdx.x] = pd;
+      rawl[hh][threadIdx.x] = praw;
     }
-    if (threadIdx.x < 16) red[threadIdx.x] = 0.f;
     px.store(Xs, LD64);
     py.store(dYs, LD64);
     ps.store(Ss, LDN);
@@ -439,7 +445,7 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
     const float cl = cumr[Q - 1];
     const float Ah = a.a_log ? -__expf(a.A[h]) : a.A[h];
     const float Dh = a.D ? a.D[h] : 0.f;
-    const float dtj = dtr[jl], cumj = cumr[jl];
+    const float dtj = dtr[hh][jl], cumj = cumr[jl];
     // ---- (1)(2) dM, M; half 0: dCB and the G row/col sums
     f32x4 m[4];
     float colG = 0.f;
@@ -467,14 +473,14 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float rs = row_sum16(gr[r]);
-            if (li == 0) atomicAdd(&dcum[16 * I + 4 * lg + r], rs);
+            if (li == 0) dcw[hh][wid][16 * I + 4 * lg + r] += rs;
           }
         }
       }
     }
     if (half == 0) {
       colG = rows_sum4(colG);
-      if (l < 16) atomicAdd(&dcum[jl], -colG);
+      if (l < 16) dcw[hh][wid][jl] -= colG;
     }
     // ---- (3) dXdt = M^T dY, (4) BdS = B dS^T, (6) Yoff = C S^T  for this half's p-tiles
     f32x4 dxd[2], bds[2], yo[2];
@@ -514,7 +520,7 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int j = 16 * w + 4 * lg + r;
-      const float dt_ = dtr[j];
+      const float dt_ = dtr[hh][j];
       const float ej = __expf(cl - cumr[j]);
       const float wj = ej * dt_;
       const float ei = __expf(cumr[j]);
@@ -534,19 +540,19 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
       up = row_sum16(up) * wj;
       yp = row_sum16(yp) * ei;
       if (li == 0) {
-        atomicAdd(&ddtd[j], ddp);
-        atomicAdd(&dcum[j], yp - up);
+        ddw[hh][half][j] += ddp;
+        dcw[hh][wid][j] += yp - up;
       }
       usum += up;
     }
     usum = rows_sum4(usum);  // the wave's U total over its 16 rows (x its p-half)
-    if (l == 0) atomicAdd(&dcum[Q - 1], usum);
+    if (l == 0) dcw[hh][wid][Q - 1] += usum;
     dDp = wave_sum(dDp);
-    if (l == 0) atomicAdd(&red[0], dDp);
+    if (l == 0) redw[hh][wid] = dDp;
     // ---- (7) dC_off += (e^{cum_i} dY) S , (8) dB_off += (w_j x) dS   for this half's n-tiles
     {
       const float ei = __expf(cumr[jl]);
-      const float wl = __expf(cl - cumr[jl]) * dtr[jl];
+      const float wl = __expf(cl - cumr[jl]) * dtr[hh][jl];
 #pragma unroll
       for (int ks = 0; ks < P / 32; ++ks) {
         const bf16x8 Ay = scale_frag(frag_kc(dYs, LD64, 16 * w, 32 * ks), ei);
@@ -571,38 +577,51 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
         for (int k = 0; k < 8; ++k) s += fa[k] * fb[k];
       }
       s = wave_sum(s);
-      if (l == 0) atomicAdd(&dcum[Q - 1], s * __expf(cl));
+      if (l == 0) dcw[hh][wid][Q - 1] += s * __expf(cl);
     }
-    __syncthreads();
-    store_tile<Q, 64>(a.dx + (int64_t)b * a.sdxb + (int64_t)c * Q * a.sdxl + (int64_t)h * a.sdxh, a.sdxl, Os, LD64,
-                      valid);
-    // ---- (10) dt gradients for this head (wave 0; lane = local step)
-    if (wid == 0) {
-      float da = dcum[l];
+    // dX: each wave stores the 16x32 sub-tile of Os it wrote itself (same-wave LDS ops are in order,
+    // so no block barrier is needed)
+    {
+      const int row = 16 * w + (l >> 2), col = 32 * half + 8 * (l & 3);
+      if (row < valid)
+        *reinterpret_cast<uint4*>(a.dx + (int64_t)b * a.sdxb + (int64_t)(c * Q + row) * a.sdxl +
+                                  (int64_t)h * a.sdxh + col) = *reinterpret_cast<const uint4*>(Os + row * LD64 + col);
+    }
+  }
+  __syncthreads();
+  // ---- (10) dt gradients, one wave per head of the group (lane = local step)
+  if (wid < a.HG) {
+    const int hh = wid, h = h0 + wid;
+    const float Ah = a.a_log ? -__expf(a.A[h]) : a.A[h];
+    float da = 0.f;
 #pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {  // reverse inclusive scan: da_i = sum_{t>=i} dcum_t
-        const float y = __shfl_down(da, off, 64);
-        if (l + off < 64) da += y;
-      }
-      const float ddt = ddtd[l] + da * Ah;
-      const float dAp = wave_sum(da * dtr[l]);
-      const int t = c * Q + l;
-      float gdt = 0.f;
-      if (t < a.L) {
-        float raw = rawdt;
-        if (a.dt_bias) raw += a.dt_bias[h];
-        const float v = a.softplus ? softplusf_(raw) : raw;
-        const bool inside = (v >= a.dt_min) && (v <= a.dt_max);
-        gdt = inside ? ddt * (a.softplus ? sigmoidf_(raw) : 1.f) : 0.f;
-        st_any(a.ddt, a.ddt_dtype, (int64_t)b * a.sddtb + (int64_t)t * a.sddtl + (int64_t)h * a.sddth, gdt);
-      }
-      const float dbp = wave_sum(gdt);
-      if (l == 0) {
-        const int64_t pi = ((int64_t)b * a.nc + c) * a.psl + h;
-        a.part_dA[pi] = a.a_log ? dAp * Ah : dAp;  // d/dA_log = dA * A
-        a.part_dbias[pi] = dbp;
-        a.part_dD[pi] = red[0];
-      }
+    for (int v = 0; v < 8; ++v) da += dcw[hh][v][l];
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {  // reverse inclusive scan: da_i = sum_{t>=i} dcum_t
+      const float y = __shfl_down(da, off, 64);
+      if (l + off < 64) da += y;
+    }
+    const float ddt = (ddw[hh][0][l] + ddw[hh][1][l]) + da * Ah;
+    const float dAp = wave_sum(da * dtr[hh][l]);
+    const int t = c * Q + l;
+    float gdt = 0.f;
+    if (t < a.L) {
+      float raw = rawl[hh][l];
+      if (a.dt_bias) raw += a.dt_bias[h];
+      const float v = a.softplus ? softplusf_(raw) : raw;
+      const bool inside = (v >= a.dt_min) && (v <= a.dt_max);
+      gdt = inside ? ddt * (a.softplus ? sigmoidf_(raw) : 1.f) : 0.f;
+      st_any(a.ddt, a.ddt_dtype, (int64_t)b * a.sddtb + (int64_t)t * a.sddtl + (int64_t)h * a.sddth, gdt);
+    }
+    const float dbp = wave_sum(gdt);
+    if (l == 0) {
+      const int64_t pi = ((int64_t)b * a.nc + c) * a.psl + h;
+      a.part_dA[pi] = a.a_log ? dAp * Ah : dAp;  // d/dA_log = dA * A
+      a.part_dbias[pi] = dbp;
+      float dd = 0.f;
+#pragma unroll
+      for (int v = 0; v < 8; ++v) dd += redw[hh][v];
+      a.part_dD[pi] = dd;
     }
   }
   // ---- head-group partials
