@@ -5,353 +5,464 @@
 //   y_t    = sum_n C_t[n] h_t[n] + D[d] u_t ;  out_t = y_t * silu(z_t)
 // (upstream csrc/selective_scan)
 //
-// Work decomposition (MI355X-first):
-//  * a 256-thread workgroup owns Kc channels of one batch row and walks them one channel at a time;
-//    its 4 wavefronts split the N states (N/4 each), so every (channel, state) recurrence lives in
-//    exactly one wave and the per-state cross-channel sums dB[t,n], dC[t,n] accumulate in that
-//    wave's REGISTERS over the Kc channels — deterministic, no float atomics.  Sums over n (y, du,
-//    ddelta) are the only cross-wave traffic: one LDS partial row per wave, one barrier.
-//  * time is cut into tiles of 64 lanes x ITEMS steps; each lane composes its ITEMS steps into an
-//    affine map (a, b), a wave64 Hillis-Steele scan over lanes combines the maps, and the state at
-//    the tile boundary is carried in LDS per (channel, state) across tiles.
-//  * backward replays the forward inside the tile from the saved tile-start states, then runs the
-//    adjoint recurrence lambda_t = dy_t C_t + a_{t+1} lambda_{t+1} as a reverse wave scan.
-//  * loads along time are 16-B vectors (8 x bf16) whenever the row is aligned.
+// Work decomposition (MI355X-first; details above each kernel):
+//  * forward: one wavefront per (b, d) row, lanes over time (16 steps each), all N states per wave;
+//    the cross-lane recurrence is a DPP affine prefix scan (row_shr / row_bcast, no LDS).
+//  * backward: a workgroup owns 64 channels of one batch row and walks tiles of 512 steps from the
+//    end; its 4 waves split the N states, replay the forward from the saved tile-start states and
+//    run the adjoint as a DPP suffix scan; dB/dC sums over channels stay in registers.
+//  * deterministic everywhere: every partial has exactly one writer, reductions run in fixed order.
 #include "common.h"
 #include "selective_scan.h"
+#include <type_traits>
 
 namespace mamba_amd {
 
-constexpr int SS_ITEMS = 8;
-constexpr int SS_T = 64 * SS_ITEMS;
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr int SF_IT = 16, SF_T = 64 * SF_IT;  // forward: one wave walks a row in 1024-step tiles
+constexpr int SB_IT = 4, SB_T = 64 * SB_IT;   // backward tiles; also the saved-carry granularity
+constexpr int SB_W = 4;                       // waves per backward workgroup
+constexpr int SB_KC = 64;                     // channels per backward workgroup
 
-template <typename T>
-__device__ __forceinline__ void load_items(const T* row, int t0, int L, bool vec, float (&o)[SS_ITEMS]) {
-  if (vec && t0 + SS_ITEMS <= L) {
-    ld8bf(reinterpret_cast<const bf16_t*>(row + t0), o);
+// ---- item I/O: IT consecutive steps of one (b, d) row (16-B vectors when aligned) -------------
+// VEC: every row segment is a whole number of 16-B vectors inside [0, L) or entirely outside
+// (host guarantees: bf16, aligned rows, L % IT == 0) -> no per-element guards in the hot kernels.
+template <bool VEC, typename T, int IT>
+__device__ __forceinline__ void load_items(const T* row, int t0, int L, float (&o)[IT]) {
+  if constexpr (VEC) {
+    static_assert(IT % 8 == 0 || IT == 4, "vector item loads are 8 or 16 bytes");
+    if (t0 < L) {
+      if constexpr (IT == 4) {
+        const uint2 v = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(row) + t0);
+        o[0] = __uint_as_float(v.x << 16); o[1] = __uint_as_float(v.x & 0xffff0000u);
+        o[2] = __uint_as_float(v.y << 16); o[3] = __uint_as_float(v.y & 0xffff0000u);
+      } else {
+#pragma unroll
+        for (int q = 0; q < IT / 8; ++q) {
+          float tmp[8];
+          ld8bf(reinterpret_cast<const bf16_t*>(row) + t0 + 8 * q, tmp);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[8 * q + j] = tmp[j];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < IT; ++i) o[i] = 0.f;
+    }
   } else {
 #pragma unroll
-    for (int i = 0; i < SS_ITEMS; ++i) o[i] = (t0 + i < L) ? ld(row + t0 + i) : 0.f;
+    for (int i = 0; i < IT; ++i) o[i] = (t0 + i < L) ? ld(row + t0 + i) : 0.f;
   }
 }
-template <>
-__device__ __forceinline__ void load_items<float>(const float* row, int t0, int L, bool vec, float (&o)[SS_ITEMS]) {
+template <bool VEC, typename T, int IT>
+__device__ __forceinline__ void store_items(T* row, int t0, int L, const float (&o)[IT]) {
+  if constexpr (VEC) {
+    static_assert(IT % 8 == 0, "vector item stores are 16 bytes");
+    if (t0 < L) {
 #pragma unroll
-  for (int i = 0; i < SS_ITEMS; ++i) o[i] = (t0 + i < L) ? row[t0 + i] : 0.f;
-}
-
-// inclusive scan of affine maps over the 64 lanes: (a1,b1) then (a2,b2) = (a1 a2, a2 b1 + b2)
-__device__ __forceinline__ void wave_affine_scan(float& a, float& b) {
-  const int lane = threadIdx.x & 63;
+      for (int q = 0; q < IT / 8; ++q) {
+        float tmp[8];
 #pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const float pa = __shfl_up(a, off, 64), pb = __shfl_up(b, off, 64);
-    if (lane >= off) {
-      b = a * pb + b;
-      a = a * pa;
+        for (int j = 0; j < 8; ++j) tmp[j] = o[8 * q + j];
+        st8bf(reinterpret_cast<bf16_t*>(row) + t0 + 8 * q, tmp);
+      }
     }
-  }
-}
-// reverse inclusive scan: lane i composes lanes i..63 in reverse order:
-//   (a_i, b_i) after (a_{i+1}, b_{i+1}):  lambda_i = b_i + a_i * lambda_{i+1}
-__device__ __forceinline__ void wave_affine_rscan(float& a, float& b) {
-  const int lane = threadIdx.x & 63;
+  } else {
 #pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const float na = __shfl_down(a, off, 64), nb = __shfl_down(b, off, 64);
-    if (lane + off < 64) {
-      b = b + a * nb;
-      a = a * na;
-    }
+    for (int i = 0; i < IT; ++i)
+      if (t0 + i < L) st(row + t0 + i, o[i]);
   }
 }
 
-template <typename T, int N>
+// ---- wave64 affine scans on DPP (no LDS round trips) -----------------------------------------
+template <int CTRL, int RM = 0xF>
+__device__ __forceinline__ float dppf(float old, float src) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old), __builtin_bit_cast(int, src),
+                                                               CTRL, RM, 0xF, false));
+}
+__device__ __forceinline__ float readlanef(float v, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+// combine the map held `off` lanes away (applied first) into (a, b): (a, b) <- (a*pa, a*pb + b)
+#define SS_STEP(CTRL, RM)                                                       \
+  {                                                                             \
+    const float pa = dppf<CTRL, RM>(1.f, a), pb = dppf<CTRL, RM>(0.f, b);       \
+    b = fmaf(a, pb, b);                                                         \
+    a *= pa;                                                                    \
+  }
+// inclusive prefix over lanes 0..i of the maps h -> a h + b (lane 0 applied first):
+// row_shr 1/2/4/8 inside each 16-lane row, then row_bcast:15 / row_bcast:31 across rows
+__device__ __forceinline__ void scan_prefix(float& a, float& b) {
+  SS_STEP(0x111, 0xF) SS_STEP(0x112, 0xF) SS_STEP(0x114, 0xF) SS_STEP(0x118, 0xF)
+  SS_STEP(0x142, 0xA) SS_STEP(0x143, 0xC)
+}
+// inclusive suffix over lanes i..63 (lane 63 applied first): row_shl inside rows, then the
+// four row totals (lanes 0/16/32/48) are composed through readlane
+__device__ __forceinline__ void scan_suffix(float& a, float& b) {
+  SS_STEP(0x101, 0xF) SS_STEP(0x102, 0xF) SS_STEP(0x104, 0xF) SS_STEP(0x108, 0xF)
+  const float a1 = readlanef(a, 16), b1 = readlanef(b, 16);
+  const float a2 = readlanef(a, 32), b2 = readlanef(b, 32);
+  const float a3 = readlanef(a, 48), b3 = readlanef(b, 48);
+  const float c1a = a2 * a3, c1b = fmaf(a2, b3, b2);  // rows 2..3
+  const float c0a = a1 * c1a, c0b = fmaf(a1, c1b, b1);  // rows 1..3
+  const int row = (threadIdx.x & 63) >> 4;
+  const float ca = row == 0 ? c0a : row == 1 ? c1a : row == 2 ? a3 : 1.f;
+  const float cb = row == 0 ? c0b : row == 1 ? c1b : row == 2 ? b3 : 0.f;
+  b = fmaf(a, cb, b);
+  a *= ca;
+}
+#undef SS_STEP
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += dppf<0x111>(0.f, v);
+  v += dppf<0x112>(0.f, v);
+  v += dppf<0x114>(0.f, v);
+  v += dppf<0x118>(0.f, v);
+  v += dppf<0x142, 0xA>(0.f, v);
+  v += dppf<0x143, 0xC>(0.f, v);
+  return readlanef(v, 63);
+}
+
+// ============================== forward ========================================================
+// One wavefront per (b, d) row; lane i owns SF_IT consecutive steps of the current 1024-step tile
+// and ALL N states, so the sum over n for y stays in registers.  Per state: the lane composes its
+// steps into one affine map, a DPP prefix scan combines the 64 lanes, the lane replays its steps
+// from its true starting state.  The state at every SB_T boundary is saved for the backward.
+template <typename T, int N, bool VEC>
 __global__ __launch_bounds__(256) void selscan_fwd_k(SelScanArgs a) {
-  constexpr int NW = N / 4;
-  __shared__ float ypart[4][SS_T];
-  __shared__ float carry_s[64][N];
-  const int dg = blockIdx.x, b = blockIdx.y;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int d0 = dg * a.Kc, nch = min(a.Kc, a.D - d0);
-  const int ntiles = (a.L + SS_T - 1) / SS_T;
-  for (int v = threadIdx.x; v < 64 * N; v += 256) carry_s[v / N][v % N] = 0.f;
-  __syncthreads();
-  for (int tile = 0; tile < ntiles; ++tile) {
-    const int t0 = tile * SS_T;
-    const int tl = t0 + lane * SS_ITEMS;
-    for (int ci = 0; ci < nch; ++ci) {
-      const int d = d0 + ci;
-      const int g = d / (a.D / a.G);
-      const T* urow = ((const T*)a.u_) + (int64_t)b * a.sub + (int64_t)d * a.sud;
-      const T* drow = ((const T*)a.delta_) + (int64_t)b * a.sdb + (int64_t)d * a.sdd;
-      float u[SS_ITEMS], dl[SS_ITEMS], yp[SS_ITEMS];
-      load_items<T>(urow, tl, a.L, a.vec, u);
-      load_items<T>(drow, tl, a.L, a.vec, dl);
-      const float bias = a.delta_bias ? a.delta_bias[d] : 0.f;
+  const int lane = threadIdx.x & 63;
+  const int row = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (row >= a.B * a.D) return;
+  const int b = row / a.D, d = row % a.D;
+  const int g = d / (a.D / a.G);
+  const T* urow = ((const T*)a.u_) + (int64_t)b * a.sub + (int64_t)d * a.sud;
+  const T* drow = ((const T*)a.delta_) + (int64_t)b * a.sdb + (int64_t)d * a.sdd;
+  const T* zrow = a.z_ ? ((const T*)a.z_) + (int64_t)b * a.szb + (int64_t)d * a.szd : nullptr;
+  T* orow = ((T*)a.out_) + (int64_t)b * a.sob + (int64_t)d * a.sod;
+  const T* Bb = ((const T*)a.Bm_) + (int64_t)b * a.sBb + (int64_t)g * a.sBg;
+  const T* Cb = ((const T*)a.Cm_) + (int64_t)b * a.sCb + (int64_t)g * a.sCg;
+  const float Dd = a.D_ ? a.D_[d] : 0.f;
+  const float bias = a.delta_bias ? a.delta_bias[d] : 0.f;
+  const int nck = (a.L + SB_T - 1) / SB_T;
+  __shared__ float hcs[4][N];  // per-wave carried state (uniform), one writer lane
+  float* hc = hcs[threadIdx.x >> 6];
+  if (lane < N) hc[lane] = 0.f;
+  for (int t0 = 0; t0 < a.L; t0 += SF_T) {
+    const int tl = t0 + lane * SF_IT;
+    float u[SF_IT], dl[SF_IT], y[SF_IT];
+    load_items<VEC, T, SF_IT>(urow, tl, a.L, u);
+    load_items<VEC, T, SF_IT>(drow, tl, a.L, dl);
 #pragma unroll
-      for (int i = 0; i < SS_ITEMS; ++i) {
-        float v = dl[i] + bias;
-        v = a.softplus ? softplusf_(v) : v;
-        dl[i] = (tl + i < a.L) ? v : 0.f;
-        yp[i] = 0.f;
-      }
-#pragma unroll
-      for (int nn = 0; nn < NW; ++nn) {
-        const int n = w * NW + nn;
-        const float An = a.A[d * N + n];
-        float Bv[SS_ITEMS], Cv[SS_ITEMS];
-        load_items<T>(((const T*)a.Bm_) + (int64_t)b * a.sBb + (int64_t)g * a.sBg + (int64_t)n * a.sBn, tl, a.L, a.vecbc, Bv);
-        load_items<T>(((const T*)a.Cm_) + (int64_t)b * a.sCb + (int64_t)g * a.sCg + (int64_t)n * a.sCn, tl, a.L, a.vecbc, Cv);
-        float Ac[SS_ITEMS], Bc[SS_ITEMS];
-        float ca = 1.f, cb = 0.f;
-#pragma unroll
-        for (int i = 0; i < SS_ITEMS; ++i) {
-          const float ai = __expf(dl[i] * An);
-          cb = ai * cb + dl[i] * Bv[i] * u[i];
-          ca = ca * ai;
-          Ac[i] = ca;
-          Bc[i] = cb;
-        }
-        float sa = ca, sb = cb;
-        wave_affine_scan(sa, sb);
-        float ea = __shfl_up(sa, 1, 64), eb = __shfl_up(sb, 1, 64);
-        if (lane == 0) { ea = 1.f; eb = 0.f; }
-        const float c0 = carry_s[ci][n];
-        const float hs = ea * c0 + eb;
-        float hlast = 0.f;
-#pragma unroll
-        for (int i = 0; i < SS_ITEMS; ++i) {
-          const float hi = Ac[i] * hs + Bc[i];
-          yp[i] += Cv[i] * hi;
-          hlast = hi;
-        }
-        const float cnew = __shfl(hlast, 63, 64);
-        if (lane == 0) {
-          if (a.carries) a.carries[(((int64_t)b * a.D + d) * ntiles + tile) * N + n] = c0;
-          carry_s[ci][n] = cnew;
-          if (tile == ntiles - 1 && a.last_state) a.last_state[((int64_t)b * a.D + d) * N + n] = cnew;
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < SS_ITEMS; ++i) ypart[w][lane * SS_ITEMS + i] = yp[i];
-      __syncthreads();
-      const float Dd = a.D_ ? a.D_[d] : 0.f;
-      T* orow = ((T*)a.out_) + (int64_t)b * a.sob + (int64_t)d * a.sod;
-      const T* zrow = a.z_ ? ((const T*)a.z_) + (int64_t)b * a.szb + (int64_t)d * a.szd : nullptr;
-      for (int k = threadIdx.x; k < SS_T; k += 256) {
-        const int t = t0 + k;
-        if (t < a.L) {
-          float y = ypart[0][k] + ypart[1][k] + ypart[2][k] + ypart[3][k] + Dd * ld(urow + t);
-          if (zrow) y *= siluf_(ld(zrow + t));
-          st(orow + t, y);
-        }
-      }
-      __syncthreads();
+    for (int i = 0; i < SF_IT; ++i) {
+      float v = dl[i] + bias;
+      v = a.softplus ? softplus_fast(v) : v;
+      dl[i] = (tl + i < a.L) ? v : 0.f;
+      y[i] = 0.f;
     }
+#pragma unroll 1
+    for (int n = 0; n < N; ++n) {  // keep each state's loads in its own iteration (bounded registers)
+      const float A2 = a.A[d * N + n] * kLog2e;
+      float Bv[SF_IT], Cv[SF_IT], av[SF_IT], xb[SF_IT];
+      load_items<VEC, T, SF_IT>(Bb + (int64_t)n * a.sBn, tl, a.L, Bv);
+      load_items<VEC, T, SF_IT>(Cb + (int64_t)n * a.sCn, tl, a.L, Cv);
+      float ca = 1.f, cb = 0.f;
+#pragma unroll
+      for (int i = 0; i < SF_IT; ++i) {
+        av[i] = __builtin_amdgcn_exp2f(dl[i] * A2);
+        xb[i] = dl[i] * u[i] * Bv[i];
+        cb = fmaf(av[i], cb, xb[i]);
+        ca *= av[i];
+      }
+      scan_prefix(ca, cb);
+      const float hend = fmaf(ca, hc[n], cb);     // state after this lane's last step
+      const float hin = dppf<0x138>(hc[n], hend);  // wave_shr:1 -> state before this lane's first step
+      if (a.carries && (lane & (SB_T / SF_IT - 1)) == 0 && tl < a.L)
+        a.carries[((int64_t)row * nck + tl / SB_T) * N + n] = hin;
+      float h = hin;
+#pragma unroll
+      for (int i = 0; i < SF_IT; ++i) {
+        h = fmaf(av[i], h, xb[i]);
+        y[i] = fmaf(Cv[i], h, y[i]);
+      }
+      const float hnext = readlanef(hend, 63);
+      if (lane == 0) hc[n] = hnext;
+    }
+    float zz[SF_IT];
+    if (zrow) load_items<VEC, T, SF_IT>(zrow, tl, a.L, zz);
+#pragma unroll
+    for (int i = 0; i < SF_IT; ++i) {
+      float o = fmaf(Dd, u[i], y[i]);
+      if (zrow) o *= siluf_(zz[i]);
+      y[i] = o;
+    }
+    store_items<VEC, T, SF_IT>(orow, tl, a.L, y);
   }
+  if (a.last_state && lane < N) a.last_state[(int64_t)row * N + lane] = hc[lane];
 }
 
-template <typename T, int N>
-__global__ __launch_bounds__(256) void selscan_bwd_k(SelScanArgs a) {
-  constexpr int NW = N / 4;
-  __shared__ float ypart[4][SS_T];
-  __shared__ float upart[4][SS_T];
-  __shared__ float dpart[4][SS_T];
-  __shared__ float lam_s[64][N];
-  const int dg = blockIdx.x, b = blockIdx.y;
+// ============================== backward =======================================================
+// A 512-thread workgroup owns SB_KC channels of one batch row and walks the SB_T-step tiles from
+// the last to the first; inside a tile it takes the channels one at a time with all 8 waves:
+// wave w owns states [w NW, (w+1) NW).  For its states a wave
+//   * replays the forward from the saved tile-start state (DPP prefix scan) keeping h_t,
+//   * runs the adjoint x_t = exp(dt_t A)(dy_t C_t + x_{t+1}) as a DPP suffix scan, whose carry into
+//     the previous tile is kept in LDS per (channel, state),
+//   * accumulates dB[t,n] and dC[t,n] for ITS states over all channels of the group in REGISTERS
+//     (written once per tile as the group's partial; deterministic, no atomics).
+// Sums over n (du, ddelta, y for dz) go through one LDS row per wave and are finished item-parallel
+// (thread = time step, fixed-order sum over the 8 rows, coalesced I/O).
+template <typename T, int N, bool VEC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void selscan_bwd_k(SelScanArgs a) {
+  constexpr int NW = N >= SB_W ? N / SB_W : 1;
+  constexpr int IT = SB_IT;
+  __shared__ float part[SB_W][3][SB_T];
+  __shared__ __attribute__((aligned(16))) bf16_t BCs[2][N][SB_T];  // this tile's B, C (group of d0), bf16 as in HBM
+  __shared__ float lamc[SB_KC][N];
+  __shared__ float dAacc[SB_KC][N];
+  __shared__ float dDacc[SB_KC][SB_W], dbacc[SB_KC][SB_W];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int d0 = dg * a.Kc, nch = min(a.Kc, a.D - d0);
-  const int ntiles = (a.L + SS_T - 1) / SS_T;
-  const int ndg = (a.D + a.Kc - 1) / a.Kc;
-  for (int v = threadIdx.x; v < 64 * N; v += 256) lam_s[v / N][v % N] = 0.f;
+  const int dg = blockIdx.x, b = blockIdx.y;
+  const int d0 = dg * SB_KC, nch = min(SB_KC, a.D - d0);
+  const int ntl = (a.L + SB_T - 1) / SB_T;
+  const int ndg = (a.D + SB_KC - 1) / SB_KC;
+  const bool has_states = w * NW < N;
+  for (int v = threadIdx.x; v < SB_KC * N; v += 64 * SB_W) {
+    (&lamc[0][0])[v] = 0.f;
+    (&dAacc[0][0])[v] = 0.f;
+  }
+  for (int v = threadIdx.x; v < SB_KC * SB_W; v += 64 * SB_W) {
+    (&dDacc[0][0])[v] = 0.f;
+    (&dbacc[0][0])[v] = 0.f;
+  }
   __syncthreads();
-  for (int tile = ntiles - 1; tile >= 0; --tile) {
-    const int t0 = tile * SS_T;
-    const int tl = t0 + lane * SS_ITEMS;
-    float dBa[NW][SS_ITEMS], dCa[NW][SS_ITEMS];
+  for (int tile = ntl - 1; tile >= 0; --tile) {
+    const int tl = tile * SB_T + lane * IT;
+    float accB[NW][IT], accC[NW][IT];
 #pragma unroll
     for (int nn = 0; nn < NW; ++nn)
 #pragma unroll
-      for (int i = 0; i < SS_ITEMS; ++i) dBa[nn][i] = dCa[nn][i] = 0.f;
-    for (int ci = 0; ci < nch; ++ci) {
-      const int d = d0 + ci;
+      for (int i = 0; i < IT; ++i) accB[nn][i] = accC[nn][i] = 0.f;
+    const int g0 = d0 / (a.D / a.G);
+    {  // B and C do not depend on the channel: stage the tile once for all SB_KC channels
+      const T* Bb = ((const T*)a.Bm_) + (int64_t)b * a.sBb + (int64_t)g0 * a.sBg;
+      const T* Cb = ((const T*)a.Cm_) + (int64_t)b * a.sCb + (int64_t)g0 * a.sCg;
+      for (int v = threadIdx.x; v < N * SB_T; v += 64 * SB_W) {
+        const int n = v / SB_T, t = tile * SB_T + v % SB_T;
+        BCs[0][n][v % SB_T] = f2bf(t < a.L ? ld(Bb + (int64_t)n * a.sBn + t) : 0.f);
+        BCs[1][n][v % SB_T] = f2bf(t < a.L ? ld(Cb + (int64_t)n * a.sCn + t) : 0.f);
+      }
+    }
+    __syncthreads();
+    // next channel's rows, fetched while the current one is processed (VEC path)
+    uint2 nu = make_uint2(0, 0), nd = nu, ng = nu, nz = nu;
+    auto fetch = [&](int k) {
+      if constexpr (VEC) {
+        if (k < nch && tl < a.L) {
+          const int d = d0 + k;
+          nu = *reinterpret_cast<const uint2*>(((const bf16_t*)a.u_) + (int64_t)b * a.sub + (int64_t)d * a.sud + tl);
+          nd = *reinterpret_cast<const uint2*>(((const bf16_t*)a.delta_) + (int64_t)b * a.sdb + (int64_t)d * a.sdd + tl);
+          ng = *reinterpret_cast<const uint2*>(((const bf16_t*)a.dout_) + (int64_t)b * a.sgb + (int64_t)d * a.sgd + tl);
+          if (a.z_) nz = *reinterpret_cast<const uint2*>(((const bf16_t*)a.z_) + (int64_t)b * a.szb + (int64_t)d * a.szd + tl);
+        }
+      }
+    };
+    if (has_states) fetch(0);
+    for (int k = 0; k < nch; ++k) {
+      const int d = d0 + k;
       const int g = d / (a.D / a.G);
       const T* urow = ((const T*)a.u_) + (int64_t)b * a.sub + (int64_t)d * a.sud;
       const T* drow = ((const T*)a.delta_) + (int64_t)b * a.sdb + (int64_t)d * a.sdd;
       const T* grow = ((const T*)a.dout_) + (int64_t)b * a.sgb + (int64_t)d * a.sgd;
       const T* zrow = a.z_ ? ((const T*)a.z_) + (int64_t)b * a.szb + (int64_t)d * a.szd : nullptr;
-      float u[SS_ITEMS], dl[SS_ITEMS], dlraw[SS_ITEMS], go[SS_ITEMS], zz[SS_ITEMS];
-      load_items<T>(urow, tl, a.L, a.vec, u);
-      load_items<T>(drow, tl, a.L, a.vec, dlraw);
-      load_items<T>(grow, tl, a.L, a.vecg, go);
-      if (zrow) load_items<T>(zrow, tl, a.L, a.vecz, zz);
       const float bias = a.delta_bias ? a.delta_bias[d] : 0.f;
-#pragma unroll
-      for (int i = 0; i < SS_ITEMS; ++i) {
-        const float v0 = dlraw[i] + bias;
-        dl[i] = (tl + i < a.L) ? (a.softplus ? softplusf_(v0) : v0) : 0.f;
-      }
-      // ---- phase 1: replay the forward for this wave's states, keep h_{t-1}
-      float hprev[NW][SS_ITEMS];
-      float yp[SS_ITEMS];
-#pragma unroll
-      for (int i = 0; i < SS_ITEMS; ++i) yp[i] = 0.f;
-#pragma unroll
-      for (int nn = 0; nn < NW; ++nn) {
-        const int n = w * NW + nn;
-        const float An = a.A[d * N + n];
-        float Bv[SS_ITEMS], Cv[SS_ITEMS];
-        load_items<T>(((const T*)a.Bm_) + (int64_t)b * a.sBb + (int64_t)g * a.sBg + (int64_t)n * a.sBn, tl, a.L, a.vecbc, Bv);
-        load_items<T>(((const T*)a.Cm_) + (int64_t)b * a.sCb + (int64_t)g * a.sCg + (int64_t)n * a.sCn, tl, a.L, a.vecbc, Cv);
-        float Ac[SS_ITEMS], Bc[SS_ITEMS];
-        float ca = 1.f, cb = 0.f;
-#pragma unroll
-        for (int i = 0; i < SS_ITEMS; ++i) {
-          const float ai = __expf(dl[i] * An);
-          cb = ai * cb + dl[i] * Bv[i] * u[i];
-          ca = ca * ai;
-          Ac[i] = ca;
-          Bc[i] = cb;
+      if (has_states) {
+        const T* Bb = ((const T*)a.Bm_) + (int64_t)b * a.sBb + (int64_t)g * a.sBg;
+        const T* Cb = ((const T*)a.Cm_) + (int64_t)b * a.sCb + (int64_t)g * a.sCg;
+        float u[IT], dl[IT], dy[IT], zz[IT];
+        if constexpr (VEC) {
+          auto unpack4 = [](uint2 v, float (&o)[IT]) {
+            o[0] = __uint_as_float(v.x << 16); o[1] = __uint_as_float(v.x & 0xffff0000u);
+            o[2] = __uint_as_float(v.y << 16); o[3] = __uint_as_float(v.y & 0xffff0000u);
+          };
+          unpack4(nu, u); unpack4(nd, dl); unpack4(ng, dy); unpack4(nz, zz);
+          fetch(k + 1);
+        } else {
+          load_items<VEC, T, IT>(urow, tl, a.L, u);
+          load_items<VEC, T, IT>(drow, tl, a.L, dl);
+          load_items<VEC, T, IT>(grow, tl, a.L, dy);
+          if (zrow) load_items<VEC, T, IT>(zrow, tl, a.L, zz);
         }
-        float sa = ca, sb = cb;
-        wave_affine_scan(sa, sb);
-        float ea = __shfl_up(sa, 1, 64), eb = __shfl_up(sb, 1, 64);
-        if (lane == 0) { ea = 1.f; eb = 0.f; }
-        const float c0 = a.carries[(((int64_t)b * a.D + d) * ntiles + tile) * N + n];
-        const float hs = ea * c0 + eb;
-        float hp = hs;
+        if (zrow) {
 #pragma unroll
-        for (int i = 0; i < SS_ITEMS; ++i) {
-          hprev[nn][i] = hp;
-          const float hi = Ac[i] * hs + Bc[i];
-          yp[i] += Cv[i] * hi;
-          hp = hi;
+          for (int i = 0; i < IT; ++i) dy[i] *= siluf_(zz[i]);
         }
-      }
 #pragma unroll
-      for (int i = 0; i < SS_ITEMS; ++i) ypart[w][lane * SS_ITEMS + i] = yp[i];
-      __syncthreads();
-      const float Dd = a.D_ ? a.D_[d] : 0.f;
-      float dy[SS_ITEMS];
-#pragma unroll
-      for (int i = 0; i < SS_ITEMS; ++i) dy[i] = zrow ? go[i] * siluf_(zz[i]) : go[i];
-      // ---- phase 2: adjoint recurrence per state
-      float dup[SS_ITEMS], ddp[SS_ITEMS];
-#pragma unroll
-      for (int i = 0; i < SS_ITEMS; ++i) dup[i] = ddp[i] = 0.f;
-#pragma unroll
-      for (int nn = 0; nn < NW; ++nn) {
-        const int n = w * NW + nn;
-        const float An = a.A[d * N + n];
-        float Bv[SS_ITEMS], Cv[SS_ITEMS], av[SS_ITEMS];
-        load_items<T>(((const T*)a.Bm_) + (int64_t)b * a.sBb + (int64_t)g * a.sBg + (int64_t)n * a.sBn, tl, a.L, a.vecbc, Bv);
-        load_items<T>(((const T*)a.Cm_) + (int64_t)b * a.sCb + (int64_t)g * a.sCg + (int64_t)n * a.sCn, tl, a.L, a.vecbc, Cv);
-#pragma unroll
-        for (int i = 0; i < SS_ITEMS; ++i) av[i] = __expf(dl[i] * An);
-        // lane-local reverse composition: lambda_i = dyC_i + a_{i+1} lambda_{i+1}
-        // map over the lane's items from the right: (A_i, B_i) with lambda_i = B_i + A_i * lambda_next
-        float ra = 1.f, rb = 0.f;  // composed map of items i..ITEMS-1 wrt lambda after the lane
-        float RA[SS_ITEMS], RB[SS_ITEMS];
-#pragma unroll
-        for (int i = SS_ITEMS - 1; i >= 0; --i) {
-          const float anext = (i + 1 < SS_ITEMS) ? av[i + 1] : 1.f;  // a of the following step (in-lane)
-          // lambda_i = dy_i C_i + anext * lambda_{i+1};  lambda_{i+1} = RB_{i+1} + RA_{i+1} * lam_out
-          rb = dy[i] * Cv[i] + anext * rb;
-          ra = anext * ra;
-          RA[i] = ra;
-          RB[i] = rb;
+        for (int i = 0; i < IT; ++i) {
+          const float v = dl[i] + bias;
+          dl[i] = (tl + i < a.L) ? (a.softplus ? softplus_fast(v) : v) : 0.f;
         }
-        // across lanes: lam_out of lane L = a_first(L+1) * lambda_first(L+1)
-        // lane map: lambda_0 = RB_0 + RA_0 * lam_out; contribution to previous lane: a0 * lambda_0
-        float ma = av[0] * RA[0], mb = av[0] * RB[0];
-        wave_affine_rscan(ma, mb);  // lane i: composed map for lanes i..63 (input: carry from next tile)
-        float na = __shfl_down(ma, 1, 64), nb = __shfl_down(mb, 1, 64);
-        if (lane == 63) { na = 1.f; nb = 0.f; }
-        const float cin = lam_s[ci][n];  // a_T * lambda_T from the following tile
-        const float lam_out = nb + na * cin;
-        float dAp = 0.f;
+        float du[IT], dd[IT], yv[IT];
 #pragma unroll
-        for (int i = 0; i < SS_ITEMS; ++i) {
-          const float lam = RB[i] + RA[i] * lam_out;
-          const float dlu = dl[i] * u[i];
-          dBa[nn][i] += lam * dlu;
-          const float hcur = av[i] * hprev[nn][i] + dl[i] * Bv[i] * u[i];
-          dCa[nn][i] += dy[i] * hcur;
-          dup[i] += lam * dl[i] * Bv[i];
-          const float t1 = lam * av[i] * hprev[nn][i];
-          ddp[i] += lam * u[i] * Bv[i] + An * t1;
-          dAp += dl[i] * t1;
-        }
-        const float cnew = __shfl(mb + ma * cin, 0, 64);  // a_0 * lambda_0 of this tile (lane 0)
-        dAp = wave_sum(dAp);
-        if (lane == 0) {
-          lam_s[ci][n] = cnew;
-          a.part_dA[((int64_t)b * a.D + d) * N + n] += dAp;
-        }
-      }
-      __syncthreads();  // ypart reads done before the partial rows are reused
-#pragma unroll
-      for (int i = 0; i < SS_ITEMS; ++i) {
-        upart[w][lane * SS_ITEMS + i] = dup[i];
-        dpart[w][lane * SS_ITEMS + i] = ddp[i];
-      }
-      __syncthreads();
-      T* durow = ((T*)a.du_) + (int64_t)b * a.sdub + (int64_t)d * a.sdud;
-      T* ddrow = ((T*)a.ddelta_) + (int64_t)b * a.sddb + (int64_t)d * a.sddd;
-      T* dzrow = a.dz_ ? ((T*)a.dz_) + (int64_t)b * a.sdzb + (int64_t)d * a.sdzd : nullptr;
-      float dDp = 0.f, dbp = 0.f;
-      for (int k = threadIdx.x; k < SS_T; k += 256) {
-        const int t = t0 + k;
-        if (t < a.L) {
-          const float uu = ld(urow + t);
-          const float g = ld(grow + t);
-          float dyv = g, y = ypart[0][k] + ypart[1][k] + ypart[2][k] + ypart[3][k] + Dd * uu;
-          if (zrow) {
-            const float zv = ld(zrow + t);
-            const float sg = sigmoidf_(zv);
-            dyv = g * zv * sg;
-            if (dzrow) st(dzrow + t, g * y * sg * (1.f + zv * (1.f - sg)));
+        for (int i = 0; i < IT; ++i) du[i] = dd[i] = yv[i] = 0.f;
+        // runtime loop over this wave's states; the accumulators rotate so the live one is always
+        // slot 0 (static register indices, no overlap of the states' working sets)
+#pragma unroll 1
+        for (int nn = 0; nn < NW; ++nn) {
+          const int n = w * NW + nn;
+          const float An = a.A[d * N + n];
+          const float A2 = An * kLog2e;
+          float Bv[IT], Cv[IT], av[IT], hs[IT];
+          if (g == g0) {
+            static_assert(IT == 4, "LDS B/C reads are one 8-byte read per lane");
+            const uint2 bq = *reinterpret_cast<const uint2*>(&BCs[0][n][lane * IT]);
+            const uint2 cq = *reinterpret_cast<const uint2*>(&BCs[1][n][lane * IT]);
+            Bv[0] = __uint_as_float(bq.x << 16); Bv[1] = __uint_as_float(bq.x & 0xffff0000u);
+            Bv[2] = __uint_as_float(bq.y << 16); Bv[3] = __uint_as_float(bq.y & 0xffff0000u);
+            Cv[0] = __uint_as_float(cq.x << 16); Cv[1] = __uint_as_float(cq.x & 0xffff0000u);
+            Cv[2] = __uint_as_float(cq.y << 16); Cv[3] = __uint_as_float(cq.y & 0xffff0000u);
+          } else {
+            load_items<VEC, T, IT>(Bb + (int64_t)n * a.sBn, tl, a.L, Bv);
+            load_items<VEC, T, IT>(Cb + (int64_t)n * a.sCn, tl, a.L, Cv);
           }
-          st(durow + t, upart[0][k] + upart[1][k] + upart[2][k] + upart[3][k] + Dd * dyv);
-          const float raw = ld(drow + t) + bias;
-          const float ddl = (dpart[0][k] + dpart[1][k] + dpart[2][k] + dpart[3][k]) *
-                            (a.softplus ? sigmoidf_(raw) : 1.f);
-          st(ddrow + t, ddl);
-          dDp += dyv * uu;
-          dbp += ddl;
+          // forward replay from the saved tile-start state
+          float ca = 1.f, cb = 0.f;
+#pragma unroll
+          for (int i = 0; i < IT; ++i) {
+            av[i] = __builtin_amdgcn_exp2f(dl[i] * A2);
+            cb = fmaf(av[i], cb, dl[i] * u[i] * Bv[i]);
+            ca *= av[i];
+          }
+          scan_prefix(ca, cb);
+          const float hc0 = a.carries[(((int64_t)b * a.D + d) * ntl + tile) * N + n];
+          const float hend = fmaf(ca, hc0, cb);
+          float h = dppf<0x138>(hc0, hend);
+#pragma unroll
+          for (int i = 0; i < IT; ++i) {
+            h = fmaf(av[i], h, dl[i] * u[i] * Bv[i]);
+            hs[i] = h;
+            yv[i] = fmaf(Cv[i], h, yv[i]);
+          }
+          // adjoint: x_t = av_t (dy_t C_t + x_{t+1}),  lambda_t = dy_t C_t + x_{t+1}
+          float ma = 1.f, mb = 0.f;
+#pragma unroll
+          for (int i = IT - 1; i >= 0; --i) {
+            mb = av[i] * fmaf(dy[i], Cv[i], mb);
+            ma *= av[i];
+          }
+          scan_suffix(ma, mb);
+          const float xc = lamc[k][n];
+          const float xfirst = fmaf(ma, xc, mb);
+          float x = dppf<0x130>(xc, xfirst);  // wave_shl:1 -> x after this lane's last step
+          const float xnew = readlanef(xfirst, 0);
+          float dAp = 0.f;
+#pragma unroll
+          for (int i = IT - 1; i >= 0; --i) {
+            const float lam = fmaf(dy[i], Cv[i], x);
+            x = av[i] * lam;
+            const float dlu = dl[i] * u[i];
+            accB[0][i] = fmaf(lam, dlu, accB[0][i]);
+            accC[0][i] = fmaf(dy[i], hs[i], accC[0][i]);
+            du[i] = fmaf(lam, Bv[i], du[i]);
+            const float t1 = lam * (hs[i] - dlu * Bv[i]);  // lam * av * h_{t-1}
+            dd[i] = fmaf(lam * u[i], Bv[i], fmaf(An, t1, dd[i]));
+            dAp = fmaf(dl[i], t1, dAp);
+          }
+          dAp = wave_sum_dpp(dAp);
+          if (lane == 0) {
+            lamc[k][n] = xnew;
+            dAacc[k][n] += dAp;
+          }
+#pragma unroll
+          for (int i = 0; i < IT; ++i) {
+            const float tb = accB[0][i], tc = accC[0][i];
+#pragma unroll
+            for (int q = 0; q + 1 < NW; ++q) {
+              accB[q][i] = accB[q + 1][i];
+              accC[q][i] = accC[q + 1][i];
+            }
+            accB[NW - 1][i] = tb;
+            accC[NW - 1][i] = tc;
+          }
         }
-      }
-      dDp = wave_sum(dDp);
-      dbp = wave_sum(dbp);
-      // per-channel partials summed over the 4 waves in a fixed order through LDS
-      __syncthreads();
-      if (lane == 0) {
-        upart[w][0] = dDp;
-        dpart[w][0] = dbp;
-      }
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        a.part_dD[(int64_t)b * a.D + d] += upart[0][0] + upart[1][0] + upart[2][0] + upart[3][0];
-        a.part_dbias[(int64_t)b * a.D + d] += dpart[0][0] + dpart[1][0] + dpart[2][0] + dpart[3][0];
-      }
-      __syncthreads();
-    }
-    // tile partials of dB / dC for this channel group
 #pragma unroll
-    for (int nn = 0; nn < NW; ++nn) {
-      const int n = w * NW + nn;
-      float* pb = a.part_dB + (((int64_t)b * ndg + dg) * N + n) * a.L;
-      float* pc = a.part_dC + (((int64_t)b * ndg + dg) * N + n) * a.L;
+        for (int i = 0; i < IT; ++i) {
+          part[w][0][lane * IT + i] = du[i] * dl[i];
+          part[w][1][lane * IT + i] = dd[i];
+          part[w][2][lane * IT + i] = yv[i];
+        }
+      } else {
 #pragma unroll
-      for (int i = 0; i < SS_ITEMS; ++i) {
-        const int t = tl + i;
+        for (int i = 0; i < IT; ++i) part[w][0][lane * IT + i] = part[w][1][lane * IT + i] = part[w][2][lane * IT + i] = 0.f;
+      }
+      __syncthreads();
+      // finish item-parallel: thread j <-> step tile*SB_T + j
+      float dDp = 0.f, dbp = 0.f;
+      if (threadIdx.x < SB_T) {
+        const int j = threadIdx.x, t = tile * SB_T + j;
         if (t < a.L) {
-          pb[t] = dBa[nn][i];
-          pc[t] = dCa[nn][i];
+          float sdu = 0.f, sdd = 0.f, sy = 0.f;
+#pragma unroll
+          for (int v = 0; v < SB_W; ++v) {
+            sdu += part[v][0][j];
+            sdd += part[v][1][j];
+            sy += part[v][2][j];
+          }
+          const float Dd = a.D_ ? a.D_[d] : 0.f;
+          const float uu = ld(urow + t), raw = ld(drow + t) + bias, go = ld(grow + t);
+          float dyv = go, dz = 0.f;
+          if (zrow) {
+            const float zv = ld(zrow + t), sg = sigmoidf_(zv);
+            dyv = go * zv * sg;
+            dz = go * fmaf(Dd, uu, sy) * sg * (1.f + zv * (1.f - sg));
+          }
+          const float ddl = sdd * (a.softplus ? sigmoidf_(raw) : 1.f);
+          st(((T*)a.du_) + (int64_t)b * a.sdub + (int64_t)d * a.sdud + t, fmaf(Dd, dyv, sdu));
+          st(((T*)a.ddelta_) + (int64_t)b * a.sddb + (int64_t)d * a.sddd + t, ddl);
+          if (zrow && a.dz_) st(((T*)a.dz_) + (int64_t)b * a.sdzb + (int64_t)d * a.sdzd + t, dz);
+          dDp = dyv * uu;
+          dbp = ddl;
+        }
+      }
+      dDp = wave_sum_dpp(dDp);
+      dbp = wave_sum_dpp(dbp);
+      if (lane == 0) {
+        dDacc[k][w] += dDp;
+        dbacc[k][w] += dbp;
+      }
+      __syncthreads();  // part[] consumed before the next channel overwrites it
+    }
+    // this tile's dB / dC partial for the group's channels (this wave's states)
+    if (has_states) {
+#pragma unroll
+      for (int nn = 0; nn < NW; ++nn) {
+        const int n = w * NW + nn;
+        float* pb = a.part_dB + (((int64_t)b * ndg + dg) * N + n) * a.L;
+        float* pc = a.part_dC + (((int64_t)b * ndg + dg) * N + n) * a.L;
+        if (tl + IT <= a.L && (a.L % 4) == 0) {
+          *reinterpret_cast<float4*>(pb + tl) = make_float4(accB[nn][0], accB[nn][1], accB[nn][2], accB[nn][3]);
+          *reinterpret_cast<float4*>(pc + tl) = make_float4(accC[nn][0], accC[nn][1], accC[nn][2], accC[nn][3]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < IT; ++i)
+            if (tl + i < a.L) {
+              pb[tl + i] = accB[nn][i];
+              pc[tl + i] = accC[nn][i];
+            }
         }
       }
     }
+  }
+  __syncthreads();
+  for (int v = threadIdx.x; v < nch * N; v += 64 * SB_W)
+    a.part_dA[((int64_t)b * a.D + d0 + v / N) * N + v % N] = dAacc[v / N][v % N];
+  for (int v = threadIdx.x; v < nch; v += 64 * SB_W) {
+    float sD = 0.f, sb = 0.f;
+#pragma unroll
+    for (int q = 0; q < SB_W; ++q) {
+      sD += dDacc[v][q];
+      sb += dbacc[v][q];
+    }
+    a.part_dD[(int64_t)b * a.D + d0 + v] = sD;
+    a.part_dbias[(int64_t)b * a.D + d0 + v] = sb;
   }
 }
 
@@ -391,18 +502,22 @@ __global__ void selscan_reduce_bc_k(SelScanArgs a) {
   } while (0)
 
 hipError_t launch_selscan_fwd(const SelScanArgs& a, hipStream_t st) {
-  if (a.Kc > 64) return hipErrorInvalidValue;
-  dim3 grid((a.D + a.Kc - 1) / a.Kc, a.B), block(256);
-  SS_DISPATCH(hipLaunchKernelGGL((selscan_fwd_k<TT, NN>), grid, block, 0, st, a));
+  const int64_t rows = (int64_t)a.B * a.D;
+  dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  const bool v = a.dtype == kBF16 && a.vec && a.vecbc && (!a.z_ || a.vecz) && a.L % SF_IT == 0;
+  if (v) SS_DISPATCH(hipLaunchKernelGGL((selscan_fwd_k<TT, NN, true>), grid, block, 0, st, a));
+  else SS_DISPATCH(hipLaunchKernelGGL((selscan_fwd_k<TT, NN, false>), grid, block, 0, st, a));
   return hipGetLastError();
 }
 
-int selscan_ntiles(int L) { return (L + SS_T - 1) / SS_T; }
+int selscan_ntiles(int L) { return (L + SB_T - 1) / SB_T; }
 
 hipError_t launch_selscan_bwd(const SelScanArgs& a, hipStream_t st) {
-  if (a.Kc > 64) return hipErrorInvalidValue;
-  dim3 grid((a.D + a.Kc - 1) / a.Kc, a.B), block(256);
-  SS_DISPATCH(hipLaunchKernelGGL((selscan_bwd_k<TT, NN>), grid, block, 0, st, a));
+  if (a.Kc != SB_KC) return hipErrorInvalidValue;
+  dim3 grid((a.D + SB_KC - 1) / SB_KC, a.B), block(64 * SB_W);
+  const bool v = a.dtype == kBF16 && a.vec && a.vecbc && a.vecg && (!a.z_ || a.vecz) && a.L % 8 == 0;
+  if (v) SS_DISPATCH(hipLaunchKernelGGL((selscan_bwd_k<TT, NN, true>), grid, block, 0, st, a));
+  else SS_DISPATCH(hipLaunchKernelGGL((selscan_bwd_k<TT, NN, false>), grid, block, 0, st, a));
   MAMBA_HIP_CHECK(hipGetLastError());
   const int64_t total = (int64_t)a.B * a.G * a.N * a.L;
   if (a.dtype == kBF16)

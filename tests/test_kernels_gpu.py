@@ -211,12 +211,13 @@ def test_mamba2_inner(cuda):
         assert rel(a, b_) < 3e-2, (i, rel(a, b_))
 
 
-@pytest.mark.parametrize("L", [512, 700])
+@pytest.mark.parametrize("L,n", [(512, 16), (700, 16), (2048, 16), (1500, 8), (256, 4)])
 @pytest.mark.parametrize("with_z", [True, False])
-def test_selective_scan(cuda, L, with_z):
+def test_selective_scan(cuda, L, n, with_z):
+    """vector path (L % 16 == 0), guarded path, several forward/backward tiles, N = 16/8/4."""
     from mamba_distributed_amd.ops.selective_scan import selective_scan_fn
     torch.manual_seed(5)
-    b, d, n = 2, 96, 16
+    b, d = 2, 96
     u = torch.randn(b, d, L, device=cuda).to(torch.bfloat16)
     delta = (torch.randn(b, d, L, device=cuda) * 0.5 - 1).to(torch.bfloat16)
     A = -torch.rand(d, n, device=cuda) * 4 - 0.1
