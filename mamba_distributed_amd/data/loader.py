@@ -90,6 +90,12 @@ class SyntheticTokens:
         buf = torch.randint(0, self.V, (self.B * self.T + 1,), generator=self.gen, device=self.device)
         return buf[:-1].view(self.B, self.T), buf[1:].view(self.B, self.T)
 
+    def state_dict(self):
+        return {"generator": self.gen.get_state().cpu()}
+
+    def load_state_dict(self, s):
+        self.gen.set_state(s["generator"])
+
 
 def write_synthetic_shards(root: str, n_train: int = 2, n_val: int = 1, tokens_per_shard: int = 1 << 16,
                            vocab_size: int = 50304, seed: int = 0, dtype=np.uint16) -> List[str]:

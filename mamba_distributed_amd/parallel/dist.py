@@ -60,7 +60,17 @@ def init_distributed(backend: str = "auto", device_type: str = "auto", timeout_s
     kw = {}
     if backend == "nccl" and want_cuda:
         kw["device_id"] = torch.device(dev)
-    dist.init_process_group(backend=backend, timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    timeout = datetime.timedelta(seconds=timeout_s)
+    if os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "").lower() == "true":
+        # under torchrun the agent hosts the rendezvous store and keeps it across worker restarts;
+        # scope this attempt's keys so restarted workers never read the dead attempt's addresses
+        attempt = os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")
+        base = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), world, is_master=False,
+                             timeout=timeout)
+        store = dist.PrefixStore(f"mamba_amd/attempt{attempt}", base)
+        dist.init_process_group(backend=backend, store=store, rank=rank, world_size=world, timeout=timeout, **kw)
+    else:
+        dist.init_process_group(backend=backend, timeout=timeout, **kw)
     return DistInfo(True, rank, local_rank, world, dev, backend)
 
 
@@ -85,6 +95,15 @@ def all_reduce_max(t: torch.Tensor) -> torch.Tensor:
     if dist.is_available() and dist.is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return t
+
+
+def all_gather_object(obj):
+    """List of every rank's ``obj`` (just ``[obj]`` without a process group)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return [obj]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
 
 
 def barrier():

@@ -8,8 +8,14 @@ checkpoint every 1000, samples every 250, ``MambaConfig(d_model=768, vocab_size=
 Log formats are kept byte-compatible (train.py:151, 237-241): ``"{step} val {:.4f}"``,
 ``"{step} train {:.6f}"`` and the ``step {:5d} | loss: ... | tok/sec: ...`` stdout line.
 Additions: flags (model preset, Mamba1/Mamba2, sizes, synthetic data, steps, DDP knobs), resume
-(optimizer + loader + RNG in the checkpoint), steady-state tok/s excluding eval steps (A10),
-optional JSONL metrics.
+(optimizer + every rank's loader position + RNG in the checkpoint), steady-state tok/s excluding
+eval steps (A10), optional JSONL metrics, and a fault-injection hook for the elastic-restart test
+(SURVEY.md §5.3): ``MAMBA_AMD_FAULT_AT_STEP=k`` [``MAMBA_AMD_FAULT_RANK=r``] kills rank r at the start
+of step k on the first torchrun attempt; ``torchrun --max-restarts N ... train.py --resume`` then
+restarts every worker from the latest checkpoint.
+
+Checkpoint timing follows the reference: ``model_{step}.pt`` is written at the START of ``step``
+(after validation, before that step's update), so resuming from it re-runs ``step``.
 """
 from __future__ import annotations
 
@@ -28,7 +34,7 @@ from .config import MambaConfig, preset
 from .data.loader import DataLoaderLite, SyntheticTokens
 from .lm import LMHeadModel
 from .parallel import ddp as ddp_mod
-from .parallel.dist import all_reduce_avg, destroy, init_distributed
+from .parallel.dist import all_gather_object, all_reduce_avg, destroy, init_distributed
 from .utils.checkpoint import latest_checkpoint, load_checkpoint, save_checkpoint, set_rng_state
 from .utils.lr import get_lr
 
@@ -66,6 +72,7 @@ class TrainArgs:
     metrics_jsonl: Optional[str] = None
     sample_prompt: str = "Hello, I'm a language model,"
     device_type: str = "auto"
+    tuned_gemms: bool = True             # replay the shipped gfx950 GEMM solution table
 
 
 def build_config(a: TrainArgs) -> MambaConfig:
@@ -107,6 +114,9 @@ class Trainer:
             self.val_loader = DataLoaderLite(a.B, a.T, self.info.rank, world, "val", self.master, a.data_root)
         if self.device_type == "cuda":
             torch.set_float32_matmul_precision("high")
+            if a.tuned_gemms:
+                from .utils.gemm_tuning import enable_tuned_gemms
+                enable_tuned_gemms()
         self.raw_model = LMHeadModel(self.config, device=self.device)
         self.raw_model.to(self.device)
         if self.master:
@@ -117,6 +127,7 @@ class Trainer:
         os.makedirs(a.log_dir, exist_ok=True)
         self.log_file = os.path.join(a.log_dir, "log.txt")
         self.start_step = 0
+        self.resumed_at = None
         if a.resume:
             self._resume()
         if self.master and self.start_step == 0:
@@ -147,12 +158,16 @@ class Trainer:
             self.optimizer.load_state_dict(ck["optimizer"])
         if "loader" in ck and hasattr(self.train_loader, "load_state_dict"):
             loaders = ck["loader"]
+            if isinstance(loaders, list) and len(loaders) != self.info.world_size and self.master:
+                print(f"warning: checkpoint has {len(loaders)} loader states for world size {self.info.world_size}")
             st = loaders[self.info.rank] if isinstance(loaders, list) and self.info.rank < len(loaders) else None
             if st is not None:
                 self.train_loader.load_state_dict(st)
         if "rng" in ck:
             set_rng_state(ck["rng"])
-        self.start_step = int(ck["step"]) + 1
+        # the checkpoint was taken at the start of ck["step"], before that step's update
+        self.start_step = int(ck["step"])
+        self.resumed_at = self.start_step
         if self.master:
             print(f"resumed from {path} at step {self.start_step}")
 
@@ -208,12 +223,24 @@ class Trainer:
         return loss_accum, norm, lr
 
     def save(self, step, val_loss):
+        """Collective (every rank calls it): gathers all ranks' loader positions, rank 0 writes."""
+        st = self.train_loader.state_dict() if hasattr(self.train_loader, "state_dict") else None
+        loader_states = all_gather_object(st)
+        if not self.master:
+            return None
         path = os.path.join(self.a.log_dir, f"model_{step:05d}.pt")
         opt = self.optimizer if self.a.save_optimizer else None
-        loader_state = self.train_loader.state_dict() if hasattr(self.train_loader, "state_dict") else None
         save_checkpoint(path, self.raw_model, step, val_loss, optimizer=opt,
-                        loader_state=[loader_state] if loader_state is not None else None)
+                        loader_state=loader_states if st is not None else None, include_rng=True)
         return path
+
+    def _maybe_inject_fault(self, step):
+        at = os.environ.get("MAMBA_AMD_FAULT_AT_STEP")
+        if at is None or int(at) != step or os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") != "0":
+            return
+        if self.info.rank == int(os.environ.get("MAMBA_AMD_FAULT_RANK", "0")):
+            print(f"[fault-injection] rank {self.info.rank} exiting at step {step}", flush=True)
+            os._exit(17)
 
     def run(self):
         a = self.a
@@ -223,18 +250,20 @@ class Trainer:
             t0 = time.time()
             last_step = step == last - 1
             eval_step = False
-            if step % a.val_every == 0 or last_step:
+            resumed_here = step == self.resumed_at  # its validation/checkpoint happened before the restart
+            if (step % a.val_every == 0 or last_step) and not resumed_here:
                 eval_step = True
                 val_loss = self.validate()
                 if self.master:
                     print(f"validation loss: {val_loss:.4f}")
                     with open(self.log_file, "a") as f:
                         f.write(f"{step} val {val_loss:.4f}\n")
-                    if step > 0 and (step % a.ckpt_every == 0 or last_step):
-                        self.save(step, val_loss)
-            if (step > 0 and step % a.sample_every == 0) or last_step:
+                if step > 0 and (step % a.ckpt_every == 0 or last_step):
+                    self.save(step, val_loss)
+            if ((step > 0 and step % a.sample_every == 0) or last_step) and not resumed_here:
                 eval_step = True
                 self.sample()
+            self._maybe_inject_fault(step)
             loss_accum, norm, lr = self.train_step(step)
             if self.device_type == "cuda":
                 torch.cuda.synchronize()

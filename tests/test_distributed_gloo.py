@@ -89,3 +89,45 @@ def test_two_node_rendezvous_on_localhost(tmp_path):
         assert p.returncode == 0, e[-3000:]
     sd_single, _ = _run_single(tmp_path, data, B=4)
     _assert_close_sd(torch.load(os.path.join(log, "model_00002.pt"))["model"], sd_single)
+
+
+def _loss_by_step(stdout):
+    out = {}
+    for l in stdout.splitlines():
+        if l.startswith("step "):
+            out[int(l.split("|")[0].split()[1])] = float(l.split("loss: ")[1].split(" ")[0])
+    return out  # last occurrence wins (re-run steps after a restart)
+
+
+def test_elastic_restart_resumes_from_checkpoint(tmp_path):
+    """SURVEY.md §5.3 fault injection: rank 1 dies at the start of step 3 on the first attempt;
+    torchrun (--max-restarts 1) restarts both workers, train.py --resume reloads model, optimizer,
+    every rank's loader position and RNG from model_00002.pt (written at the start of step 2) and
+    re-runs steps 2-5.  The losses must equal an uninterrupted run's."""
+    data = str(tmp_path / "data")
+    write_synthetic_shards(data, n_train=1, n_val=1, tokens_per_shard=1 << 14, vocab_size=50304)
+    args = [a for a in COMMON]
+    args[args.index("--steps") + 1] = "6"
+    args[args.index("--val-every") + 1] = "2"
+    args[args.index("--ckpt-every") + 1] = "2"
+
+    def launch(log, restarts, fault):
+        env = _env()
+        if fault:
+            env.update(MAMBA_AMD_FAULT_AT_STEP="3", MAMBA_AMD_FAULT_RANK="1")
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+               "--max-restarts", str(restarts), "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+               os.path.join(ROOT, "train.py"), *args, "--B", "2", "--data-root", data, "--log-dir", log, "--resume"]
+        # own session: the elastic agent signals its process group when it tears workers down
+        return subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=900, start_new_session=True)
+
+    ref = launch(str(tmp_path / "clean"), 0, False)
+    assert ref.returncode == 0, ref.stderr[-3000:]
+    ft = launch(str(tmp_path / "faulty"), 1, True)
+    assert ft.returncode == 0, ft.stderr[-3000:]
+    assert "[fault-injection] rank 1 exiting at step 3" in ft.stdout + ft.stderr
+    assert "model_00002.pt at step 2" in ft.stdout
+    la, lb = _loss_by_step(ref.stdout), _loss_by_step(ft.stdout)
+    assert sorted(la) == list(range(6)) and sorted(lb) == list(range(6)), (la, lb)
+    for s in (2, 3, 4, 5):
+        assert abs(la[s] - lb[s]) <= 1e-6 * abs(la[s]), (s, la[s], lb[s])
