@@ -48,9 +48,10 @@ def test_trainer_logs_checkpoints_and_resume(tmp_path, capsys):
     assert os.path.exists(tmp_path / "model_00003.pt")
     rec = [json.loads(l) for l in open(tmp_path / "m.jsonl")]
     assert [r["step"] for r in rec] == [0, 1, 2, 3]
-    # resume from model_00003.pt continues at step 4
+    # model_00003.pt is written at the START of step 3 (before its update, as in the reference), so
+    # resuming from it re-runs step 3
     t = Trainer(_args(tmp_path, steps=6, resume=True))
-    assert t.start_step == 4
+    assert t.start_step == 3
     t.run()
     lines = open(tmp_path / "log.txt").read().splitlines()
     assert lines[-1].startswith("5 train")
