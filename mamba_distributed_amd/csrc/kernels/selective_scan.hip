@@ -528,39 +528,76 @@ hipError_t launch_selscan_bwd(const SelScanArgs& a, hipStream_t st) {
 }
 
 // ---- single-token state update (decode), Mamba-1 and Mamba-2 forms -------------------------
-// state (b, H, P, N) fp32 [Mamba-1: H = d, P = 1]; x, z (b, H, P); dt (b, H) [Mamba-1: dt per d]
-template <typename T>
-__global__ void ssm_update_k(SSMUpdateArgs a) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // over B*H*P
-  if (i >= (int64_t)a.B * a.H * a.P) return;
-  const int p = i % a.P, h = (i / a.P) % a.H, b = i / ((int64_t)a.P * a.H);
-  const int g = h / (a.H / a.G);
-  float dt = ld((const T*)a.dt_ + (int64_t)b * a.sdtb + (int64_t)h * a.sdth + (int64_t)p * a.sdtp);
-  if (a.dt_bias) dt += a.dt_bias[a.dt_bias_per_p ? h * a.P + p : h];
-  if (a.softplus) dt = softplusf_(dt);
-  const float xv = ld((const T*)a.x_ + (int64_t)b * a.sxb + (int64_t)h * a.sxh + p);
-  float* s = a.state + (((int64_t)b * a.H + h) * a.P + p) * a.N;
-  const T* Bp = ((const T*)a.Bm_) + (int64_t)b * a.sBb + (int64_t)g * a.sBg;
-  const T* Cp = ((const T*)a.Cm_) + (int64_t)b * a.sCb + (int64_t)g * a.sCg;
-  float y = 0.f;
-  for (int n = 0; n < a.N; ++n) {
-    const float An = a.A_per_n ? a.A[(h * a.P + p) * a.N + n] : a.A[h];
-    const float nv = s[n] * __expf(dt * An) + dt * xv * ld(Bp + n);
-    s[n] = nv;
-    y += nv * ld(Cp + n);
+// state (b, H, P, N) fp32 [Mamba-1: H = d, P = 1]; x, z (b, H, P); dt (b, H) [Mamba-1: dt per d].
+// One row (b, h, p) = N contiguous states is owned by a group of LPR = min(N, 64) lanes (NPL states
+// per lane, lane-strided so each load is one coalesced line); y = sum_n C_n h_n is a butterfly over
+// the group.  A decode step is ~B*H*P*N*8 bytes of state traffic, so the layout is chosen for
+// full-width coalesced state reads/writes and enough waves to cover the chip even at batch 1.
+template <typename T, int LPR, int NPL>
+__global__ __launch_bounds__(256) void ssm_update_k(SSMUpdateArgs a) {
+  constexpr int RPW = 64 / LPR;
+  const int lane = threadIdx.x & 63, sub = lane % LPR;
+  const int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / LPR;
+  const int64_t rows = (int64_t)a.B * a.H * a.P;
+  float y = 0.f, xv = 0.f;
+  int p = 0, h = 0, b = 0;
+  if (row < rows) {
+    p = row % a.P;
+    h = (row / a.P) % a.H;
+    b = row / ((int64_t)a.P * a.H);
+    const int g = h / (a.H / a.G);
+    float dt = ld((const T*)a.dt_ + (int64_t)b * a.sdtb + (int64_t)h * a.sdth + (int64_t)p * a.sdtp);
+    if (a.dt_bias) dt += a.dt_bias[a.dt_bias_per_p ? h * a.P + p : h];
+    if (a.softplus) dt = softplusf_(dt);
+    xv = ld((const T*)a.x_ + (int64_t)b * a.sxb + (int64_t)h * a.sxh + p);
+    float* st_ = a.state + row * a.N;
+    const T* Bp = ((const T*)a.Bm_) + (int64_t)b * a.sBb + (int64_t)g * a.sBg;
+    const T* Cp = ((const T*)a.Cm_) + (int64_t)b * a.sCb + (int64_t)g * a.sCg;
+    const float dtx = dt * xv;
+#pragma unroll
+    for (int q = 0; q < NPL; ++q) {
+      const int n = sub + q * LPR;
+      const float An = a.A_per_n ? a.A[(h * a.P + p) * a.N + n] : a.A[h];
+      const float nv = fmaf(st_[n], __expf(dt * An), dtx * ld(Bp + n));
+      st_[n] = nv;
+      y = fmaf(nv, ld(Cp + n), y);
+    }
   }
-  if (a.D) y += xv * a.D[a.D_per_p ? h * a.P + p : h];
-  if (a.z_) y *= siluf_(ld(((const T*)a.z_) + (int64_t)b * a.szb + (int64_t)h * a.szh + p));
-  st(((T*)a.out_) + (int64_t)b * a.H * a.P + (int64_t)h * a.P + p, y);
+#pragma unroll
+  for (int off = LPR / 2; off >= 1; off >>= 1) y += __shfl_xor(y, off, 64);
+  if (row < rows && sub == 0) {
+    if (a.D) y += xv * a.D[a.D_per_p ? h * a.P + p : h];
+    if (a.z_) y *= siluf_(ld(((const T*)a.z_) + (int64_t)b * a.szb + (int64_t)h * a.szh + p));
+    st(((T*)a.out_) + (int64_t)b * a.H * a.P + (int64_t)h * a.P + p, y);
+  }
+}
+
+template <typename T>
+static hipError_t ssm_update_launch(const SSMUpdateArgs& a, hipStream_t st) {
+  const int64_t rows = (int64_t)a.B * a.H * a.P;
+#define SSM_UP(LPR, NPL)                                                                            \
+  {                                                                                                 \
+    const int64_t waves = (rows + (64 / LPR) - 1) / (64 / LPR);                                     \
+    hipLaunchKernelGGL((ssm_update_k<T, LPR, NPL>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, a); \
+    return hipGetLastError();                                                                       \
+  }
+  switch (a.N) {
+    case 4: SSM_UP(4, 1)
+    case 8: SSM_UP(8, 1)
+    case 16: SSM_UP(16, 1)
+    case 32: SSM_UP(32, 1)
+    case 64: SSM_UP(64, 1)
+    case 128: SSM_UP(64, 2)
+    case 256: SSM_UP(64, 4)
+    default: return hipErrorInvalidValue;
+  }
+#undef SSM_UP
 }
 
 hipError_t launch_ssm_update(const SSMUpdateArgs& a, hipStream_t st) {
-  const int64_t n = (int64_t)a.B * a.H * a.P;
-  dim3 grid((unsigned)((n + 255) / 256)), block(256);
-  if (a.dtype == kBF16) hipLaunchKernelGGL(ssm_update_k<bf16_t>, grid, block, 0, st, a);
-  else if (a.dtype == kF32) hipLaunchKernelGGL(ssm_update_k<float>, grid, block, 0, st, a);
-  else return hipErrorInvalidValue;
-  return hipGetLastError();
+  if (a.dtype == kBF16) return ssm_update_launch<bf16_t>(a, st);
+  if (a.dtype == kF32) return ssm_update_launch<float>(a, st);
+  return hipErrorInvalidValue;
 }
 
 }  // namespace mamba_amd

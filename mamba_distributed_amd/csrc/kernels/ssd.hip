@@ -8,14 +8,12 @@
 //
 // Kernels (all MFMA work on v_mfma_f32_16x16x32_bf16; operand layouts in mfma.h):
 //   ssd_cumsum      wave per (b,h,chunk): dt transform + wave64 inclusive scan of dt*A.
-//   ssd_state_fwd   WG per (n-slice of 64, h, b), walks the chunks in order with the running state
-//                   in MFMA accumulators: stores S_in (bf16) per chunk, then S = e^{cum_last} S +
-//                   (w.X)^T B as 16x16x32 MFMAs whose operands come through ds_read_b64_tr_b16
-//                   (token-major tiles contracted over time need the hardware transpose).
-//   ssd_scan_fwd    WG per (chunk, head-group, b): CB^T tiles computed once and kept in registers
-//                   for all heads of the group; per head y = e^{cum} C S_in^T  +  (CB o L)^T-as-A x
-//                   (the masked CB^T accumulator feeds the next MFMA directly, PERM k order) + D x.
-//   ssd_dstate_bwd  reverse-time twin of ssd_state_fwd: dS_out per chunk (bf16), dS_init.
+//   ssd_fused_fwd   WG per (h, b) walks the chunks in order with the running state in MFMA
+//                   accumulators; per chunk: S_in -> HBM (saved for the backward), y = e^{cum} C S_in^T
+//                   + (CB^T o L o dt)-as-A x (the masked CB^T accumulator feeds the next MFMA directly,
+//                   PERM k order) + D x, then S = e^{cum_last} S + (w.X)^T B with operands through
+//                   ds_read_b64_tr_b16 (token-major tiles contracted over time need the transpose).
+//   ssd_dstate_bwd  reverse-time state pass: dS_out per chunk (bf16), dS_init.
 //   ssd_chunk_bwd   WG per (chunk, head-group, b): dM, M, dX, ddt (incl. the in-chunk reverse cumsum
 //                   of dcum), dA/dD/dbias partials; head-summed dCB, dB_off, dC_off accumulators
 //                   stay in registers across the heads of the group (no per-head HBM round trip).
@@ -28,7 +26,7 @@ namespace mamba_amd {
 
 constexpr int Q = 64;
 constexpr int P = 64;
-constexpr int LD64 = 72;  // padded LDS row (elements) for 64-wide bf16 tiles
+constexpr int LD64 = 80;  // padded LDS row (elements) for 64-wide bf16 tiles: conflict-free b128 / tr_perm fragment reads
 
 __device__ __forceinline__ float ld_any(const void* p, int dt, int64_t i) {
   return dt == kF32 ? reinterpret_cast<const float*>(p)[i] : bf2f(reinterpret_cast<const bf16_t*>(p)[i]);
@@ -107,136 +105,92 @@ struct TileState {
   }
 };
 
-// ============================== K1: chunk states + state passing (forward) =================
+// ============================== K1+K2 fused: sequential chunk walk (forward) =================
+// One 256-thread workgroup per (b, h) walks the chunks in order with the running state S (P x N) in
+// MFMA accumulators: wave w owns state rows p in [16w, 16w+16) and output rows i in [16w, 16w+16).
+// Per chunk (two barriers):
+//   S_c -> LDS (bf16) and -> HBM (saved for the backward);
+//   Y = e^{cum_i} C S_c^T + (CB^T o L o dt_j) X + D X        (Y rows stored by the wave that owns them)
+//   S_{c+1} = e^{cl} S_c + (X o w)^T B,  w_j = e^{cl - cum_j} dt_j (applied to the X fragments in VGPRs)
+// X, B, C, cum, dt of chunk c+1 are register-prefetched while chunk c computes.  Against the split
+// state/scan kernels this reads X once, never re-reads the 2x-larger state tensor, and needs no
+// per-head-group CB^T staging: HBM traffic ~ x + y + states instead of 2x + y + 2 states.
 template <int N>
-__global__ __launch_bounds__(256) void ssd_state_fwd_k(SSDArgs a) {
-  __shared__ __attribute__((aligned(16))) bf16_t Xs[Q * LD64];
-  __shared__ __attribute__((aligned(16))) bf16_t Bs[Q * LD64];
-  __shared__ __attribute__((aligned(16))) bf16_t Os[P * LD64];
-  __shared__ float wrow[Q];
-  const int ns = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-  const int g = h / (a.H / a.G);
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const float* cumbh = a.cum + ((int64_t)b * a.H + h) * a.Lp;
-  const float* dtbh = a.dtp + ((int64_t)b * a.H + h) * a.Lp;
-  const bf16_t* xg = a.x + (int64_t)b * a.sxb + (int64_t)h * a.sxh;
-  const bf16_t* bg = a.Bm + (int64_t)b * a.sBb + (int64_t)g * a.sBg + ns * 64;
-  f32x4 acc[4];
-#pragma unroll
-  for (int nt = 0; nt < 4; ++nt) {
-    acc[nt] = zero4();
-    if (a.init) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int p = 16 * w + 4 * (l >> 4) + r, n = ns * 64 + 16 * nt + (l & 15);
-        acc[nt][r] = a.init[(((int64_t)b * a.H + h) * P + p) * N + n];
-      }
-    }
-  }
-  Tile64<256> px, pb;
-  float pw = 0.f, pcl = 0.f;
-  px.load(xg, a.sxl, min(Q, a.L));
-  pb.load(bg, a.sBl, min(Q, a.L));
-  if (threadIdx.x < Q) { pw = cumbh[threadIdx.x] ; pcl = cumbh[Q - 1]; pw = __expf(pcl - pw) * dtbh[threadIdx.x]; }
-  for (int c = 0; c < a.nc; ++c) {
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) acc_to_lds(Os, LD64, 16 * w, 16 * nt, acc[nt]);
-    if (threadIdx.x < Q) wrow[threadIdx.x] = pw;
-    const float decay = __expf(cumbh[c * Q + Q - 1]);
-    __syncthreads();
-    store_tile<P, 64>(a.states + ((((int64_t)b * a.nc + c) * a.H + h) * P) * N + ns * 64, N, Os, LD64, P);
-    px.store(Xs, LD64, wrow);
-    pb.store(Bs, LD64);
-    if (c + 1 < a.nc) {  // prefetch chunk c+1 while this chunk's MFMAs run
-      const int valid = min(Q, a.L - (c + 1) * Q);
-      px.load(xg + (int64_t)(c + 1) * Q * a.sxl, a.sxl, valid);
-      pb.load(bg + (int64_t)(c + 1) * Q * a.sBl, a.sBl, valid);
-      if (threadIdx.x < Q) {
-        const int t = (c + 1) * Q + threadIdx.x;
-        pw = __expf(cumbh[(c + 1) * Q + Q - 1] - cumbh[t]) * dtbh[t];
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) acc[nt] *= decay;
-#pragma unroll
-    for (int ks = 0; ks < Q / 32; ++ks) {
-      const bf16x8 A = frag_tr(Xs, LD64, 32 * ks, 16 * w);
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) acc[nt] = mfma16(A, frag_tr(Bs, LD64, 32 * ks, 16 * nt), acc[nt]);
-    }
-  }
-  if (a.final_state) {
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int p = 16 * w + 4 * (l >> 4) + r, n = ns * 64 + 16 * nt + (l & 15);
-        a.final_state[(((int64_t)b * a.H + h) * P + p) * N + n] = acc[nt][r];
-      }
-  }
-}
-
-// ============================== K2: chunk output (forward) ==================================
-template <int N>
-__global__ __launch_bounds__(256) void ssd_scan_fwd_k(SSDArgs a) {
-  constexpr int LDN = N + 8;
+__global__ __launch_bounds__(256) void ssd_fused_fwd_k(SSDArgs a) {
+  constexpr int LDN = N + 16;  // conflict-free ds_read_b128 fragments (see LD64)
+  constexpr int NTS = N / 16;  // state n-tiles per wave
   __shared__ __attribute__((aligned(16))) bf16_t Cs[Q * LDN];
   __shared__ __attribute__((aligned(16))) bf16_t Bs[Q * LDN];
   __shared__ __attribute__((aligned(16))) bf16_t Ss[P * LDN];
   __shared__ __attribute__((aligned(16))) bf16_t Xs[Q * LD64];
-  __shared__ __attribute__((aligned(16))) bf16_t XDs[Q * LD64];  // also the output staging tile
-  __shared__ float cumr[Q], dtr[Q];
-  bf16_t* Os = XDs;
-  const int c = blockIdx.x, hgi = blockIdx.y, b = blockIdx.z;
-  const int h0 = hgi * a.HG, g = h0 / (a.H / a.G);
+  __shared__ __attribute__((aligned(16))) bf16_t Os[Q * LD64];
+  __shared__ __attribute__((aligned(16))) float cumr[Q], dtr[Q], wjr[Q];  // wjr = e^{cl-cum_j} dt_j
+  const int h = blockIdx.x, b = blockIdx.y;
+  const int g = h / (a.H / a.G);
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const int valid = min(Q, a.L - c * Q);
-  // prefetch head h0's tiles before the shared C/B work
-  Tile64<256> px;
-  TileState<256, N> ps;
-  float pc = 0.f, pd = 0.f;
-  auto prefetch = [&](int h) {
-    px.load(a.x + (int64_t)b * a.sxb + (int64_t)c * Q * a.sxl + (int64_t)h * a.sxh, a.sxl, valid);
-    ps.load(a.states + ((((int64_t)b * a.nc + c) * a.H + h) * P) * N);
-    if (threadIdx.x < Q) {
-      const int64_t bh = ((int64_t)b * a.H + h) * a.Lp + (int64_t)c * Q + threadIdx.x;
-      pc = a.cum[bh];
-      pd = a.dtp[bh];
-    }
-  };
-  prefetch(h0);
-  stage_tile<Q, N>(Cs, LDN, a.Cm + (int64_t)b * a.sCb + (int64_t)c * Q * a.sCl + (int64_t)g * a.sCg, a.sCl, valid);
-  stage_tile<Q, N>(Bs, LDN, a.Bm + (int64_t)b * a.sBb + (int64_t)c * Q * a.sBl + (int64_t)g * a.sBg, a.sBl, valid);
-  __syncthreads();
-  // CB^T tiles: rows j (tile jt), cols i (tile w); only jt <= w is ever non-zero (causal)
-  f32x4 cbt[4];
+  const int li = l & 15, lg = l >> 4;
+  const float* cumbh = a.cum + ((int64_t)b * a.H + h) * a.Lp;
+  const float* dtbh = a.dtp + ((int64_t)b * a.H + h) * a.Lp;
+  const bf16_t* xg = a.x + (int64_t)b * a.sxb + (int64_t)h * a.sxh;
+  const bf16_t* bg = a.Bm + (int64_t)b * a.sBb + (int64_t)g * a.sBg;
+  const bf16_t* cg = a.Cm + (int64_t)b * a.sCb + (int64_t)g * a.sCg;
+  const float Dh = a.D ? a.D[h] : 0.f;
+  f32x4 st[NTS];  // S rows 16w + 4lg + r, cols 16nt + li
 #pragma unroll
-  for (int jt = 0; jt < 4; ++jt) {
-    cbt[jt] = zero4();
-    if (jt <= w) {
+  for (int nt = 0; nt < NTS; ++nt) {
+    st[nt] = zero4();
+    if (a.init) {
 #pragma unroll
-      for (int ks = 0; ks < N / 32; ++ks)
-        cbt[jt] = mfma16(frag_kc(Bs, LDN, 16 * jt, 32 * ks), frag_kc(Cs, LDN, 16 * w, 32 * ks), cbt[jt]);
+      for (int r = 0; r < 4; ++r)
+        st[nt][r] = a.init[(((int64_t)b * a.H + h) * P + 16 * w + 4 * lg + r) * N + 16 * nt + li];
     }
   }
-  const float Dh0 = 0.f;
-  (void)Dh0;
-  for (int hh = 0; hh < a.HG; ++hh) {
-    const int h = h0 + hh;
-    __syncthreads();  // previous head's readers of Xs / XDs(Os) / Ss / cumr are done
-    if (threadIdx.x < Q) {
-      cumr[threadIdx.x] = pc;
-      dtr[threadIdx.x] = pd;
+  Tile64<256> px;
+  TileState<256, N> pb, pc;
+  float pcum = 0.f, pdt = 0.f;
+  auto prefetch = [&](int c) {
+    const int valid = min(Q, a.L - c * Q);
+    px.load(xg + (int64_t)c * Q * a.sxl, a.sxl, valid);
+#pragma unroll
+    for (int i = 0; i < N / 64; ++i) {
+      pb.t[i].load(bg + (int64_t)c * Q * a.sBl + 64 * i, a.sBl, valid);
+      pc.t[i].load(cg + (int64_t)c * Q * a.sCl + 64 * i, a.sCl, valid);
     }
+    if (threadIdx.x < Q) {
+      pcum = cumbh[c * Q + threadIdx.x];
+      pdt = dtbh[c * Q + threadIdx.x];
+    }
+  };
+  prefetch(0);
+  for (int c = 0; c < a.nc; ++c) {
+    const int valid = min(Q, a.L - c * Q);
+    __syncthreads();  // chunk c-1 is fully consumed
     px.store(Xs, LD64);
-    ps.store(Ss, LDN);
+    pb.store(Bs, LDN);
+    pc.store(Cs, LDN);
+    if (threadIdx.x < Q) {  // wave 0: lane = local step
+      cumr[threadIdx.x] = pcum;
+      dtr[threadIdx.x] = pdt;
+      wjr[threadIdx.x] = __expf(__shfl(pcum, Q - 1, 64) - pcum) * pdt;
+    }
+#pragma unroll
+    for (int nt = 0; nt < NTS; ++nt) acc_to_lds(Ss, LDN, 16 * w, 16 * nt, st[nt]);
     __syncthreads();
-    px.store(XDs, LD64, dtr);
-    if (hh + 1 < a.HG) prefetch(h + 1);
-    __syncthreads();
+    if (c + 1 < a.nc) prefetch(c + 1);
+    const float cl = cumr[Q - 1];
+    // ---- save S_c for the backward (rows 16w.., one 16-B vector per lane per 64 columns)
+    {
+      bf16_t* sg = a.states + ((((int64_t)b * a.nc + c) * a.H + h) * P) * N;
+#pragma unroll
+      for (int q = 0; q < N / 64; ++q) {
+        const int row = 16 * w + (l >> 2), col = 64 * q + 16 * (l & 3);
+        *reinterpret_cast<uint4*>(sg + (int64_t)row * N + col) = *reinterpret_cast<const uint4*>(Ss + row * LDN + col);
+        *reinterpret_cast<uint4*>(sg + (int64_t)row * N + col + 8) =
+            *reinterpret_cast<const uint4*>(Ss + row * LDN + col + 8);
+      }
+    }
+    // ---- Y_off = e^{cum_i} C_i . S_c^T   (rows i of tile w, 4 p-tiles)
     f32x4 acc[4];
-    // y_off = e^{cum_i} C_i . S^T
 #pragma unroll
     for (int pt = 0; pt < 4; ++pt) {
       acc[pt] = zero4();
@@ -244,22 +198,34 @@ __global__ __launch_bounds__(256) void ssd_scan_fwd_k(SSDArgs a) {
       for (int ks = 0; ks < N / 32; ++ks)
         acc[pt] = mfma16(frag_kc(Cs, LDN, 16 * w, 32 * ks), frag_kc(Ss, LDN, 16 * pt, 32 * ks), acc[pt]);
     }
+    {
+      const float4 ci = *reinterpret_cast<const float4*>(&cumr[16 * w + 4 * lg]);
+      const float e[4] = {__expf(ci.x), __expf(ci.y), __expf(ci.z), __expf(ci.w)};
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float e = __expf(cumr[16 * w + 4 * (l >> 4) + r]);
+      for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int pt = 0; pt < 4; ++pt) acc[pt][r] *= e;
+        for (int pt = 0; pt < 4; ++pt) acc[pt][r] *= e[r];
     }
-    // y_diag: masked CB^T (rows j, cols i) used as A = (M^T)^T in PERM order
-    const int i_col = 16 * w + (l & 15);
+    // ---- Y_diag: CB^T tiles (rows j of tile jt <= w, cols i of tile w), masked, decayed, x dt_j
+    const int i_col = 16 * w + li;
     const float cum_i = cumr[i_col];
     f32x4 mt[4];
 #pragma unroll
     for (int jt = 0; jt < 4; ++jt) {
+      mt[jt] = zero4();
+      if (jt <= w) {
+        f32x4 cb = zero4();
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int j = 16 * jt + 4 * (l >> 4) + r;
-        mt[jt][r] = (jt <= w && j <= i_col) ? cbt[jt][r] * __expf(cum_i - cumr[j]) : 0.f;
+        for (int ks = 0; ks < N / 32; ++ks)
+          cb = mfma16(frag_kc(Bs, LDN, 16 * jt, 32 * ks), frag_kc(Cs, LDN, 16 * w, 32 * ks), cb);
+        const float4 cj4 = *reinterpret_cast<const float4*>(&cumr[16 * jt + 4 * lg]);
+        const float4 dj4 = *reinterpret_cast<const float4*>(&dtr[16 * jt + 4 * lg]);
+        const float cj[4] = {cj4.x, cj4.y, cj4.z, cj4.w}, dj[4] = {dj4.x, dj4.y, dj4.z, dj4.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int j = 16 * jt + 4 * lg + r;
+          mt[jt][r] = (j <= i_col) ? cb[r] * __expf(cum_i - cj[r]) * dj[r] : 0.f;
+        }
       }
     }
 #pragma unroll
@@ -267,23 +233,47 @@ __global__ __launch_bounds__(256) void ssd_scan_fwd_k(SSDArgs a) {
       if (2 * ks <= w) {
         const bf16x8 A = acc_frag(mt[2 * ks], mt[2 * ks + 1]);
 #pragma unroll
-        for (int pt = 0; pt < 4; ++pt) acc[pt] = mfma16(A, frag_tr_perm(XDs, LD64, 32 * ks, 16 * pt), acc[pt]);
+        for (int pt = 0; pt < 4; ++pt) acc[pt] = mfma16(A, frag_tr_perm(Xs, LD64, 32 * ks, 16 * pt), acc[pt]);
       }
     }
-    const float Dh = a.D ? a.D[h] : 0.f;
-    bf16x4 xr[4];
+    // ---- + D x, stage this wave's 16 rows, store them (no block barrier: same-wave LDS order)
 #pragma unroll
-    for (int pt = 0; pt < 4; ++pt) xr[pt] = acc_rows4(Xs, LD64, 16 * w, 16 * pt);
-    __syncthreads();  // every wave is done reading XDs before it becomes the output tile
+    for (int pt = 0; pt < 4; ++pt) {
+      const bf16x4 xr = acc_rows4(Xs, LD64, 16 * w, 16 * pt);
 #pragma unroll
-    for (int pt = 0; pt < 4; ++pt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = 16 * w + 4 * (l >> 4) + r, p = 16 * pt + (l & 15);
-        Os[i * LD64 + p] = f2bf(acc[pt][r] + Dh * (float)xr[pt][r]);
+      for (int r = 0; r < 4; ++r)
+        Os[(16 * w + 4 * lg + r) * LD64 + 16 * pt + li] = f2bf(acc[pt][r] + Dh * (float)xr[r]);
+    }
+    {
+      const int row = 16 * w + (l >> 2), col = 16 * (l & 3);
+      if (row < valid) {
+        bf16_t* yg = a.y + (int64_t)b * a.syb + (int64_t)(c * Q + row) * a.syl + (int64_t)h * a.syh + col;
+        *reinterpret_cast<uint4*>(yg) = *reinterpret_cast<const uint4*>(Os + row * LD64 + col);
+        *reinterpret_cast<uint4*>(yg + 8) = *reinterpret_cast<const uint4*>(Os + row * LD64 + col + 8);
       }
-    __syncthreads();
-    store_tile<Q, 64>(a.y + (int64_t)b * a.syb + (int64_t)c * Q * a.syl + (int64_t)h * a.syh, a.syl, Os, LD64, valid);
+    }
+    // ---- S_{c+1} = e^{cl} S_c + (X o w)^T B
+    const float decay = __expf(cl);
+#pragma unroll
+    for (int nt = 0; nt < NTS; ++nt) st[nt] *= decay;
+#pragma unroll
+    for (int ks = 0; ks < Q / 32; ++ks) {
+      bf16x8 A = frag_tr(Xs, LD64, 32 * ks, 16 * w);  // A[p][k=j], j = 32ks + 8lg + jj
+      const float4 w0 = *reinterpret_cast<const float4*>(&wjr[32 * ks + 8 * lg]);
+      const float4 w1 = *reinterpret_cast<const float4*>(&wjr[32 * ks + 8 * lg + 4]);
+      const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) A[jj] = (__bf16)((float)A[jj] * wv[jj]);
+#pragma unroll
+      for (int nt = 0; nt < NTS; ++nt) st[nt] = mfma16(A, frag_tr(Bs, LDN, 32 * ks, 16 * nt), st[nt]);
+    }
+  }
+  if (a.final_state) {
+#pragma unroll
+    for (int nt = 0; nt < NTS; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        a.final_state[(((int64_t)b * a.H + h) * P + 16 * w + 4 * lg + r) * N + 16 * nt + li] = st[nt][r];
   }
 }
 
@@ -363,7 +353,7 @@ __global__ __launch_bounds__(256) void ssd_dstate_bwd_k(SSDArgs a) {
 // wait for the other; only half 0 accumulates dCB and the G row/col sums.
 template <int N>
 __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
-  constexpr int LDN = N + 8;
+  constexpr int LDN = N + 16;  // conflict-free ds_read_b128 fragments (see LD64)
   constexpr int NT = N / 16;
   constexpr int NTH = NT / 2;
   __shared__ __attribute__((aligned(16))) bf16_t Cs[Q * LDN];
@@ -648,7 +638,7 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
 // ============================== K5: dB / dC (backward) =======================================
 template <int N>
 __global__ __launch_bounds__(256) void ssd_dbc_bwd_k(SSDArgs a) {
-  constexpr int LDN = N + 8;
+  constexpr int LDN = N + 16;  // conflict-free ds_read_b128 fragments (see LD64)
   constexpr int NT = N / 16;
   __shared__ __attribute__((aligned(16))) bf16_t Cs[Q * LDN];
   __shared__ __attribute__((aligned(16))) bf16_t Bs[Q * LDN];
@@ -716,9 +706,7 @@ hipError_t launch_ssd_fwd(const SSDArgs& a, hipStream_t st) {
   const int64_t waves = (int64_t)a.B * a.H * a.nc;
   hipLaunchKernelGGL(ssd_cumsum_k, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, a);
   MAMBA_HIP_CHECK(hipGetLastError());
-  N_SWITCH(a.N, hipLaunchKernelGGL(ssd_state_fwd_k<NN>, dim3(NN / 64, a.H, a.B), dim3(256), 0, st, a));
-  MAMBA_HIP_CHECK(hipGetLastError());
-  N_SWITCH(a.N, hipLaunchKernelGGL(ssd_scan_fwd_k<NN>, dim3(a.nc, a.nhg, a.B), dim3(256), 0, st, a));
+  N_SWITCH(a.N, hipLaunchKernelGGL(ssd_fused_fwd_k<NN>, dim3(a.H, a.B), dim3(256), 0, st, a));
   return hipGetLastError();
 }
 

@@ -73,7 +73,10 @@ class LMHeadModel(MambaLMHeadModel):
 
     @torch.no_grad()
     def generate(self, text: str, top_k: int = 50, max_length: int = 32, seed: int = 42,
-                 use_cache: bool = True) -> str:
+                 use_cache: bool = True, use_graph: Optional[bool] = None) -> str:
+        """Top-k sampling (reference model.py:49-75).  ``use_cache`` (default): O(1) state-cached
+        decode; on a GPU with a pure Mamba stack the per-token step replays a HIP graph
+        (``inference.GraphedDecoder``).  ``use_cache=False``: the reference's full recompute."""
         dev = next(self.parameters()).device
         ids = self.enc.encode(text)
         eot = self.enc.eot_token if hasattr(self.enc, "eot_token") else getattr(self.enc, "eos_token_id", None)
@@ -88,17 +91,16 @@ class LMHeadModel(MambaLMHeadModel):
                 if nxt == eot:
                     break
             return self.enc.decode(xgen[0].tolist())
-        params = InferenceParams(max_seqlen=xgen.shape[1] + max_length, max_batch_size=1)
-        logits = MambaLMHeadModel.forward(self, xgen, inference_params=params, num_last_tokens=1).logits
+        from .inference import GraphedDecoder
+        dec = GraphedDecoder(self, batch_size=1, max_seqlen=xgen.shape[1] + max_length, use_graph=use_graph)
+        logits = dec.prefill(xgen)
         out = list(ids)
         for i in range(max_length):
-            nxt = self.top_k_sampling(logits[0, -1], k=top_k, generator=gen)
+            nxt = self.top_k_sampling(logits[0], k=top_k, generator=gen)
             out.append(nxt)
             if nxt == eot or i == max_length - 1:
                 break
-            params.seqlen_offset += 1 if i else xgen.shape[1]
-            tok = torch.tensor([[nxt]], device=dev)
-            logits = MambaLMHeadModel.forward(self, tok, inference_params=params).logits
+            logits = dec.step(torch.tensor([nxt], device=dev))
         return self.enc.decode(out)
 
     # ------------------------------------------------------------------------------------

@@ -18,11 +18,11 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.conv1d import causal_conv1d_update
+from ..ops.conv1d import causal_conv1d_fn, causal_conv1d_update
 from ..ops.norm import RMSNormGated
-from ..ops.reference import causal_conv1d_ref, ssd_chunked_ref, softplus_inverse
+from ..ops.reference import softplus_inverse
 from ..ops.selective_scan import selective_state_update
-from ..ops.ssd import mamba2_inner_fn
+from ..ops.ssd import mamba2_inner_fn, mamba_chunk_scan_combined
 
 
 class Mamba2(nn.Module):
@@ -108,14 +108,14 @@ class Mamba2(nn.Module):
         xt = xBC.transpose(1, 2)
         w = self.d_conv
         conv_state.copy_(F.pad(xt, (max(0, w - 1 - xt.shape[-1]), 0))[..., -(w - 1):])
-        xBC = causal_conv1d_ref(xt, self.conv1d.weight.reshape(xt.shape[1], -1), self.conv1d.bias,
-                                "silu").transpose(1, 2)
+        xBC = causal_conv1d_fn(xt, self.conv1d.weight, self.conv1d.bias, "silu").transpose(1, 2)
         x, Bm, Cm = torch.split(xBC, [di, gn, gn], dim=-1)
-        y, last = ssd_chunked_ref(x.unflatten(-1, (H, self.headdim)), dt, A,
-                                  Bm.unflatten(-1, (self.ngroups, self.d_state)),
-                                  Cm.unflatten(-1, (self.ngroups, self.d_state)), min(64, self.chunk_size),
-                                  D=self.D, dt_bias=self.dt_bias, dt_softplus=True, dt_limit=self.dt_limit,
-                                  return_final_states=True)
+        y, last = mamba_chunk_scan_combined(x.unflatten(-1, (H, self.headdim)), dt, A,
+                                            Bm.unflatten(-1, (self.ngroups, self.d_state)),
+                                            Cm.unflatten(-1, (self.ngroups, self.d_state)),
+                                            min(64, self.chunk_size), D=self.D, dt_bias=self.dt_bias,
+                                            dt_softplus=True, dt_limit=self.dt_limit, return_final_states=True)
+        y = y.to(zxbcdt.dtype)
         ssm_state.copy_(last)
         return self.norm(y.flatten(-2), z)
 

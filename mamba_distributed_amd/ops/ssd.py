@@ -66,7 +66,9 @@ def mamba_chunk_scan_combined(x, dt, A, B, C, chunk_size=256, D=None, z=None, dt
                               dt_limit=(0.0, _INF), return_final_states=False):
     """x (b,l,h,p), dt (b,l,h), A (h), B/C (b,l,g,n) -> y (b,l,h,p) [, final_states (b,h,p,n)]."""
     assert seq_idx is None, "seq_idx (packed variable-length) is not supported yet"
-    if _ext.use_native(x) and z is None and (D is None or D.dim() == 1):
+    # native kernels are bf16 (the training/serving dtype); fp32 activations (e.g. the reference's
+    # fp32 HellaSwag eval) take the fp32 reference path
+    if x.dtype == torch.bfloat16 and _ext.use_native(x) and z is None and (D is None or D.dim() == 1):
         out = _SSDFn.apply(x, dt, A, B, C, D, dt_bias, initial_states, dt_softplus,
                            float(dt_limit[0]), float(dt_limit[1]), return_final_states)
         return out
@@ -164,7 +166,7 @@ def mamba2_inner_fn(zxbcdt, conv_w, conv_b, dt_bias, A, D, norm_w, eps, headdim,
     """conv1d+SiLU -> SSD -> gated RMSNorm on the in_proj output; returns (b, l, d_inner).
     ``A_is_log``: ``A`` is the A_log parameter; the kernels apply A = -exp(A_log) and return dA_log
     (saves the per-layer exp/neg launches and their backward)."""
-    if _ext.use_native(zxbcdt):
+    if zxbcdt.dtype == torch.bfloat16 and _ext.use_native(zxbcdt):
         return _Mamba2InnerFn.apply(zxbcdt, conv_w, conv_b, dt_bias, A, D, norm_w, eps, headdim,
                                     ngroups, d_state, float(dt_limit[0]), float(dt_limit[1]),
                                     norm_before_gate, A_is_log)

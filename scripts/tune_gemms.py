@@ -21,6 +21,8 @@ def main():
     p.add_argument("--T", type=int, default=1024)
     p.add_argument("--out", default=gemm_tuning.DEFAULT_TABLE)
     p.add_argument("--max-ms", type=int, default=40)
+    p.add_argument("--decode-batch", type=int, nargs="*", default=[],
+                   help="also tune the decode GEMVs (M = batch) of a bf16 model")
     a = p.parse_args()
     if os.path.exists(a.out):
         torch.cuda.tunable.read_file(a.out)  # keep earlier shapes
@@ -35,6 +37,16 @@ def main():
             loss.backward()
             torch.cuda.synchronize()
             print(f"{name} fused_ce={fused}: {len(torch.cuda.tunable.get_results())} tuned GEMMs", flush=True)
+        if a.decode_batch:
+            from mamba_distributed_amd.inference import GraphedDecoder
+            mb = model.to(torch.bfloat16).eval()
+            for bs in a.decode_batch:
+                dec = GraphedDecoder(mb, batch_size=bs, max_seqlen=64, use_graph=False)
+                logits = dec.prefill(torch.randint(0, cfg.vocab_size, (bs, 16), device="cuda"))
+                for _ in range(2):
+                    logits = dec.step(logits.argmax(-1))
+                torch.cuda.synchronize()
+                print(f"{name} decode batch {bs}: {len(torch.cuda.tunable.get_results())} tuned GEMMs", flush=True)
         del model
         torch.cuda.empty_cache()
     n = gemm_tuning.flush(a.out)

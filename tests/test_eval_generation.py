@@ -2,6 +2,7 @@
 import json
 import os
 
+import pytest
 import torch
 
 from mamba_distributed_amd import LMHeadModel, MambaConfig, preset
@@ -84,3 +85,26 @@ def test_generate_api():
     b = m.generate("Hi", max_length=6, seed=3)
     c = m.generate("Hi", max_length=6, seed=3, use_cache=False)
     assert a == b == c  # seeded + cached decode == recompute
+
+
+@pytest.mark.parametrize("layer", ["Mamba1", "Mamba2"])
+def test_decoder_cached_steps_match_full_recompute(layer):
+    """inference.GraphedDecoder (eager on CPU): prefill + per-token steps give the same logits as
+    re-running the whole prefix (the reference's generate)."""
+    from mamba_distributed_amd import LMHeadModel, MambaConfig
+    from mamba_distributed_amd.inference import GraphedDecoder
+    torch.manual_seed(0)
+    cfg = MambaConfig(d_model=64, n_layer=2, vocab_size=256, ssm_cfg={"layer": layer, **(
+        {"headdim": 16, "d_state": 16, "chunk_size": 16} if layer == "Mamba2" else {})})
+    m = LMHeadModel(cfg, device="cpu").eval()
+    ids = torch.randint(0, 256, (2, 11))
+    dec = GraphedDecoder(m, batch_size=2, max_seqlen=32, use_graph=False)
+    logits = dec.prefill(ids[:, :7])
+    with torch.no_grad():
+        full = m(ids[:, :7])[0][:, -1]
+    torch.testing.assert_close(logits, full, rtol=1e-4, atol=1e-4)
+    for t in range(7, 11):
+        logits = dec.step(ids[:, t])
+        with torch.no_grad():
+            full = m(ids[:, :t + 1])[0][:, -1]
+        torch.testing.assert_close(logits, full, rtol=1e-4, atol=1e-4)
