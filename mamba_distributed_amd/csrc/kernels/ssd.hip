@@ -278,69 +278,71 @@ __global__ __launch_bounds__(256) void ssd_fused_fwd_k(SSDArgs a) {
 }
 
 // ============================== K3: reverse state pass (backward) ===========================
+// WG per (h, b) walks the chunks from the last: dS_out(c) -> HBM (bf16), then
+// dS = e^{cum_last} dS + (e^{cum} dY)^T C.  All N columns per workgroup, so each dY tile is read once.
 template <int N>
 __global__ __launch_bounds__(256) void ssd_dstate_bwd_k(SSDArgs a) {
+  constexpr int LDN = N + 16;
+  constexpr int NTS = N / 16;
   __shared__ __attribute__((aligned(16))) bf16_t Ys[Q * LD64];
-  __shared__ __attribute__((aligned(16))) bf16_t Cs[Q * LD64];
-  __shared__ __attribute__((aligned(16))) bf16_t Os[P * LD64];
+  __shared__ __attribute__((aligned(16))) bf16_t Cs[Q * LDN];
+  __shared__ __attribute__((aligned(16))) bf16_t Os[P * LDN];
   __shared__ float er[Q];
-  const int ns = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int h = blockIdx.x, b = blockIdx.y;
   const int g = h / (a.H / a.G);
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const float* cumbh = a.cum + ((int64_t)b * a.H + h) * a.Lp;
   const bf16_t* yg = a.dy + (int64_t)b * a.sdyb + (int64_t)h * a.sdyh;
-  const bf16_t* cg = a.Cm + (int64_t)b * a.sCb + (int64_t)g * a.sCg + ns * 64;
-  f32x4 acc[4];
+  const bf16_t* cg = a.Cm + (int64_t)b * a.sCb + (int64_t)g * a.sCg;
+  f32x4 acc[NTS];
 #pragma unroll
-  for (int nt = 0; nt < 4; ++nt) {
+  for (int nt = 0; nt < NTS; ++nt) {
     acc[nt] = zero4();
     if (a.dfinal) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int p = 16 * w + 4 * (l >> 4) + r, n = ns * 64 + 16 * nt + (l & 15);
+        const int p = 16 * w + 4 * (l >> 4) + r, n = 16 * nt + (l & 15);
         acc[nt][r] = a.dfinal[(((int64_t)b * a.H + h) * P + p) * N + n];
       }
     }
   }
-  Tile64<256> py, pcs;
+  Tile64<256> py;
+  TileState<256, N> pcs;
   float pe = 0.f;
-  {
-    const int c = a.nc - 1, valid = min(Q, a.L - c * Q);
+  auto prefetch = [&](int c) {
+    const int valid = min(Q, a.L - c * Q);
     py.load(yg + (int64_t)c * Q * a.sdyl, a.sdyl, valid);
-    pcs.load(cg + (int64_t)c * Q * a.sCl, a.sCl, valid);
+#pragma unroll
+    for (int i = 0; i < N / 64; ++i) pcs.t[i].load(cg + (int64_t)c * Q * a.sCl + 64 * i, a.sCl, valid);
     if (threadIdx.x < Q) pe = __expf(cumbh[c * Q + threadIdx.x]);
-  }
+  };
+  prefetch(a.nc - 1);
   for (int c = a.nc - 1; c >= 0; --c) {
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) acc_to_lds(Os, LD64, 16 * w, 16 * nt, acc[nt]);
+    for (int nt = 0; nt < NTS; ++nt) acc_to_lds(Os, LDN, 16 * w, 16 * nt, acc[nt]);
     if (threadIdx.x < Q) er[threadIdx.x] = pe;
     const float decay = __expf(cumbh[c * Q + Q - 1]);
     __syncthreads();
-    store_tile<P, 64>(a.dstates + ((((int64_t)b * a.nc + c) * a.H + h) * P) * N + ns * 64, N, Os, LD64, P);
+    store_tile<P, N>(a.dstates + ((((int64_t)b * a.nc + c) * a.H + h) * P) * N, N, Os, LDN, P);
     py.store(Ys, LD64, er);
-    pcs.store(Cs, LD64);
-    if (c > 0) {
-      const int cn = c - 1, valid = min(Q, a.L - cn * Q);
-      py.load(yg + (int64_t)cn * Q * a.sdyl, a.sdyl, valid);
-      pcs.load(cg + (int64_t)cn * Q * a.sCl, a.sCl, valid);
-      if (threadIdx.x < Q) pe = __expf(cumbh[cn * Q + threadIdx.x]);
-    }
+    pcs.store(Cs, LDN);
+    if (c > 0) prefetch(c - 1);
     __syncthreads();
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) acc[nt] *= decay;
+    for (int nt = 0; nt < NTS; ++nt) acc[nt] *= decay;
 #pragma unroll
     for (int ks = 0; ks < Q / 32; ++ks) {
       const bf16x8 A = frag_tr(Ys, LD64, 32 * ks, 16 * w);
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) acc[nt] = mfma16(A, frag_tr(Cs, LD64, 32 * ks, 16 * nt), acc[nt]);
+      for (int nt = 0; nt < NTS; ++nt) acc[nt] = mfma16(A, frag_tr(Cs, LDN, 32 * ks, 16 * nt), acc[nt]);
     }
   }
   if (a.dinit) {
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
+    for (int nt = 0; nt < NTS; ++nt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int p = 16 * w + 4 * (l >> 4) + r, n = ns * 64 + 16 * nt + (l & 15);
+        const int p = 16 * w + 4 * (l >> 4) + r, n = 16 * nt + (l & 15);
         a.dinit[(((int64_t)b * a.H + h) * P + p) * N + n] = acc[nt][r];
       }
   }
@@ -417,14 +419,58 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
     dBa[nt] = zero4();
     dCa[nt] = zero4();
   }
+  // ---- (10) dt gradients for a batch of up to 8 heads, one wave per head (lane = local step);
+  // the per-head slots form a ring of 8 so any head-group size fits in LDS
+  auto flush = [&](int first, int cnt) {
+    __syncthreads();  // every wave's slot contributions for these heads are written
+    if (wid < cnt) {
+      const int hh = first + wid, h = h0 + hh, sl = hh & 7;
+      const float Ah = a.a_log ? -__expf(a.A[h]) : a.A[h];
+      float da = 0.f;
+#pragma unroll
+      for (int v = 0; v < 8; ++v) da += dcw[sl][v][l];
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {  // reverse inclusive scan: da_i = sum_{t>=i} dcum_t
+        const float y = __shfl_down(da, off, 64);
+        if (l + off < 64) da += y;
+      }
+      const float ddt = (ddw[sl][0][l] + ddw[sl][1][l]) + da * Ah;
+      const float dAp = wave_sum(da * dtr[sl][l]);
+      const int t = c * Q + l;
+      float gdt = 0.f;
+      if (t < a.L) {
+        float raw = rawl[sl][l];
+        if (a.dt_bias) raw += a.dt_bias[h];
+        const float v = a.softplus ? softplusf_(raw) : raw;
+        const bool inside = (v >= a.dt_min) && (v <= a.dt_max);
+        gdt = inside ? ddt * (a.softplus ? sigmoidf_(raw) : 1.f) : 0.f;
+        st_any(a.ddt, a.ddt_dtype, (int64_t)b * a.sddtb + (int64_t)t * a.sddtl + (int64_t)h * a.sddth, gdt);
+      }
+      const float dbp = wave_sum(gdt);
+      if (l == 0) {
+        const int64_t pi = ((int64_t)b * a.nc + c) * a.psl + h;
+        a.part_dA[pi] = a.a_log ? dAp * Ah : dAp;  // d/dA_log = dA * A
+        a.part_dbias[pi] = dbp;
+        float dd = 0.f;
+#pragma unroll
+        for (int v = 0; v < 8; ++v) dd += redw[sl][v];
+        a.part_dD[pi] = dd;
+      }
+      // recycle this head's slots for head hh + 8 (the next head's top barrier orders it)
+#pragma unroll
+      for (int v = 0; v < 8; ++v) dcw[sl][v][l] = 0.f;
+      ddw[sl][0][l] = 0.f;
+      ddw[sl][1][l] = 0.f;
+    }
+  };
   const int jl = 16 * w + li;  // this lane's column index in the M / dM tiles
   for (int hh = 0; hh < a.HG; ++hh) {
     const int h = h0 + hh;
     __syncthreads();  // previous head fully consumed (LDS tiles, dcum, Os)
     if (threadIdx.x < Q) {
       cumr[threadIdx.x] = pc;
-      dtr[hh][threadIdx.x] = pd;
-      rawl[hh][threadIdx.x] = praw;
+      dtr[hh & 7][threadIdx.x] = pd;
+      rawl[hh & 7][threadIdx.x] = praw;
     }
     px.store(Xs, LD64);
     py.store(dYs, LD64);
@@ -435,7 +481,7 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
     const float cl = cumr[Q - 1];
     const float Ah = a.a_log ? -__expf(a.A[h]) : a.A[h];
     const float Dh = a.D ? a.D[h] : 0.f;
-    const float dtj = dtr[hh][jl], cumj = cumr[jl];
+    const float dtj = dtr[hh & 7][jl], cumj = cumr[jl];
     // ---- (1)(2) dM, M; half 0: dCB and the G row/col sums
     f32x4 m[4];
     float colG = 0.f;
@@ -463,14 +509,14 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float rs = row_sum16(gr[r]);
-            if (li == 0) dcw[hh][wid][16 * I + 4 * lg + r] += rs;
+            if (li == 0) dcw[hh & 7][wid][16 * I + 4 * lg + r] += rs;
           }
         }
       }
     }
     if (half == 0) {
       colG = rows_sum4(colG);
-      if (l < 16) dcw[hh][wid][jl] -= colG;
+      if (l < 16) dcw[hh & 7][wid][jl] -= colG;
     }
     // ---- (3) dXdt = M^T dY, (4) BdS = B dS^T, (6) Yoff = C S^T  for this half's p-tiles
     f32x4 dxd[2], bds[2], yo[2];
@@ -510,7 +556,7 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int j = 16 * w + 4 * lg + r;
-      const float dt_ = dtr[hh][j];
+      const float dt_ = dtr[hh & 7][j];
       const float ej = __expf(cl - cumr[j]);
       const float wj = ej * dt_;
       const float ei = __expf(cumr[j]);
@@ -530,19 +576,19 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
       up = row_sum16(up) * wj;
       yp = row_sum16(yp) * ei;
       if (li == 0) {
-        ddw[hh][half][j] += ddp;
-        dcw[hh][wid][j] += yp - up;
+        ddw[hh & 7][half][j] += ddp;
+        dcw[hh & 7][wid][j] += yp - up;
       }
       usum += up;
     }
     usum = rows_sum4(usum);  // the wave's U total over its 16 rows (x its p-half)
-    if (l == 0) dcw[hh][wid][Q - 1] += usum;
+    if (l == 0) dcw[hh & 7][wid][Q - 1] += usum;
     dDp = wave_sum(dDp);
-    if (l == 0) redw[hh][wid] = dDp;
+    if (l == 0) redw[hh & 7][wid] = dDp;
     // ---- (7) dC_off += (e^{cum_i} dY) S , (8) dB_off += (w_j x) dS   for this half's n-tiles
     {
       const float ei = __expf(cumr[jl]);
-      const float wl = __expf(cl - cumr[jl]) * dtr[hh][jl];
+      const float wl = __expf(cl - cumr[jl]) * dtr[hh & 7][jl];
 #pragma unroll
       for (int ks = 0; ks < P / 32; ++ks) {
         const bf16x8 Ay = scale_frag(frag_kc(dYs, LD64, 16 * w, 32 * ks), ei);
@@ -567,7 +613,7 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
         for (int k = 0; k < 8; ++k) s += fa[k] * fb[k];
       }
       s = wave_sum(s);
-      if (l == 0) dcw[hh][wid][Q - 1] += s * __expf(cl);
+      if (l == 0) dcw[hh & 7][wid][Q - 1] += s * __expf(cl);
     }
     // dX: each wave stores the 16x32 sub-tile of Os it wrote itself (same-wave LDS ops are in order,
     // so no block barrier is needed)
@@ -577,42 +623,7 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
         *reinterpret_cast<uint4*>(a.dx + (int64_t)b * a.sdxb + (int64_t)(c * Q + row) * a.sdxl +
                                   (int64_t)h * a.sdxh + col) = *reinterpret_cast<const uint4*>(Os + row * LD64 + col);
     }
-  }
-  __syncthreads();
-  // ---- (10) dt gradients, one wave per head of the group (lane = local step)
-  if (wid < a.HG) {
-    const int hh = wid, h = h0 + wid;
-    const float Ah = a.a_log ? -__expf(a.A[h]) : a.A[h];
-    float da = 0.f;
-#pragma unroll
-    for (int v = 0; v < 8; ++v) da += dcw[hh][v][l];
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {  // reverse inclusive scan: da_i = sum_{t>=i} dcum_t
-      const float y = __shfl_down(da, off, 64);
-      if (l + off < 64) da += y;
-    }
-    const float ddt = (ddw[hh][0][l] + ddw[hh][1][l]) + da * Ah;
-    const float dAp = wave_sum(da * dtr[hh][l]);
-    const int t = c * Q + l;
-    float gdt = 0.f;
-    if (t < a.L) {
-      float raw = rawl[hh][l];
-      if (a.dt_bias) raw += a.dt_bias[h];
-      const float v = a.softplus ? softplusf_(raw) : raw;
-      const bool inside = (v >= a.dt_min) && (v <= a.dt_max);
-      gdt = inside ? ddt * (a.softplus ? sigmoidf_(raw) : 1.f) : 0.f;
-      st_any(a.ddt, a.ddt_dtype, (int64_t)b * a.sddtb + (int64_t)t * a.sddtl + (int64_t)h * a.sddth, gdt);
-    }
-    const float dbp = wave_sum(gdt);
-    if (l == 0) {
-      const int64_t pi = ((int64_t)b * a.nc + c) * a.psl + h;
-      a.part_dA[pi] = a.a_log ? dAp * Ah : dAp;  // d/dA_log = dA * A
-      a.part_dbias[pi] = dbp;
-      float dd = 0.f;
-#pragma unroll
-      for (int v = 0; v < 8; ++v) dd += redw[hh][v];
-      a.part_dD[pi] = dd;
-    }
+    if ((hh & 7) == 7 || hh == a.HG - 1) flush(hh & ~7, (hh & 7) + 1);
   }
   // ---- head-group partials
   const int64_t pbase = ((int64_t)b * a.nc + c) * a.nhg + hgi;
@@ -711,7 +722,7 @@ hipError_t launch_ssd_fwd(const SSDArgs& a, hipStream_t st) {
 }
 
 hipError_t launch_ssd_bwd(const SSDArgs& a, hipStream_t st) {
-  N_SWITCH(a.N, hipLaunchKernelGGL(ssd_dstate_bwd_k<NN>, dim3(NN / 64, a.H, a.B), dim3(256), 0, st, a));
+  N_SWITCH(a.N, hipLaunchKernelGGL(ssd_dstate_bwd_k<NN>, dim3(a.H, a.B), dim3(256), 0, st, a));
   MAMBA_HIP_CHECK(hipGetLastError());
   N_SWITCH(a.N, hipLaunchKernelGGL(ssd_chunk_bwd_k<NN>, dim3(a.nc, a.nhg, a.B), dim3(512), 0, st, a));
   MAMBA_HIP_CHECK(hipGetLastError());

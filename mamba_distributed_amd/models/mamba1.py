@@ -24,9 +24,9 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import _ext
-from ..ops.conv1d import causal_conv1d_update
+from ..ops.conv1d import causal_conv1d_fn, causal_conv1d_update
 from ..ops.reference import causal_conv1d_ref, selective_scan_ref, softplus_inverse
-from ..ops.selective_scan import selective_state_update
+from ..ops.selective_scan import selective_scan_fn, selective_state_update
 
 
 def _cm(t2d: torch.Tensor, b: int, l: int) -> torch.Tensor:
@@ -178,7 +178,7 @@ class Mamba(nn.Module):
         if conv_state is not None:  # prefill: remember the last d_conv-1 inputs for decoding
             x = xz3[:, :self.d_inner]
             conv_state.copy_(F.pad(x, (max(0, self.d_conv - 1 - l), 0))[..., -(self.d_conv - 1):])
-            y, last = self._inner_ref_with_state(xz3, A)
+            y, last = self._inner_with_state(xz3, A)
             ssm_state.copy_(last)
         else:
             y = mamba1_inner_ref(xz3, self.conv1d.weight, self.conv1d.bias, self.x_proj.weight,
@@ -187,16 +187,18 @@ class Mamba(nn.Module):
                        None if self.out_proj.bias is None else self.out_proj.bias.to(cd))
         return out
 
-    def _inner_ref_with_state(self, xz3, A):
+    def _inner_with_state(self, xz3, A):
+        """Prompt pass that also returns the final SSM state (cache fill for decoding): native
+        conv + scan kernels on a GPU (the scan returns its last state), oracles on the CPU."""
         di = self.d_inner
         R, N = self.dt_rank, self.d_state
         x, z = xz3[:, :di], xz3[:, di:]
-        conv_out = causal_conv1d_ref(x, self.conv1d.weight.reshape(di, -1), self.conv1d.bias, "silu")
+        conv_out = causal_conv1d_fn(x, self.conv1d.weight.reshape(di, -1), self.conv1d.bias, "silu")
         x_dbl = torch.einsum("rd,bdl->brl", self.x_proj.weight.to(conv_out.dtype), conv_out)
         delta = torch.einsum("dr,brl->bdl", self.dt_proj.weight.to(x_dbl.dtype), x_dbl[:, :R])
-        return selective_scan_ref(conv_out, delta, A, x_dbl[:, R:R + N].unsqueeze(1),
-                                  x_dbl[:, R + N:].unsqueeze(1), self.D.float(), z,
-                                  self.dt_proj.bias.float(), True, return_last_state=True)
+        return selective_scan_fn(conv_out, delta, A, x_dbl[:, R:R + N].unsqueeze(1),
+                                 x_dbl[:, R + N:].unsqueeze(1), self.D.float(), z,
+                                 self.dt_proj.bias.float(), True, return_last_state=True)
 
     @torch.no_grad()
     def step(self, hidden_states, conv_state, ssm_state):

@@ -3,14 +3,16 @@
 Call surface mirrors upstream ``selective_scan_fn`` / ``mamba_inner_fn`` (SURVEY.md D9, D10,
 K1/K2) that the reference reaches through ``Mamba.forward`` (reference model.py:8).
 
-GPU (csrc/kernels/selective_scan.hip): one wavefront per (batch, channel).  The sequence is cut
-into 64-lane x ITEMS time tiles: each lane composes its ITEMS consecutive steps into one affine map
-(a, b) per state, a wave64 prefix scan (DPP row ops + ``permlane32``-free shuffles) combines the 64
-lane maps, and the carry (the state at the tile boundary) stays in registers across tiles.  All
-16 states are processed in registers; B/C tiles are staged once per tile and broadcast from LDS.
-Backward runs the same structure in reverse time (adjoint scan) and recomputes the forward states
-tile by tile from the saved per-tile carries; dB/dC are reduced across the channels of a group with
-a deterministic two-pass reduction (no float atomics).
+GPU (csrc/kernels/selective_scan.hip):
+  * forward: one wavefront per (batch, channel) row, lanes over time (16 steps per lane), all N
+    states per wave; per state each lane composes its steps into one affine map, a DPP prefix
+    scan (row_shr / row_bcast) combines the 64 lane maps, and the state at each backward-tile
+    boundary is saved ("carries") for the backward.
+  * backward: a workgroup owns 64 channels of one batch row and walks 256-step tiles from the
+    end; its 4 waves split the states, replay the forward from the saved carries and run the
+    adjoint as a DPP suffix scan.  B/C tiles are staged once in LDS for all channels, the next
+    channel's rows are prefetched, and dB/dC are summed over the channels in registers (fixed-order,
+    no float atomics).
 """
 from __future__ import annotations
 

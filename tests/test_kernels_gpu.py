@@ -159,6 +159,23 @@ def test_ssd_fwd_bwd(cuda, b, L, H, G, N):
         assert rel(a, b_) < 3e-2, (nm, rel(a, b_))
 
 
+@pytest.mark.parametrize("hg", ["24", "12", "3"])
+def test_ssd_head_groups(cuda, monkeypatch, hg):
+    """chunk-bwd head groups larger than the 8-slot dt-gradient ring (flushed every 8 heads) and
+    odd sizes; forced through the MAMBA_AMD_SSD_HG override, checked against the reference."""
+    from mamba_distributed_amd.ops.ssd import mamba_chunk_scan_combined
+    monkeypatch.setenv("MAMBA_AMD_SSD_HG", hg)
+    x, dt, A, Bm, Cm, D, dt_bias = _ssd_inputs(cuda, 2, 200, 24, 1, 128, seed=11)
+
+    def f(x, dt, A, Bm, Cm, D, dt_bias):
+        return mamba_chunk_scan_combined(x, dt, A, Bm, Cm, 64, D=D, dt_bias=dt_bias, dt_softplus=True)
+
+    on, orf, gn, gr = run_both(f, f, [x, dt, A, Bm, Cm, D, dt_bias])
+    assert rel(on, orf) < 2e-2, rel(on, orf)
+    for nm, a, b_ in zip(["x", "dt", "A", "B", "C", "D", "dt_bias"], gn, gr):
+        assert rel(a, b_) < 3e-2, (hg, nm, rel(a, b_))
+
+
 def test_ssd_initial_and_final_states(cuda):
     from mamba_distributed_amd.ops.ssd import mamba_chunk_scan_combined
     x, dt, A, Bm, Cm, D, dt_bias = _ssd_inputs(cuda, 2, 192, 4, 1, 128, seed=5)
