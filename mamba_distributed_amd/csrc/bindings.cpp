@@ -557,6 +557,48 @@ Tensor ssm_state_update(Tensor state, Tensor x, Tensor dt, Tensor A, Tensor Bm, 
   return out;
 }
 
+// C = A . B^T for bf16 K-contiguous operands (the projection forward); out optional (may be a
+// row-strided view, e.g. a column slice of a wider buffer)
+Tensor gemm_tn(Tensor A, Tensor B, optional<Tensor> out) {
+  check_cuda(A, "A");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(A.device());
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "gemm_tn: A (M,K), B (N,K)");
+  TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "gemm_tn: bf16 operands");
+  TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1, "gemm_tn: K-contiguous operands");
+  const int64_t M = A.size(0), N = B.size(0), K = A.size(1);
+  Tensor C = out.has_value() && out->defined() ? *out : at::empty({M, N}, A.options());
+  TORCH_CHECK(C.dim() == 2 && C.size(0) == M && C.size(1) == N && C.stride(1) == 1 && C.scalar_type() == at::kBFloat16,
+              "gemm_tn: out (M,N) bf16 with unit column stride");
+  TORCH_CHECK((uintptr_t)A.data_ptr() % 16 == 0 && (uintptr_t)B.data_ptr() % 16 == 0 && (uintptr_t)C.data_ptr() % 16 == 0,
+              "gemm_tn: 16-B aligned operands");
+  TORCH_CHECK(mamba_amd::gemm_tn_supported((int)M, (int)N, (int)K, A.stride(0), B.stride(0), C.stride(0)),
+              "gemm_tn: needs K % 64 == 0, N % 8 == 0, row strides % 8 == 0");
+  HIPCHK(mamba_amd::launch_gemm_tn_bf16(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0),
+                                        (int)M, (int)N, (int)K, cur_stream()));
+  return C;
+}
+
+// dW (fp32, (P, Q)) = dY^T X for token-major bf16 dY (M, P), X (M, Q); out optional (accumulate=True
+// adds into it, e.g. an existing fp32 .grad)
+Tensor gemm_wgrad(Tensor dY, Tensor X, optional<Tensor> out, bool accumulate) {
+  check_cuda(dY, "dY");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(dY.device());
+  TORCH_CHECK(dY.dim() == 2 && X.dim() == 2 && dY.size(0) == X.size(0), "gemm_wgrad: dY (M,P), X (M,Q)");
+  TORCH_CHECK(dY.scalar_type() == at::kBFloat16 && X.scalar_type() == at::kBFloat16, "gemm_wgrad: bf16 operands");
+  TORCH_CHECK(dY.stride(1) == 1 && X.stride(1) == 1, "gemm_wgrad: unit column stride");
+  TORCH_CHECK((uintptr_t)dY.data_ptr() % 16 == 0 && (uintptr_t)X.data_ptr() % 16 == 0, "gemm_wgrad: 16-B aligned");
+  const int64_t M = dY.size(0), P = dY.size(1), Q = X.size(1);
+  Tensor C = out.has_value() && out->defined() ? *out : at::empty({P, Q}, dY.options().dtype(at::kFloat));
+  TORCH_CHECK(C.scalar_type() == at::kFloat && C.is_contiguous() && C.size(0) == P && C.size(1) == Q,
+              "gemm_wgrad: out must be contiguous fp32 (P,Q)");
+  TORCH_CHECK(!accumulate || (out.has_value() && out->defined()), "gemm_wgrad: accumulate needs out");
+  const int S = mamba_amd::gemm_wgrad_splits((int)M, (int)P, (int)Q);
+  auto part = at::empty({S, P, Q}, dY.options().dtype(at::kFloat));
+  HIPCHK(mamba_amd::launch_gemm_wgrad(dY.data_ptr(), dY.stride(0), X.data_ptr(), X.stride(0), part.data_ptr<float>(),
+                                      C.data_ptr<float>(), (int)M, (int)P, (int)Q, accumulate, cur_stream()));
+  return C;
+}
+
 }  // namespace
 
 TORCH_LIBRARY(mamba_amd, m) {
@@ -589,12 +631,16 @@ TORCH_LIBRARY(mamba_amd, m) {
   m.def("selscan_bwd_into(Tensor dout, Tensor u, Tensor delta, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? z, "
         "Tensor? delta_bias, Tensor carries, bool softplus, Tensor(a!) dz_out, Tensor(b!) dB_out, Tensor(c!) dC_out) "
         "-> Tensor[]");
+  m.def("gemm_tn(Tensor A, Tensor B, Tensor(a!)? out=None) -> Tensor");
+  m.def("gemm_wgrad(Tensor dY, Tensor X, Tensor(a!)? out=None, bool accumulate=False) -> Tensor");
   m.def("ssm_state_update(Tensor(a!) state, Tensor x, Tensor dt, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? z, "
         "Tensor? dt_bias, bool softplus) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(mamba_amd, CUDA, m) {
   m.impl("add_rmsnorm_fwd", &add_rmsnorm_fwd);
+  m.impl("gemm_tn", &gemm_tn);
+  m.impl("gemm_wgrad", &gemm_wgrad);
   m.impl("add_rmsnorm_bwd", &add_rmsnorm_bwd);
   m.impl("gated_rmsnorm_fwd", &gated_rmsnorm_fwd);
   m.impl("gated_rmsnorm_bwd", &gated_rmsnorm_bwd);

@@ -113,7 +113,10 @@ def main(argv=None):
     p.add_argument("--debug", action="store_true")
     p.add_argument("--verbose", action="store_true")
     a = p.parse_args(argv)
-    build(a.jobs, a.force, a.debug, a.verbose)
+    out = build(a.jobs, a.force, a.debug, a.verbose)
+    # link-time check: the extension must resolve all its symbols against torch (loads on CPU too)
+    import torch
+    torch.ops.load_library(out)
 
 
 if __name__ == "__main__":

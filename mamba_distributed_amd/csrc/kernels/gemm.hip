@@ -1,0 +1,406 @@
+// bf16 GEMM for the forward projections: C[M, N] = A[M, K] . B[N, K]^T  (fp32 accumulate, bf16 out).
+//
+// Both operands are K-contiguous row-major (activations x[M, K], weights W[N, K] as nn.Linear stores
+// them), which is the in_proj / out_proj forward of every Mamba block.  On the
+// 280M shapes (M = 32768, K = 768 / 1536, N = 3352 / 768) the library picks 256-wide tiles that
+// leave a 1.5-wave tail (N = 768) or a mostly empty last column tile (N = 3352).
+//
+// Structure (cdna_hip_programming.md §5 "step-3" GEMM, MI355X_MICROARCH.md LDS rules):
+//  * 128 x 128 output tile per 256-thread workgroup, 4 waves as 2 x 2, each wave 64 x 64 =
+//    4 x 4 v_mfma_f32_16x16x32_bf16 accumulators; BK = 64.
+//  * global -> LDS with global_load_lds_dwordx4 (no VGPR staging), double-buffered: tile k+1 is
+//    in flight while tile k is consumed; one vmcnt(0) + barrier per K-step.
+//  * the LDS image is lane-linear (the DMA writes base + lane*16), so the bank-conflict XOR swizzle
+//    (16-B chunk c of row r stored at chunk c ^ (r & 7)) is applied to the per-lane SOURCE address
+//    and undone on the ds_read_b128 fragment read (both sides of the same involution).
+//  * XCD-aware bijective workgroup remap: consecutive output tiles (same A row-panel) share an L2.
+//  * epilogue staged through LDS so every global store is a full 16-B vector; columns >= N masked
+//    (N % 8 == 0), B rows >= N are clamped on load (their results are never stored).
+#include "mfma.h"
+#include "launchers.h"
+#include <algorithm>
+
+namespace mamba_amd {
+
+namespace {
+constexpr int GBM = 128, GBN = 128, GBK = 64;
+constexpr int GTILE_BYTES = GBM * GBK * 2;  // one operand tile: 16 KB
+constexpr int GLDC = GBN + 8;               // padded epilogue row (elements)
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+// 16-B chunk (row r, chunk c) of a [128][64] bf16 tile lives at byte r*128 + ((c ^ (r & 7)) << 4)
+__device__ __forceinline__ int swz(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
+
+// issue the DMA of one [128 x 64] tile: 1024 chunks, 4 per thread; LDS slot q holds the source
+// chunk that the swizzle maps there
+__device__ __forceinline__ void load_tile(const bf16_t* g, int64_t ld, int row0, int rows_valid, int k0,
+                                          char* lds) {
+  const int tid = threadIdx.x, w = tid >> 6;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int q = i * 256 + tid;           // LDS chunk slot written by this lane
+    const int r = q >> 3, cs = q & 7;      // slot row / chunk
+    const int c = cs ^ (r & 7);            // logical k-chunk stored in that slot
+    const int rr = min(r, rows_valid - 1);  // clamp (tail rows are never stored)
+    const bf16_t* src = g + (int64_t)(row0 + rr) * ld + k0 + c * 8;
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds + (i * 256 + w * 64) * 16), 16, 0, 0);
+  }
+}
+
+// k-contiguous MFMA operand (STD order) from a swizzled tile: rows r0 + (l & 15), k = 32 ks + 8 (l >> 4)
+__device__ __forceinline__ bf16x8 frag(const char* lds, int r0, int ks) {
+  const int l = threadIdx.x & 63, r = r0 + (l & 15), c = 4 * ks + (l >> 4);
+  return *reinterpret_cast<const bf16x8*>(lds + swz(r, c));
+}
+}  // namespace
+
+__global__ __launch_bounds__(256) void gemm_tn_bf16_k(const bf16_t* __restrict__ A, int64_t lda,
+                                                      const bf16_t* __restrict__ B, int64_t ldb,
+                                                      bf16_t* __restrict__ C, int64_t ldc, int M, int N, int K) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * GTILE_BYTES];  // [buf][A|B]; epilogue reuses it
+  const int tiles_n = (N + GBN - 1) / GBN;
+  const int nwg = ((M + GBM - 1) / GBM) * tiles_n;
+  const int t = xcd_remap(blockIdx.x, nwg);
+  const int m0 = (t / tiles_n) * GBM, n0 = (t % tiles_n) * GBN;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int wm = w >> 1, wn = w & 1;
+  const int mvalid = min(GBM, M - m0), nvalid = min(GBN, N - n0);
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = zero4();
+  const int KT = K / GBK;
+  load_tile(A, lda, m0, mvalid, 0, smem);
+  load_tile(B, ldb, n0, nvalid, 0, smem + GTILE_BYTES);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < KT; ++kt) {
+    char* cur = smem + (kt & 1) * 2 * GTILE_BYTES;
+    if (kt + 1 < KT) {  // the other buffer was released by the previous iteration's barrier
+      char* nxt = smem + ((kt + 1) & 1) * 2 * GTILE_BYTES;
+      load_tile(A, lda, m0, mvalid, (kt + 1) * GBK, nxt);
+      load_tile(B, ldb, n0, nvalid, (kt + 1) * GBK, nxt + GTILE_BYTES);
+    }
+#pragma unroll
+    for (int ks = 0; ks < GBK / 32; ++ks) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = frag(cur, wm * 64 + 16 * i, ks);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = frag(cur + GTILE_BYTES, wn * 64 + 16 * j, ks);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  // epilogue: acc -> bf16 LDS tile [128][GLDC] -> 16-B row stores
+  bf16_t* Cs = reinterpret_cast<bf16_t*>(smem);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Cs[(wm * 64 + 16 * i + 4 * (l >> 4) + r) * GLDC + wn * 64 + 16 * j + (l & 15)] = f2bf(acc[i][j][r]);
+  __syncthreads();
+  for (int v = threadIdx.x; v < GBM * (GBN / 8); v += 256) {
+    const int r = v / (GBN / 8), c = (v % (GBN / 8)) * 8;
+    if (r < mvalid && c < nvalid)
+      *reinterpret_cast<uint4*>(C + (int64_t)(m0 + r) * ldc + n0 + c) = *reinterpret_cast<const uint4*>(Cs + r * GLDC + c);
+  }
+}
+
+// ================================ weight gradient ==============================================
+// C[P, Q] (fp32) = dY[M, P]^T . X[M, Q]: the nn.Linear weight gradient (dW = dY^T X), reduced over the
+// M = batch*seqlen tokens.  The output is small (768 x 1536 = 72 tiles of 128^2), so M is split into
+// S slices (S * tiles ~ 2-3 workgroups per CU); each workgroup writes an fp32 partial and a
+// second kernel sums the S partials in a fixed order (deterministic), writing fp32 directly (the
+// parameter's gradient dtype: no bf16 round trip, no cast kernel).
+// Both operands are token-major, i.e. the contraction index runs down the rows of the staged tiles,
+// so the MFMA operands come through ds_read_b64_tr_b16 (frag_tr): A[p][k=m] from the dY tile and
+// B[k=m][q] from the X tile.  Tiles are register-staged (global -> VGPR -> padded LDS) and double
+// buffered: tile k+1 is loaded while tile k is multiplied, one barrier per k-step.
+namespace {
+constexpr int WB = 128;       // output tile (P x Q)
+constexpr int WK = 64;        // token rows per k-step
+constexpr int WLD = WB + 8;   // padded LDS row (elements)
+
+struct WStage {  // one 64 x 128 bf16 tile = 1024 16-B chunks, 4 per thread
+  uint4 v[4];
+  __device__ __forceinline__ void load(const bf16_t* g, int64_t ld, int m0, int mlim, int c0, int clim) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = i * 256 + threadIdx.x, r = q >> 4, c = (q & 15) * 8;
+      v[i] = (m0 + r < mlim && c0 + c < clim) ? *reinterpret_cast<const uint4*>(g + (int64_t)(m0 + r) * ld + c0 + c)
+                                              : make_uint4(0, 0, 0, 0);
+    }
+  }
+  __device__ __forceinline__ void store(bf16_t* lds) const {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = i * 256 + threadIdx.x, r = q >> 4, c = (q & 15) * 8;
+      *reinterpret_cast<uint4*>(lds + r * WLD + c) = v[i];
+    }
+  }
+};
+}  // namespace
+
+__global__ __launch_bounds__(256) void gemm_wgrad_k(const bf16_t* __restrict__ dY, int64_t ldy,
+                                                    const bf16_t* __restrict__ X, int64_t ldx,
+                                                    float* __restrict__ part, int M, int P, int Q, int mslice) {
+  __shared__ __attribute__((aligned(16))) bf16_t As[2][WK * WLD];
+  __shared__ __attribute__((aligned(16))) bf16_t Bs[2][WK * WLD];
+  const int tq = (Q + WB - 1) / WB, tp = (P + WB - 1) / WB;
+  const int nwg = gridDim.x;
+  const int t = xcd_remap(blockIdx.x, nwg);
+  const int tile = t % (tp * tq), sl = t / (tp * tq);
+  const int p0 = (tile / tq) * WB, q0 = (tile % tq) * WB;
+  const int mb = sl * mslice, me = min(M, mb + mslice);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int wp = w >> 1, wq = w & 1;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = zero4();
+  WStage sa, sb;
+  sa.load(dY, ldy, mb, me, p0, P);
+  sb.load(X, ldx, mb, me, q0, Q);
+  const int KT = (me - mb + WK - 1) / WK;
+  sa.store(As[0]);
+  sb.store(Bs[0]);
+  __syncthreads();
+  for (int kt = 0; kt < KT; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < KT) {
+      sa.load(dY, ldy, mb + (kt + 1) * WK, me, p0, P);
+      sb.load(X, ldx, mb + (kt + 1) * WK, me, q0, Q);
+    }
+#pragma unroll
+    for (int ks = 0; ks < WK / 32; ++ks) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = frag_tr(As[cur], WLD, 32 * ks, wp * 64 + 16 * i);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = frag_tr(Bs[cur], WLD, 32 * ks, wq * 64 + 16 * j);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+    }
+    if (kt + 1 < KT) {  // buffer cur^1 was last read in iteration kt-1, before its closing barrier
+      sa.store(As[cur ^ 1]);
+      sb.store(Bs[cur ^ 1]);
+    }
+    __syncthreads();
+  }
+  float* pc = part + (int64_t)sl * P * Q;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int p = p0 + wp * 64 + 16 * i + 4 * (l >> 4) + r, q = q0 + wq * 64 + 16 * j + (l & 15);
+        if (p < P && q < Q) pc[(int64_t)p * Q + q] = acc[i][j][r];
+      }
+}
+
+// Large-tile path (M % 64 == 0): tiles filled by global_load_lds_dwordx4 straight into LDS (no VGPR
+// staging, double-buffered, one vmcnt(0) + barrier per k-step).  The DMA image must be lane-linear
+// (unpadded 256-B rows), which puts all rows of a transposed read on the same banks (8-way); the
+// 16-B chunk s of row r is therefore stored at s ^ 2 f(r), f(r) = (r & 3) | ((r >> 3) & 1) << 2,
+// applied on the SOURCE address and undone on the ds_read_b64_tr_b16 address (f separates the
+// rows r and r + 8 that one 32-lane half reads together: conflict-free, checked in a bank model).
+namespace {
+__device__ __forceinline__ int wswz(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
+
+__device__ __forceinline__ bf16x8 wfrag(const char* lds, int k0, int c0) {
+  const int l = threadIdx.x & 63, g = l >> 4, li = l & 15;
+  const int u = (c0 >> 2) + (li & 3);
+  const int r0 = k0 + 8 * g + (li >> 2), r1 = r0 + 4;
+  const char* a0 = lds + r0 * (WB * 2) + ((u ^ (wswz(r0) << 2)) << 3);
+  const char* a1 = lds + r1 * (WB * 2) + ((u ^ (wswz(r1) << 2)) << 3);
+  return cat8(tr4(reinterpret_cast<const bf16_t*>(a0)), tr4(reinterpret_cast<const bf16_t*>(a1)));
+}
+}  // namespace
+
+// 256 x 256 output tile, 512 threads (8 waves as 2 (P) x 4 (Q), each 128 x 64 = 8 x 4 MFMA tiles).
+// A 128^2 tile moves 64 FLOP per staged byte, which at the MFMA rate needs ~64 B/clk/CU of L2 read
+// bandwidth (the per-CU L2 share); 256^2 halves that.  Operand tiles are [64 tokens][256 cols] stored
+// as two swizzled [64][128] halves; LDS 2 buffers x (32 + 32) KB = 128 KB -> one workgroup per CU,
+// so the split count targets one full round of workgroups.
+template <int TP, int TQ>
+__global__ __launch_bounds__(512) void gemm_wgrad_big_k(const bf16_t* __restrict__ dY, int64_t ldy,
+                                                        const bf16_t* __restrict__ X, int64_t ldx,
+                                                        float* __restrict__ part, int M, int P, int Q, int mslice) {
+  constexpr int HB = WK * WB * 2;            // one [64][128] half-tile: 16 KB
+  constexpr int AB = (TP / WB) * HB, BB = (TQ / WB) * HB;
+  constexpr int WQN = 4, WPN = 2;            // wave grid
+  constexpr int MI = TP / WPN / 16, NJ = TQ / WQN / 16;
+  __shared__ __attribute__((aligned(16))) char smem[2 * (AB + BB)];
+  const int tq = (Q + TQ - 1) / TQ, tp = (P + TP - 1) / TP;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = t % (tp * tq), sl = t / (tp * tq);
+  const int p0 = (tile / tq) * TP, q0 = (tile % tq) * TQ;
+  const int mb = sl * mslice, me = min(M, mb + mslice);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int wp = w / WQN, wq = w % WQN;
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = zero4();
+  auto stage = [&](int m0, char* buf) {
+    // each [64][128] half-tile is one 256-thread DMA pass (4 chunks per thread): waves 0-3 take the
+    // even halves, waves 4-7 the odd ones; slot (r, s) receives source chunk s ^ 2 f(r)
+    const int half = threadIdx.x >> 8;  // 0 or 1
+#pragma unroll
+    for (int hh = 0; hh < TP / WB; hh += 2) {
+      const int h = hh + half;
+      if (h < TP / WB) {
+        const int tid = threadIdx.x & 255, w4 = tid >> 6;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int q = i * 256 + tid, r = q >> 4, s2 = q & 15;
+          const int col = min(p0 + h * WB + 8 * (s2 ^ (2 * wswz(r))), P - 8);
+          __builtin_amdgcn_global_load_lds((const void*)(dY + (int64_t)(m0 + r) * ldy + col),
+                                           (lds_void*)(buf + h * HB + (i * 256 + w4 * 64) * 16), 16, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int hh = 0; hh < TQ / WB; hh += 2) {
+      const int h = hh + half;
+      if (h < TQ / WB) {
+        const int tid = threadIdx.x & 255, w4 = tid >> 6;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int q = i * 256 + tid, r = q >> 4, s2 = q & 15;
+          const int col = min(q0 + h * WB + 8 * (s2 ^ (2 * wswz(r))), Q - 8);
+          __builtin_amdgcn_global_load_lds((const void*)(X + (int64_t)(m0 + r) * ldx + col),
+                                           (lds_void*)(buf + AB + h * HB + (i * 256 + w4 * 64) * 16), 16, 0, 0);
+        }
+      }
+    }
+  };
+  const int KT = (me - mb) / WK;
+  if (KT > 0) stage(mb, smem);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < KT; ++kt) {
+    const char* cur = smem + (kt & 1) * (AB + BB);
+    if (kt + 1 < KT) stage(mb + (kt + 1) * WK, smem + ((kt + 1) & 1) * (AB + BB));
+#pragma unroll
+    for (int ks = 0; ks < WK / 32; ++ks) {
+      bf16x8 bfr[NJ];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int c = wq * (TQ / WQN) + 16 * j;
+        bfr[j] = wfrag(cur + AB + (c / WB) * HB, 32 * ks, c % WB);
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int c = wp * (TP / WPN) + 16 * i;
+        const bf16x8 af = wfrag(cur + (c / WB) * HB, 32 * ks, c % WB);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma16(af, bfr[j], acc[i][j]);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  float* pc = part + (int64_t)sl * P * Q;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int p = p0 + wp * (TP / WPN) + 16 * i + 4 * (l >> 4) + r;
+        const int q = q0 + wq * (TQ / WQN) + 16 * j + (l & 15);
+        if (p < P && q < Q) pc[(int64_t)p * Q + q] = acc[i][j][r];
+      }
+}
+
+// out[i] = sum_s part[s][i] (fixed order), optionally += into out (gradient accumulation)
+__global__ void wgrad_reduce_k(const float* __restrict__ part, int S, int64_t n, float* __restrict__ out,
+                               bool accumulate) {
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i >= n) return;
+  float4 s = *reinterpret_cast<const float4*>(part + i);
+  for (int k = 1; k < S; ++k) {
+    const float4 v = *reinterpret_cast<const float4*>(part + (int64_t)k * n + i);
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  if (accumulate) {
+    const float4 o = *reinterpret_cast<const float4*>(out + i);
+    s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w;
+  }
+  *reinterpret_cast<float4*>(out + i) = s;
+}
+
+namespace {
+constexpr int BT = 256;  // big-tile size
+bool wgrad_big(int M, const void* dY, const void* X) {
+  return M % WK == 0 && ((uintptr_t)dY % 16) == 0 && ((uintptr_t)X % 16) == 0;
+}
+// split count: big tiles run one workgroup per CU -> aim at one full round (~256 workgroups) with
+// >= 8 k-steps per slice; small tiles run 2 per CU -> aim at >= 512
+int wgrad_splits(int M, int P, int Q, bool big) {
+  if (big) {
+    const int tiles = ((P + BT - 1) / BT) * ((Q + BT - 1) / BT);
+    int S = std::max(1, 256 / tiles);
+    while (S > 1 && M / S < 8 * WK) --S;
+    return S;
+  }
+  const int tiles = ((P + WB - 1) / WB) * ((Q + WB - 1) / WB);
+  int S = 1;
+  while (tiles * S < 512 && M / (S * 2) >= 4 * WK) S *= 2;
+  return S;
+}
+}  // namespace
+
+int gemm_wgrad_splits(int M, int P, int Q) { return wgrad_splits(M, P, Q, M % WK == 0); }
+
+hipError_t launch_gemm_wgrad(const void* dY, int64_t ldy, const void* X, int64_t ldx, float* part, float* out,
+                             int M, int P, int Q, bool accumulate, hipStream_t st) {
+  if (ldy % 8 || ldx % 8 || P % 8 || Q % 8 || ((int64_t)P * Q) % 4) return hipErrorInvalidValue;
+  const bool big = wgrad_big(M, dY, X);
+  const int S = wgrad_splits(M, P, Q, M % WK == 0);  // same rule as gemm_wgrad_splits (part size)
+  const int mslice = ((M + S - 1) / S + WK - 1) / WK * WK;
+  if (big) {
+    const int tiles = ((P + BT - 1) / BT) * ((Q + BT - 1) / BT);
+    hipLaunchKernelGGL((gemm_wgrad_big_k<BT, BT>), dim3(tiles * S), dim3(512), 0, st, (const bf16_t*)dY, ldy,
+                       (const bf16_t*)X, ldx, part, M, P, Q, mslice);
+  } else {
+    const int tiles = ((P + WB - 1) / WB) * ((Q + WB - 1) / WB);
+    hipLaunchKernelGGL(gemm_wgrad_k, dim3(tiles * S), dim3(256), 0, st, (const bf16_t*)dY, ldy, (const bf16_t*)X, ldx,
+                       part, M, P, Q, mslice);
+  }
+  MAMBA_HIP_CHECK(hipGetLastError());
+  const int64_t n = (int64_t)P * Q;
+  hipLaunchKernelGGL(wgrad_reduce_k, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, st, part, S, n, out,
+                     accumulate);
+  return hipGetLastError();
+}
+
+bool gemm_tn_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc) {
+  return M > 0 && N > 0 && K > 0 && K % GBK == 0 && N % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0;
+}
+
+hipError_t launch_gemm_tn_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M,
+                               int N, int K, hipStream_t st) {
+  if (!gemm_tn_supported(M, N, K, lda, ldb, ldc)) return hipErrorInvalidValue;
+  const int nwg = ((M + GBM - 1) / GBM) * ((N + GBN - 1) / GBN);
+  hipLaunchKernelGGL(gemm_tn_bf16_k, dim3(nwg), dim3(256), 0, st, (const bf16_t*)A, lda, (const bf16_t*)B, ldb,
+                     (bf16_t*)C, ldc, M, N, K);
+  return hipGetLastError();
+}
+
+}  // namespace mamba_amd

@@ -52,4 +52,15 @@ hipError_t launch_conv_update(const void* x, int dt, int64_t sxb, void* state, i
                               const float* w, const float* bias, void* out, int Bn, int C, int Wd, bool silu,
                               hipStream_t st);
 
+// ---- gemm.hip ---------------------------------------------------------------------------------
+// C[M, N] = A[M, K] . B[N, K]^T, bf16 in/out, fp32 accumulate (K % 64 == 0, N % 8 == 0)
+bool gemm_tn_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc);
+hipError_t launch_gemm_tn_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M,
+                               int N, int K, hipStream_t st);
+// fp32 C[P, Q] (+)= dY[M, P]^T . X[M, Q] (bf16 token-major operands), split over M into
+// gemm_wgrad_splits() fp32 partials (part: splits * P * Q floats) summed in fixed order
+int gemm_wgrad_splits(int M, int P, int Q);
+hipError_t launch_gemm_wgrad(const void* dY, int64_t ldy, const void* X, int64_t ldx, float* part, float* out,
+                             int M, int P, int Q, bool accumulate, hipStream_t st);
+
 }  // namespace mamba_amd

@@ -19,6 +19,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.conv1d import causal_conv1d_fn, causal_conv1d_update
+from ..ops.linear import linear
 from ..ops.norm import RMSNormGated
 from ..ops.reference import softplus_inverse
 from ..ops.selective_scan import selective_state_update
@@ -91,7 +92,7 @@ class Mamba2(nn.Module):
             if inference_params.seqlen_offset > 0:
                 out, _, _ = self.step(u, conv_state, ssm_state)
                 return out
-        zxbcdt = self.in_proj(u)
+        zxbcdt = linear(u, self.in_proj)
         if conv_state is None:
             y = mamba2_inner_fn(zxbcdt, self.conv1d.weight, self.conv1d.bias, self.dt_bias, self.A_log, self.D,
                                 self.norm.weight, self.norm.eps, self.headdim, self.ngroups, self.d_state,
@@ -99,7 +100,7 @@ class Mamba2(nn.Module):
                                 A_is_log=True)
         else:
             y = self._prefill(zxbcdt, -torch.exp(self.A_log.float()), conv_state, ssm_state)
-        return self.out_proj(y)
+        return linear(y, self.out_proj)
 
     def _prefill(self, zxbcdt, A, conv_state, ssm_state):
         """Prompt pass that also fills the decode cache (conv window + final SSM state)."""

@@ -31,14 +31,16 @@ def timeit(fn, reps=20, warm=3):
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--only", default="ssd,conv,norm,gnorm,ce,selscan")
+    p.add_argument("--only", default="ssd,conv,norm,gnorm,ce,selscan,gemm")
     p.add_argument("--reps", type=int, default=20)
     p.add_argument("--B", type=int, default=32)
     p.add_argument("--L", type=int, default=1024)
     a = p.parse_args()
     only = set(a.only.split(","))
     from mamba_distributed_amd.ops import _ext
+    from mamba_distributed_amd.utils.gemm_tuning import enable_tuned_gemms
     assert _ext.load(), _ext.error()
+    enable_tuned_gemms()  # library GEMMs with the same pinned solutions as training
     ops = torch.ops.mamba_amd
     dev = "cuda"
     B, L, H, P, N, G = a.B, a.L, 24, 64, 128, 1
@@ -58,6 +60,25 @@ def main():
         res["conv_cl_fwd"] = (t, 2 * out.numel() * 2)
         t = timeit(lambda: ops.conv1d_cl_bwd(xBC, w, bias, g, True, None), a.reps)
         res["conv_cl_bwd"] = (t, 3 * out.numel() * 2)
+    if "gemm" in only:
+        import torch.nn.functional as F
+        for (M, N, K, tag) in [(B * L, dproj, 768, "in_proj"), (B * L, 768, di, "out_proj")]:
+            A = torch.randn(M, K, device=dev).to(torch.bfloat16)
+            W = torch.randn(N, K, device=dev).to(torch.bfloat16)
+            t = timeit(lambda: F.linear(A, W), a.reps)
+            res[f"gemm_{tag}_hipblaslt"] = (t, 0)
+            print(f"{tag}: hipBLASLt {2 * M * N * K / t / 1e9:.0f} TF/s", flush=True)
+            t = timeit(lambda: ops.gemm_tn(A, W, None), a.reps)
+            res[f"gemm_{tag}_native"] = (t, 0)
+            print(f"{tag}: native    {2 * M * N * K / t / 1e9:.0f} TF/s", flush=True)
+            # weight gradient dW (N, K) = dY^T (N, M) . X (M, K)
+            dY = torch.randn(M, N, device=dev).to(torch.bfloat16)
+            t = timeit(lambda: torch.mm(dY.t(), A).float(), a.reps)
+            res[f"wgrad_{tag}_hipblaslt"] = (t, 0)
+            print(f"{tag} wgrad: hipBLASLt(+fp32 cast) {2 * M * N * K / t / 1e9:.0f} TF/s", flush=True)
+            t = timeit(lambda: ops.gemm_wgrad(dY, A, None, False), a.reps)
+            res[f"wgrad_{tag}_native"] = (t, 0)
+            print(f"{tag} wgrad: native fp32          {2 * M * N * K / t / 1e9:.0f} TF/s", flush=True)
     if "ssd" in only:
         xc = torch.randn(B, L, conv_dim, device=dev).to(torch.bfloat16)
         x = xc[..., :di].unflatten(-1, (H, P))

@@ -349,3 +349,36 @@ def test_fp32_forward_on_gpu_matches_cpu(cuda, layer):
         out = m(ids.to(cuda))[0]
     assert out.dtype == torch.float32
     assert rel(out.cpu(), ref) < 1e-4
+
+
+@pytest.mark.parametrize("M,N,K", [(32768, 3352, 768), (4096, 768, 1536), (300, 200, 128), (129, 8, 64)])
+def test_gemm_tn(cuda, M, N, K):
+    """C = A B^T (bf16, fp32 accumulate) vs an fp32 matmul; ragged M/N tails and a strided output."""
+    ops = torch.ops.mamba_amd
+    torch.manual_seed(0)
+    A = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    B = torch.randn(N, K, device=cuda).to(torch.bfloat16)
+    ref = A.float() @ B.float().t()
+    C = ops.gemm_tn(A, B, None)
+    assert rel(C.float(), ref) < 1e-2
+    wide = torch.zeros(M, N + 24, device=cuda, dtype=torch.bfloat16)
+    ops.gemm_tn(A, B, wide[:, 8:8 + N])
+    assert rel(wide[:, 8:8 + N].float(), ref) < 1e-2
+    assert wide[:, :8].abs().sum() == 0 and wide[:, 8 + N:].abs().sum() == 0
+
+
+@pytest.mark.parametrize("M,P,Q", [(32768, 768, 1536), (32768, 3352, 768), (1000, 200, 136), (64, 8, 8)])
+def test_gemm_wgrad(cuda, M, P, Q):
+    """dW = dY^T X in fp32 (split over M, fixed-order reduction) vs fp32 matmul; accumulate mode."""
+    ops = torch.ops.mamba_amd
+    torch.manual_seed(1)
+    dY = torch.randn(M, P, device=cuda).to(torch.bfloat16)
+    X = torch.randn(M, Q, device=cuda).to(torch.bfloat16)
+    ref = dY.float().t() @ X.float()
+    C = ops.gemm_wgrad(dY, X, None, False)
+    assert C.dtype == torch.float32 and rel(C, ref) < 1e-4
+    acc = torch.ones(P, Q, device=cuda)
+    ops.gemm_wgrad(dY, X, acc, True)
+    assert rel(acc, ref + 1) < 1e-4
+    C2 = ops.gemm_wgrad(dY, X, None, False)
+    assert torch.equal(C, C2)  # deterministic
