@@ -4,7 +4,8 @@
 
 * ``kernels/*.hip``  pure HIP/CDNA4 device code + host launchers (no torch headers -> fast
   compiles), ``hipcc -c --offload-arch=gfx950 -O3``.
-* ``runtime/*.cpp``  host-only C++ runtime pieces (token-shard prefetcher), g++.
+* ``runtime/*.cpp``  host-only C++ runtime pieces (``token_loader.cpp``: mmap'd .npy shards +
+  prefetch thread, ``torch.classes.mamba_amd.TokenLoader``), g++ against torch's headers.
 * ``bindings.cpp``   the PyTorch operator registrations (``TORCH_LIBRARY(mamba_amd, ...)``),
   compiled against torch's headers.
 * Linked with hipcc into ``_C.so`` against torch's own libraries (the HIP runtime is the one

@@ -31,6 +31,18 @@ constexpr int LD64 = 80;  // padded LDS row (elements) for 64-wide bf16 tiles: c
 __device__ __forceinline__ float ld_any(const void* p, int dt, int64_t i) {
   return dt == kF32 ? reinterpret_cast<const float*>(p)[i] : bf2f(reinterpret_cast<const bf16_t*>(p)[i]);
 }
+// Prefetch form of ld_any: two unconditional 16-bit loads (the same instruction for either dtype, no
+// branch, no use of the value) so a register prefetch never forces an early s_waitcnt; raw_f()
+// combines them at the point of use.
+struct RawF { uint32_t lo, hi; };
+__device__ __forceinline__ RawF ld_raw(const void* p, int dt, int64_t i) {
+  const uint16_t* q = reinterpret_cast<const uint16_t*>(p);
+  const int64_t e = dt == kF32 ? 2 * i : i;
+  return {q[e], q[e + (dt == kF32 ? 1 : 0)]};
+}
+__device__ __forceinline__ float raw_f(RawF r, int dt) {
+  return __uint_as_float(dt == kF32 ? ((r.hi << 16) | r.lo) : (r.lo << 16));
+}
 __device__ __forceinline__ void st_any(void* p, int dt, int64_t i, float v) {
   if (dt == kF32) reinterpret_cast<float*>(p)[i] = v;
   else reinterpret_cast<bf16_t*>(p)[i] = f2bf(v);
@@ -67,11 +79,16 @@ template <int NT>
 struct Tile64 {
   static constexpr int K = 512 / NT;
   uint4 v[K];
+  int nv;  // rows >= nv are zero-filled at store time
+  // Branch-free: rows past the end re-read the last valid row (always a legal address) and are
+  // zeroed in store().  A `valid ? load : 0` select here makes the compiler wait for the load on
+  // the spot (s_waitcnt vmcnt(0) right after issue), which serialises the whole prefetch.
   __device__ __forceinline__ void load(const bf16_t* g, int64_t gs, int valid) {
+    nv = valid;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const int idx = threadIdx.x + k * NT, r = idx >> 3, c = (idx & 7) * 8;
-      v[k] = r < valid ? *reinterpret_cast<const uint4*>(g + (int64_t)r * gs + c) : make_uint4(0, 0, 0, 0);
+      const int idx = threadIdx.x + k * NT, r = min(idx >> 3, valid - 1), c = (idx & 7) * 8;
+      v[k] = *reinterpret_cast<const uint4*>(g + (int64_t)r * gs + c);
     }
   }
   __device__ __forceinline__ void store(bf16_t* lds, int ld, const float* rowscale = nullptr) const {
@@ -79,6 +96,7 @@ struct Tile64 {
     for (int k = 0; k < K; ++k) {
       const int idx = threadIdx.x + k * NT, r = idx >> 3, c = (idx & 7) * 8;
       uint4 d = v[k];
+      if (r >= nv) d = make_uint4(0, 0, 0, 0);
       if (rowscale) {
         float f[8];
         ld8bf(reinterpret_cast<const bf16_t*>(&d), f);
@@ -156,10 +174,8 @@ __global__ __launch_bounds__(256) void ssd_fused_fwd_k(SSDArgs a) {
       pb.t[i].load(bg + (int64_t)c * Q * a.sBl + 64 * i, a.sBl, valid);
       pc.t[i].load(cg + (int64_t)c * Q * a.sCl + 64 * i, a.sCl, valid);
     }
-    if (threadIdx.x < Q) {
-      pcum = cumbh[c * Q + threadIdx.x];
-      pdt = dtbh[c * Q + threadIdx.x];
-    }
+    pcum = cumbh[c * Q + (threadIdx.x & 63)];
+    pdt = dtbh[c * Q + (threadIdx.x & 63)];
   };
   prefetch(0);
   for (int c = 0; c < a.nc; ++c) {
@@ -308,20 +324,21 @@ __global__ __launch_bounds__(256) void ssd_dstate_bwd_k(SSDArgs a) {
   }
   Tile64<256> py;
   TileState<256, N> pcs;
-  float pe = 0.f;
+  float pe = 0.f, pl = 0.f;
   auto prefetch = [&](int c) {
+    pl = cumbh[c * Q + Q - 1];
     const int valid = min(Q, a.L - c * Q);
     py.load(yg + (int64_t)c * Q * a.sdyl, a.sdyl, valid);
 #pragma unroll
     for (int i = 0; i < N / 64; ++i) pcs.t[i].load(cg + (int64_t)c * Q * a.sCl + 64 * i, a.sCl, valid);
-    if (threadIdx.x < Q) pe = __expf(cumbh[c * Q + threadIdx.x]);
+    pe = cumbh[c * Q + (threadIdx.x & 63)];  // exp at use: no ALU on a value still in flight
   };
   prefetch(a.nc - 1);
   for (int c = a.nc - 1; c >= 0; --c) {
 #pragma unroll
     for (int nt = 0; nt < NTS; ++nt) acc_to_lds(Os, LDN, 16 * w, 16 * nt, acc[nt]);
-    if (threadIdx.x < Q) er[threadIdx.x] = pe;
-    const float decay = __expf(cumbh[c * Q + Q - 1]);
+    if (threadIdx.x < Q) er[threadIdx.x] = __expf(pe);
+    const float decay = __expf(pl);
     __syncthreads();
     store_tile<P, N>(a.dstates + ((((int64_t)b * a.nc + c) * a.H + h) * P) * N, N, Os, LDN, P);
     py.store(Ys, LD64, er);
@@ -381,17 +398,18 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
   const int valid = min(Q, a.L - c * Q);
   Tile64<512> px, py;
   TileState<512, N> ps, pds;
-  float pc = 0.f, pd = 0.f, praw = 0.f;
+  float pc = 0.f, pd = 0.f;
+  RawF praw;
+  const int tl = min(c * Q + (int)(threadIdx.x & 63), a.L - 1);  // clamped: the loads below never branch
   auto prefetch = [&](int h) {
     px.load(a.x + (int64_t)b * a.sxb + (int64_t)c * Q * a.sxl + (int64_t)h * a.sxh, a.sxl, valid);
-    if (threadIdx.x < Q && c * Q + (int)threadIdx.x < a.L)
-      praw = ld_any(a.dt, a.dt_dtype, (int64_t)b * a.sdtb + (int64_t)(c * Q + threadIdx.x) * a.sdtl + (int64_t)h * a.sdth);
+    praw = ld_raw(a.dt, a.dt_dtype, (int64_t)b * a.sdtb + (int64_t)tl * a.sdtl + (int64_t)h * a.sdth);
     py.load(a.dy + (int64_t)b * a.sdyb + (int64_t)c * Q * a.sdyl + (int64_t)h * a.sdyh, a.sdyl, valid);
     const int64_t soff = ((((int64_t)b * a.nc + c) * a.H + h) * P) * N;
     ps.load(a.states + soff);
     pds.load(a.dstates + soff);
-    if (threadIdx.x < Q) {
-      const int64_t bh = ((int64_t)b * a.H + h) * a.Lp + (int64_t)c * Q + threadIdx.x;
+    {
+      const int64_t bh = ((int64_t)b * a.H + h) * a.Lp + (int64_t)c * Q + (threadIdx.x & 63);
       pc = a.cum[bh];
       pd = a.dtp[bh];
     }
@@ -470,7 +488,7 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
     if (threadIdx.x < Q) {
       cumr[threadIdx.x] = pc;
       dtr[hh & 7][threadIdx.x] = pd;
-      rawl[hh & 7][threadIdx.x] = praw;
+      rawl[hh & 7][threadIdx.x] = raw_f(praw, a.dt_dtype);
     }
     px.store(Xs, LD64);
     py.store(dYs, LD64);

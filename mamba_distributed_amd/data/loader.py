@@ -4,9 +4,11 @@
 the split, rank r starts at B*T*r and strides B*T*world, x = buf[:-1], y = buf[1:], rollover to
 the next shard (mod #shards) when the next global window would overflow, ``reset()`` rewinds.
 
-Differences: shards are memory-mapped (``np.load(mmap_mode='r')``) instead of
-materialised as int64 in host RAM, and batches can be produced straight into pinned memory by
-the native prefetcher (``native_loader.py``) so the H2D copy is asynchronous.
+Differences: shards are memory-mapped instead of materialised as int64 in host
+RAM.  With the native extension loaded (``backend="auto"``), batches come from the C++
+``TokenLoader`` (csrc/runtime/token_loader.cpp): a producer thread assembles them ``prefetch``
+batches ahead, straight into pinned memory when a GPU is present, so the training loop only issues
+a non_blocking H2D copy.  ``backend="python"`` is the numpy path with identical semantics.
 ``SyntheticTokens`` is the no-dataset source used by bench.py / tests (BASELINE: synthetic data).
 """
 from __future__ import annotations
@@ -29,7 +31,8 @@ def _load_tokens_np(filename: str) -> np.ndarray:
 
 class DataLoaderLite:
     def __init__(self, B, T, process_rank, num_processes, split, master_process=True,
-                 data_root: str = "edu_fineweb10B", verbose: bool = True):
+                 data_root: str = "edu_fineweb10B", verbose: bool = True, backend: str = "auto",
+                 prefetch: int = 4, pin_memory: Optional[bool] = None):
         self.B = B
         self.T = T
         self.process_rank = process_rank
@@ -40,22 +43,48 @@ class DataLoaderLite:
         assert len(self.shards) > 0, f"no shards found for split {split}"
         if master_process and verbose:
             print(f"found {len(self.shards)} shards for split {split}")
+        assert backend in {"auto", "native", "python"}
+        self._native = None
+        if backend != "python":
+            from ..ops import _ext
+            if _ext.load():
+                if pin_memory is None:
+                    pin_memory = torch.cuda.is_available()
+                self._native = torch.classes.mamba_amd.TokenLoader(
+                    self.shards, B, T, process_rank, num_processes, prefetch, bool(pin_memory))
+            elif backend == "native":
+                raise RuntimeError(f"native TokenLoader unavailable: {_ext.error()}")
+        self.backend = "native" if self._native is not None else "python"
         self.reset()
 
     def reset(self):
+        if self._native is not None:
+            self._native.reset()
+            return
         self.current_shard = 0
         self.tokens = _load_tokens_np(self.shards[self.current_shard])
         self.current_position = self.B * self.T * self.process_rank
+
+    # the reference attribute names stay readable on both backends
+    def __getattr__(self, name):
+        if name in ("current_shard", "current_position") and self.__dict__.get("_native") is not None:
+            return self._native.state()[0 if name == "current_shard" else 1]
+        raise AttributeError(name)
 
     def state_dict(self):
         return {"current_shard": self.current_shard, "current_position": self.current_position}
 
     def load_state_dict(self, s):
+        if self._native is not None:
+            self._native.set_state(int(s["current_shard"]), int(s["current_position"]))
+            return
         self.current_shard = s["current_shard"]
         self.tokens = _load_tokens_np(self.shards[self.current_shard])
         self.current_position = s["current_position"]
 
     def next_batch(self):
+        if self._native is not None:
+            return self._native.next()
         B, T = self.B, self.T
         buf = torch.from_numpy(np.asarray(
             self.tokens[self.current_position: self.current_position + B * T + 1]).astype(np.int64))

@@ -10,13 +10,23 @@ from mamba_distributed_amd.utils.checkpoint import (config_from_checkpoint, late
                                                     save_checkpoint)
 
 
-def test_loader_rank_striding_and_rollover(tmp_path):
+import pytest
+
+from mamba_distributed_amd.ops import _ext
+
+_BACKENDS = ["python", pytest.param("native", marks=pytest.mark.skipif(not _ext.load(), reason="extension not built"))]
+
+
+@pytest.mark.parametrize("backend", _BACKENDS)
+def test_loader_rank_striding_and_rollover(tmp_path, backend):
     root = str(tmp_path / "shards")
     write_synthetic_shards(root, n_train=2, n_val=1, tokens_per_shard=1000, vocab_size=500)
     shards = sorted(p for p in os.listdir(root) if "train" in p)
     toks = [np.load(os.path.join(root, s)).astype(np.int64) for s in shards]
     B, T, W = 2, 8, 3
-    loaders = [DataLoaderLite(B, T, r, W, "train", r == 0, data_root=root, verbose=False) for r in range(W)]
+    loaders = [DataLoaderLite(B, T, r, W, "train", r == 0, data_root=root, verbose=False, backend=backend)
+               for r in range(W)]
+    assert all(ld.backend == backend for ld in loaders)
     for r, ld in enumerate(loaders):
         x, y = ld.next_batch()
         start = B * T * r
@@ -35,6 +45,33 @@ def test_loader_rank_striding_and_rollover(tmp_path):
     assert torch.equal(x.flatten(), torch.from_numpy(toks[1][B * T * 1:B * T * 2]))
     ld.reset()
     assert ld.current_shard == 0 and ld.current_position == B * T * 1
+
+
+@pytest.mark.skipif(not _ext.load(), reason="extension not built")
+@pytest.mark.parametrize("dtype", [np.uint16, np.int32, np.int64, np.uint8])
+def test_native_loader_matches_python(tmp_path, dtype):
+    """C++ TokenLoader (mmap + prefetch thread) == numpy DataLoaderLite, batch for batch, across
+    shard rollovers and a save/restore of the cursor mid-stream."""
+    root = str(tmp_path / "shards")
+    write_synthetic_shards(root, n_train=3, n_val=1, tokens_per_shard=777, vocab_size=250, dtype=dtype)
+    B, T, W = 3, 7, 2
+    for r in range(W):
+        py = DataLoaderLite(B, T, r, W, "train", False, data_root=root, verbose=False, backend="python")
+        nat = DataLoaderLite(B, T, r, W, "train", False, data_root=root, verbose=False, backend="native", prefetch=3)
+        saved = None
+        for i in range(40):
+            if i == 17:
+                saved = nat.state_dict()
+                assert saved == py.state_dict()
+            xp, yp = py.next_batch()
+            xn, yn = nat.next_batch()
+            assert xn.dtype == torch.int64 and xn.shape == (B, T)
+            assert torch.equal(xp, xn) and torch.equal(yp, yn), (r, i)
+        assert nat.state_dict() == py.state_dict()
+        nat.load_state_dict(saved)
+        py.load_state_dict(saved)
+        for _ in range(10):
+            assert torch.equal(py.next_batch()[0], nat.next_batch()[0])
 
 
 def test_checkpoint_roundtrip_default_torch_load(tmp_path):

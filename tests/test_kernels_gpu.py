@@ -159,6 +159,21 @@ def test_ssd_fwd_bwd(cuda, b, L, H, G, N):
         assert rel(a, b_) < 3e-2, (nm, rel(a, b_))
 
 
+def test_ssd_fp32_dt_partial_chunk(cuda):
+    """dt given in fp32 (two-halfword raw prefetch path) with a partial last chunk (clamped rows)."""
+    from mamba_distributed_amd.ops.ssd import mamba_chunk_scan_combined
+    x, dt, A, Bm, Cm, D, dt_bias = _ssd_inputs(cuda, 2, 130, 8, 1, 128, seed=3)
+    dt = dt.float()
+
+    def f(x, dt, A, Bm, Cm, D, dt_bias):
+        return mamba_chunk_scan_combined(x, dt, A, Bm, Cm, 64, D=D, dt_bias=dt_bias, dt_softplus=True)
+
+    on, orf, gn, gr = run_both(f, f, [x, dt, A, Bm, Cm, D, dt_bias])
+    assert rel(on, orf) < 2e-2, rel(on, orf)
+    for nm, a, b_ in zip(["x", "dt", "A", "B", "C", "D", "dt_bias"], gn, gr):
+        assert rel(a, b_) < 3e-2, (nm, rel(a, b_))
+
+
 @pytest.mark.parametrize("hg", ["24", "12", "3"])
 def test_ssd_head_groups(cuda, monkeypatch, hg):
     """chunk-bwd head groups larger than the 8-slot dt-gradient ring (flushed every 8 heads) and
