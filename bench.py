@@ -47,6 +47,7 @@ def main():
 
     from mamba_distributed_amd import LMHeadModel, preset
     from mamba_distributed_amd.data.loader import SyntheticTokens
+    from mamba_distributed_amd.ops import grad_accum
     from mamba_distributed_amd.parallel import ddp as ddp_mod
     from mamba_distributed_amd.parallel.dist import all_reduce_avg, all_reduce_max, barrier, destroy, init_distributed
 
@@ -68,14 +69,15 @@ def main():
     def step():
         opt.zero_grad(set_to_none=True)
         loss_acc = torch.zeros((), device=dev)
-        for micro in range(accum):
-            x, y = loader.next_batch()
-            ddp_mod.set_grad_sync(dmodel, micro == accum - 1)
-            with torch.autocast(device_type="cuda", dtype=torch.bfloat16):
-                _, loss = dmodel(x, y, return_logits=not fused)
-            loss = loss / accum
-            loss_acc += loss.detach().float()
-            loss.backward()
+        with grad_accum.accumulation_scope():
+            for micro in range(accum):
+                x, y = loader.next_batch()
+                ddp_mod.set_grad_sync(dmodel, micro == accum - 1)
+                with torch.autocast(device_type="cuda", dtype=torch.bfloat16):
+                    _, loss = dmodel(x, y, return_logits=not fused)
+                loss = loss / accum
+                loss_acc += loss.detach().float()
+                loss.backward()
         all_reduce_avg(loss_acc)
         torch.nn.utils.clip_grad_norm_(dmodel.parameters(), 1.0)
         opt.step()

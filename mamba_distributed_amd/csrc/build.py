@@ -32,6 +32,10 @@ OUT = os.path.join(PKG, "_C.so")
 ARCH = os.environ.get("MAMBA_AMD_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
+# MFMA accumulators in arch VGPRs instead of AGPRs where the kernels fit in 256 VGPRs anyway: the
+# SSD chunk walks touch their running state with VALU every chunk (decay, bf16 staging), and in
+# AGPRs each touch costs a v_accvgpr_read/write pair (~100 extra VALU per chunk in the forward).
+PER_FILE_FLAGS = {"ssd.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
 
 
 def torch_paths():
@@ -71,8 +75,8 @@ def build(jobs: int = 8, force: bool = False, debug: bool = False, verbose: bool
     for src in sorted(glob.glob(os.path.join(HERE, "kernels", "*.hip"))):
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
         objs.append(obj)
-        if force or _newer(src, obj, headers):
-            jobs_list.append([HIPCC, "-c", src, "-o", obj] + hip_flags)
+        if force or _newer(src, obj, headers) or _newer(os.path.abspath(__file__), obj, []):
+            jobs_list.append([HIPCC, "-c", src, "-o", obj] + hip_flags + PER_FILE_FLAGS.get(os.path.basename(src), []))
     for src in sorted(glob.glob(os.path.join(HERE, "runtime", "*.cpp"))):
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
         objs.append(obj)

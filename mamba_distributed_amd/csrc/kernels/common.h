@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 #include <stdint.h>
+#include <algorithm>
 #include "types.h"
 
 namespace mamba_amd {

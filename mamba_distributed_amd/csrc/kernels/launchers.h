@@ -8,7 +8,7 @@
 namespace mamba_amd {
 
 // deterministic column sum of a (nrows, ncols) fp32 partial matrix (norm.hip)
-hipError_t launch_colsum(const float* part, int nrows, int ncols, float* out, hipStream_t st);
+hipError_t launch_colsum(float* part, int nrows, int ncols, float* out, hipStream_t st);  // clobbers part
 
 // ---- norm.hip -------------------------------------------------------------------------------
 hipError_t launch_add_rmsnorm_fwd(const void* x, int xdt, int64_t sx, const void* res, int rdt, int64_t sr,

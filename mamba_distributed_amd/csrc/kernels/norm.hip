@@ -143,11 +143,11 @@ __global__ __launch_bounds__(256) void add_rmsnorm_bwd_k(
   block_dw_partial<NCH>(acc, part, D, lds);
 }
 
-// out[c] = sum_r part[r][c] in a fixed order.  Block = 64 columns x 16 row-groups (1024 threads);
-// each thread sums a strided row subset (independent loads -> deep memory-level parallelism), the
-// 16 group sums are combined through LDS in index order -> bitwise deterministic.
+// out[c] = sum_r part[r * rstride + c] in a fixed order.  Block = 64 columns x 16 row-groups (1024
+// threads); each thread sums a strided row subset (independent loads -> deep memory-level
+// parallelism), the 16 group sums are combined through LDS in index order -> bitwise deterministic.
 __global__ __launch_bounds__(1024) void colsum_k(const float* __restrict__ part, int nrows, int ncols,
-                                                 float* __restrict__ out) {
+                                                 int64_t rstride, float* __restrict__ out) {
   __shared__ float red[16][65];
   const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
@@ -155,11 +155,11 @@ __global__ __launch_bounds__(1024) void colsum_k(const float* __restrict__ part,
   if (c < ncols) {
     int r = rg;
     for (; r + 48 < nrows; r += 64) {
-      const float a0 = part[(int64_t)r * ncols + c], a1 = part[(int64_t)(r + 16) * ncols + c];
-      const float a2 = part[(int64_t)(r + 32) * ncols + c], a3 = part[(int64_t)(r + 48) * ncols + c];
+      const float a0 = part[(int64_t)r * rstride + c], a1 = part[(int64_t)(r + 16) * rstride + c];
+      const float a2 = part[(int64_t)(r + 32) * rstride + c], a3 = part[(int64_t)(r + 48) * rstride + c];
       s += (a0 + a1) + (a2 + a3);
     }
-    for (; r < nrows; r += 16) s += part[(int64_t)r * ncols + c];
+    for (; r < nrows; r += 16) s += part[(int64_t)r * rstride + c];
   }
   red[rg][cl] = s;
   __syncthreads();
@@ -171,8 +171,43 @@ __global__ __launch_bounds__(1024) void colsum_k(const float* __restrict__ part,
   }
 }
 
-hipError_t launch_colsum(const float* part, int nrows, int ncols, float* out, hipStream_t st) {
-  hipLaunchKernelGGL(colsum_k, dim3((ncols + 63) / 64), dim3(1024), 0, st, part, nrows, ncols, out);
+// Stage 1 of a tall reduction: block (column tile, split s) sums rows [s*R, min((s+1)*R, nrows)) and
+// writes the result over the first row of its own range (every read of that range precedes the
+// write: the block barrier), so no scratch buffer is needed and blocks never touch each other's rows.
+__global__ __launch_bounds__(256) void colsum_split_k(float* __restrict__ part, int nrows, int ncols, int R) {
+  __shared__ float red[4][65];
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int r0 = blockIdx.y * R, r1 = min(r0 + R, nrows);
+  float s0 = 0.f, s1 = 0.f;
+  if (c < ncols) {
+    int r = r0 + rg;
+    for (; r + 4 < r1; r += 8) {
+      s0 += part[(int64_t)r * ncols + c];
+      s1 += part[(int64_t)(r + 4) * ncols + c];
+    }
+    if (r < r1) s0 += part[(int64_t)r * ncols + c];
+  }
+  red[rg][cl] = s0 + s1;
+  __syncthreads();
+  if (rg == 0 && c < ncols) part[(int64_t)r0 * ncols + c] = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
+}
+
+// Column sums of a (nrows, ncols) fp32 partial block (clobbers `part`).  Tall blocks with few column
+// tiles (norm weight grads: 2048 x 768 -> 12 tiles) are split over >= ~512 workgroups first, so the
+// sum is bandwidth- rather than latency-bound; the second stage reduces the RS split sums.
+hipError_t launch_colsum(float* part, int nrows, int ncols, float* out, hipStream_t st) {
+  const int tiles = (ncols + 63) / 64;
+  int RS = std::min((nrows + 15) / 16, std::max(1, 512 / tiles));
+  if (RS <= 1 || nrows <= 64) {
+    hipLaunchKernelGGL(colsum_k, dim3(tiles), dim3(1024), 0, st, part, nrows, ncols, (int64_t)ncols, out);
+    return hipGetLastError();
+  }
+  const int R = (nrows + RS - 1) / RS;
+  RS = (nrows + R - 1) / R;
+  hipLaunchKernelGGL(colsum_split_k, dim3(tiles, RS), dim3(256), 0, st, part, nrows, ncols, R);
+  MAMBA_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(colsum_k, dim3(tiles), dim3(1024), 0, st, part, RS, ncols, (int64_t)R * ncols, out);
   return hipGetLastError();
 }
 

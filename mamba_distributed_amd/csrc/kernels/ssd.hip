@@ -96,7 +96,7 @@ struct Tile64 {
     for (int k = 0; k < K; ++k) {
       const int idx = threadIdx.x + k * NT, r = idx >> 3, c = (idx & 7) * 8;
       uint4 d = v[k];
-      if (r >= nv) d = make_uint4(0, 0, 0, 0);
+      if (nv < 64 && r >= nv) d = make_uint4(0, 0, 0, 0);  // uniform test first: full tiles skip the selects
       if (rowscale) {
         float f[8];
         ld8bf(reinterpret_cast<const bf16_t*>(&d), f);

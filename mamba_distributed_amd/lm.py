@@ -56,7 +56,7 @@ class LMHeadModel(MambaLMHeadModel):
                                  num_last_tokens=num_last_tokens, **mixer_kwargs).logits
         loss = None
         if targets is not None:
-            loss = cross_entropy(logits.view(-1, logits.size(-1)), targets.view(-1))
+            loss = cross_entropy(logits.reshape(-1, logits.size(-1)), targets.reshape(-1))
         return logits, loss
 
     # ------------------------------------------------------------------------------------

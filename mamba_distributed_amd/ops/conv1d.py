@@ -16,7 +16,7 @@ from typing import Optional
 
 import torch
 
-from . import _ext
+from . import _ext, grad_accum
 from .reference import causal_conv1d_ref, causal_conv1d_update_ref
 
 
@@ -41,6 +41,7 @@ class _CausalConv1dFn(torch.autograd.Function):
         ctx.save_for_backward(x, w2, bias)
         ctx.silu = silu
         ctx.wshape = weight.shape
+        ctx.params = (weight, bias)
         return out
 
     @staticmethod
@@ -52,7 +53,9 @@ class _CausalConv1dFn(torch.autograd.Function):
             dx = dx.transpose(1, 2)
         else:
             dx, dw, db = ops.conv1d_cf_bwd(x, w2, bias, dout, ctx.silu, None)
-        return dx, dw.reshape(ctx.wshape).to(w2.dtype), (db.to(bias.dtype) if bias is not None else None), None
+        pw, pb = ctx.params
+        return (dx, grad_accum.defer(pw, dw.reshape(ctx.wshape).to(w2.dtype)),
+                (grad_accum.defer(pb, db.to(bias.dtype)) if bias is not None else None), None)
 
 
 def causal_conv1d_fn(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None,

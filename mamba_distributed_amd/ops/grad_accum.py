@@ -1,0 +1,105 @@
+"""Micro-batch gradient accumulation without per-parameter add kernels (reference train.py:205-219,
+SURVEY.md R14).
+
+With 16 micro-batches per optimizer step (1 GPU) autograd's AccumulateGrad runs ``p.grad += g``
+for every parameter on every micro-step: ~450 tiny add kernels per micro-batch for the 280M
+Mamba-2 model (~2.3 ms, mostly launch latency), plus the full read-modify-write of the two large
+projection gradients.  Inside an ``accumulation_scope`` on the no-sync micro-steps:
+
+  * the projection weight gradients are accumulated by the weight-gradient GEMM itself
+    (``gemm_wgrad(..., out=p.grad, accumulate=True)``: the fixed-order split-K reduction adds into
+    the existing gradient, still deterministic);
+  * every other parameter gradient produced by a native op is queued and applied by ONE
+    ``torch._foreach_add_`` when the backward pass finishes.
+
+The last micro-step (the one that triggers DDP's bucketed all-reduce) and anything outside a scope
+use the normal autograd path, so DDP's gradient hooks fire exactly as usual.  The scope also caches
+bf16 copies of the projection weights: weights cannot change between the micro-steps of one
+optimizer step, and the fused AdamW update does not bump tensor versions, so the cache is tied to
+the scope rather than to version counters.
+"""
+from __future__ import annotations
+
+import contextlib
+from typing import Dict, List, Tuple
+
+import torch
+
+_scope_depth = 0
+_direct = False
+_pending: List[Tuple[torch.Tensor, torch.Tensor]] = []
+_flush_queued = False
+_wcache: Dict[Tuple[int, torch.dtype], Tuple[torch.Tensor, torch.Tensor]] = {}
+
+
+@contextlib.contextmanager
+def accumulation_scope():
+    """Wrap the micro-batch loop of ONE optimizer step (no parameter updates inside)."""
+    global _scope_depth, _direct
+    _scope_depth += 1
+    try:
+        yield
+    finally:
+        _scope_depth -= 1
+        if _scope_depth == 0:
+            _direct = False
+            _wcache.clear()
+
+
+def set_direct(enabled: bool) -> None:
+    """Called per micro-step (parallel/ddp.py::set_grad_sync): True on the no-sync micro-steps."""
+    global _direct
+    _direct = bool(enabled) and _scope_depth > 0
+
+
+def in_scope() -> bool:
+    return _scope_depth > 0
+
+
+def direct() -> bool:
+    return _direct and _scope_depth > 0
+
+
+def cached_cast(w: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    """``w.to(dtype)``, reused across the micro-steps of the current scope."""
+    if w.dtype == dtype or _scope_depth == 0:
+        return w.to(dtype)
+    key = (id(w), dtype)
+    ent = _wcache.get(key)
+    if ent is not None and ent[0] is w:
+        return ent[1]
+    t = w.to(dtype)
+    _wcache[key] = (w, t)  # holding w keeps id(w) unique for the scope's lifetime
+    return t
+
+
+def accumulable(param) -> bool:
+    """The parameter already holds a gradient the current micro-step may add into directly."""
+    return (direct() and isinstance(param, torch.Tensor) and param.is_leaf and param.requires_grad
+            and param.grad is not None)
+
+
+def _flush() -> None:
+    global _flush_queued
+    _flush_queued = False
+    if _pending:
+        dst = [d for d, _ in _pending]
+        src = [s for _, s in _pending]
+        _pending.clear()
+        torch._foreach_add_(dst, src)
+
+
+def defer(param, grad):
+    """Return value for ``param``'s slot in an autograd backward: ``grad`` itself on the normal
+    path, or None after queueing it for the batched accumulation at the end of this backward."""
+    global _flush_queued
+    if grad is None or not accumulable(param):
+        return grad
+    g = param.grad
+    if g.shape != grad.shape or g.dtype != grad.dtype or g.device != grad.device:
+        return grad
+    _pending.append((g, grad))
+    if not _flush_queued:
+        torch.autograd.Variable._execution_engine.queue_callback(_flush)
+        _flush_queued = True
+    return None

@@ -14,6 +14,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _ext
+from . import grad_accum
 
 
 def _compute_dtype(x: torch.Tensor) -> torch.dtype:
@@ -32,9 +33,10 @@ class _ProjFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, cd):
         x2 = x.reshape(-1, x.shape[-1]).to(cd)
-        w = weight.to(cd)
+        w = grad_accum.cached_cast(weight, cd)
         y = F.linear(x2, w)
         ctx.save_for_backward(x2, w)
+        ctx.param = weight
         ctx.wdtype = weight.dtype
         ctx.xshape = x.shape
         return y.view(*x.shape[:-1], w.shape[0])
@@ -50,11 +52,15 @@ class _ProjFn(torch.autograd.Function):
         dx = torch.mm(dy2, w) if ctx.needs_input_grad[0] else None
         dw = None
         if ctx.needs_input_grad[1]:
-            if _native_ok(dy2, x2):
-                dw = _ext.ops().gemm_wgrad(dy2, x2, None, False)
+            p = ctx.param
+            native = _native_ok(dy2, x2)
+            if (native and grad_accum.accumulable(p) and p.grad.dtype == torch.float32 and p.grad.is_contiguous()
+                    and p.grad.shape == w.shape):
+                # no-sync micro-step: the split-K reduction adds straight into p.grad
+                _ext.ops().gemm_wgrad(dy2, x2, p.grad, True)
             else:
-                dw = torch.mm(dy2.t(), x2)
-            dw = dw.to(ctx.wdtype)
+                dw = _ext.ops().gemm_wgrad(dy2, x2, None, False) if native else torch.mm(dy2.t(), x2)
+                dw = grad_accum.defer(p, dw.to(ctx.wdtype))
         return (dx.view(ctx.xshape) if dx is not None else None), dw, None
 
 

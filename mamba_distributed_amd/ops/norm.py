@@ -15,7 +15,7 @@ from typing import Optional
 import torch
 import torch.nn as nn
 
-from . import _ext
+from . import _ext, grad_accum
 from .reference import add_rms_norm_ref, gated_rms_norm_ref
 
 
@@ -41,6 +41,7 @@ class _AddRMSNormFn(torch.autograd.Function):
         out_dtype = out_dtype or x.dtype
         y, res_out, rstd = _ext.ops().add_rmsnorm_fwd(x2, r2, weight, eps, out_dtype, res_dtype)
         ctx.save_for_backward(res_out, weight, rstd)
+        ctx.param = weight
         ctx.x_dtype = x.dtype
         ctx.res_dtype = residual.dtype if residual is not None else None
         ctx.has_residual = residual is not None
@@ -67,7 +68,7 @@ class _AddRMSNormFn(torch.autograd.Function):
         dresidual = None
         if want_res:
             dresidual = (dres if res_dtype != ctx.x_dtype else dx).view(shape)
-        return dx, dw, dresidual, None, None, None, None
+        return dx, grad_accum.defer(ctx.param, dw), dresidual, None, None, None, None
 
 
 def rms_norm_fn(x, weight, bias=None, residual=None, prenorm=False, residual_in_fp32=False,
@@ -104,6 +105,7 @@ class _GatedRMSNormFn(torch.autograd.Function):
         x2, z2 = _rows(x), _rows(z)
         y, rstd = _ext.ops().gated_rmsnorm_fwd(x2, z2, weight, eps, group_size, norm_before_gate)
         ctx.save_for_backward(x2, z2, weight, rstd)
+        ctx.param = weight
         ctx.eps, ctx.group_size, ctx.nbg = eps, group_size, norm_before_gate
         ctx.shape = shape
         return y.view(shape)
@@ -113,7 +115,7 @@ class _GatedRMSNormFn(torch.autograd.Function):
         x2, z2, weight, rstd = ctx.saved_tensors
         dx, dz, dw = _ext.ops().gated_rmsnorm_bwd(_rows(dy), x2, z2, weight, rstd, ctx.group_size,
                                                   ctx.nbg, None, None)
-        return dx.view(ctx.shape), dz.view(ctx.shape), dw, None, None, None
+        return dx.view(ctx.shape), dz.view(ctx.shape), grad_accum.defer(ctx.param, dw), None, None, None
 
 
 def rmsnorm_gated_fn(x, z, weight, eps=1e-5, group_size=None, norm_before_gate=False):

@@ -21,7 +21,7 @@ from typing import Optional
 import torch
 import torch.nn.functional as F
 
-from . import _ext
+from . import _ext, grad_accum
 from .conv1d import causal_conv1d_fn
 from .reference import selective_scan_ref
 
@@ -33,6 +33,7 @@ class _SelectiveScanFn(torch.autograd.Function):
         out, carries, last = ops.selscan_fwd(u, delta, A, B, C, D, z, delta_bias, delta_softplus)
         ctx.save_for_backward(u, delta, A, B, C, D, z, delta_bias, carries)
         ctx.softplus = delta_softplus
+        ctx.params = (A, D, delta_bias)
         if return_last_state:
             return out, last
         return out
@@ -43,10 +44,12 @@ class _SelectiveScanFn(torch.autograd.Function):
         ops = _ext.ops()
         du, ddelta, dA, dB, dC, dD, dz, ddelta_bias = ops.selscan_bwd(
             dout, u, delta, A, B, C, D, z, delta_bias, carries, ctx.softplus)
-        return (du, ddelta, dA, dB.to(B.dtype), dC.to(C.dtype),
-                dD if D is not None else None,
+        pA, pD, pdb = ctx.params
+        d = grad_accum.defer
+        return (du, ddelta, d(pA, dA), dB.to(B.dtype), dC.to(C.dtype),
+                d(pD, dD) if D is not None else None,
                 dz if z is not None else None,
-                ddelta_bias if delta_bias is not None else None, None, None)
+                d(pdb, ddelta_bias) if delta_bias is not None else None, None, None)
 
 
 def selective_scan_fn(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_softplus=False,

@@ -22,7 +22,7 @@ from typing import Optional
 import torch
 import torch.nn.functional as F
 
-from . import _ext
+from . import _ext, grad_accum
 from .reference import ssd_chunked_ref, gated_rms_norm_ref, causal_conv1d_ref
 
 _INF = float("inf")
@@ -42,6 +42,7 @@ class _SSDFn(torch.autograd.Function):
         ctx.save_for_backward(x, dt, A, B, C, D, dt_bias, initial_states, cum, dtp, states)
         ctx.flags = (dt_softplus, dt_min, dt_max)
         ctx.return_final = return_final_states
+        ctx.params = (A, D, dt_bias)
         if return_final_states:
             return y, final
         return y
@@ -54,9 +55,11 @@ class _SSDFn(torch.autograd.Function):
         g = _ext.ops().ssd_bwd(dy.contiguous(), x, dt, A, B, C, D, dt_bias, init, cum, dtp, states,
                                dfinal, NATIVE_CHUNK, softplus, dt_min, dt_max, None, None, None, None)
         dx, ddt, dA, dB, dC, dD, ddt_bias, dinit = g
-        return (dx, ddt, dA, dB, dC,
-                dD if D is not None else None,
-                ddt_bias if dt_bias is not None else None,
+        pA, pD, pdtb = ctx.params
+        d = grad_accum.defer
+        return (dx, ddt, d(pA, dA), dB, dC,
+                d(pD, dD) if D is not None else None,
+                d(pdtb, ddt_bias) if dt_bias is not None else None,
                 dinit if init is not None else None,
                 None, None, None, None)
 
@@ -108,6 +111,7 @@ class _Mamba2InnerFn(torch.autograd.Function):
         ctx.save_for_backward(zxbcdt, w2, conv_b, dt_bias, A, D, norm_w, xBC_c, y, rstd, cum, dtp, states)
         ctx.meta = (eps, headdim, ngroups, d_state, dt_min, dt_max, norm_before_gate, A_is_log)
         ctx.wshape = conv_w.shape
+        ctx.params = (conv_w, conv_b, dt_bias, A, D, norm_w)
         return yn.view(b, l, di)
 
     @staticmethod
@@ -140,8 +144,11 @@ class _Mamba2InnerFn(torch.autograd.Function):
         _, _, dA, _, _, dD, ddt_bias, _ = g
         xBC = zxbcdt[..., di:di + conv_dim]
         _, dw, db = ops.conv1d_cl_bwd(xBC, w2, conv_b, dxBC_c, True, dz_all[..., di:di + conv_dim])
-        return (dz_all, dw.reshape(ctx.wshape).to(w2.dtype), db.to(conv_b.dtype) if conv_b is not None else None,
-                ddt_bias, dA, dD, dnorm_w, None, None, None, None, None, None, None, None)
+        pw, pb, pdtb, pA, pD, pn = ctx.params
+        d = grad_accum.defer
+        return (dz_all, d(pw, dw.reshape(ctx.wshape).to(w2.dtype)),
+                d(pb, db.to(conv_b.dtype)) if conv_b is not None else None,
+                d(pdtb, ddt_bias), d(pA, dA), d(pD, dD), d(pn, dnorm_w), None, None, None, None, None, None, None, None)
 
 
 def mamba2_inner_ref(zxbcdt, conv_w, conv_b, dt_bias, A, D, norm_w, eps, headdim, ngroups, d_state,

@@ -48,6 +48,10 @@ def unwrap(model):
 
 
 def set_grad_sync(model, enabled: bool):
+    """Per micro-step: True only on the last one (reference train.py:209-210).  Also tells the native
+    ops whether they may accumulate parameter gradients in place (ops/grad_accum.py)."""
+    from ..ops import grad_accum
+    grad_accum.set_direct(not enabled)
     if isinstance(model, DDP):
         model.require_backward_grad_sync = enabled
 

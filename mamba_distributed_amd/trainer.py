@@ -32,6 +32,7 @@ import torch.nn.functional as F
 
 from .config import MambaConfig, preset
 from .data.loader import DataLoaderLite, SyntheticTokens
+from .ops import grad_accum
 from .lm import LMHeadModel
 from .parallel import ddp as ddp_mod
 from .parallel.dist import all_gather_object, all_reduce_avg, destroy, init_distributed
@@ -206,14 +207,15 @@ class Trainer:
         self.model.train()
         self.optimizer.zero_grad(set_to_none=True)
         loss_accum = torch.zeros((), device=self.device)
-        for micro_step in range(self.grad_accum_steps):
-            x, y = self._batch(self.train_loader)
-            ddp_mod.set_grad_sync(self.model, micro_step == self.grad_accum_steps - 1)
-            with self._autocast():
-                _, loss = self.model(x, y, return_logits=not self.a.fused_ce)
-            loss = loss / self.grad_accum_steps
-            loss_accum += loss.detach().float()
-            loss.backward()
+        with grad_accum.accumulation_scope():  # weights are frozen until optimizer.step()
+            for micro_step in range(self.grad_accum_steps):
+                x, y = self._batch(self.train_loader)
+                ddp_mod.set_grad_sync(self.model, micro_step == self.grad_accum_steps - 1)
+                with self._autocast():
+                    _, loss = self.model(x, y, return_logits=not self.a.fused_ce)
+                loss = loss / self.grad_accum_steps
+                loss_accum += loss.detach().float()
+                loss.backward()
         all_reduce_avg(loss_accum)
         norm = torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.a.grad_clip)
         lr = self.lr(step)

@@ -397,3 +397,34 @@ def test_gemm_wgrad(cuda, M, P, Q):
     assert rel(acc, ref + 1) < 1e-4
     C2 = ops.gemm_wgrad(dY, X, None, False)
     assert torch.equal(C, C2)  # deterministic
+
+
+@pytest.mark.parametrize("layer", ["Mamba1", "Mamba2"])
+def test_in_place_grad_accumulation_matches_autograd(cuda, layer):
+    """accumulation_scope (in-place split-K wgrad accumulation + one batched add for the small
+    parameter grads on no-sync micro-steps) == plain autograd accumulation over 3 micro-batches."""
+    from mamba_distributed_amd import LMHeadModel, MambaConfig
+    from mamba_distributed_amd.ops import grad_accum
+    from mamba_distributed_amd.parallel import ddp as ddp_mod
+    torch.manual_seed(0)
+    cfg = MambaConfig(d_model=256, n_layer=2, vocab_size=1024, ssm_cfg={"layer": layer})
+    m = LMHeadModel(cfg, device=cuda)
+    batches = [torch.randint(0, 1024, (2, 160), device=cuda) for _ in range(3)]
+
+    def run(scoped):
+        m.zero_grad(set_to_none=True)
+        ctx = grad_accum.accumulation_scope() if scoped else torch.autograd.set_grad_enabled(True)
+        with ctx:
+            for i, ids in enumerate(batches):
+                ddp_mod.set_grad_sync(m, i == len(batches) - 1)
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    _, loss = m(ids[:, :-1].contiguous(), ids[:, 1:].contiguous(), return_logits=False)
+                (loss / 3).backward()
+        return {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
+
+    ref = run(False)
+    got = run(True)
+    assert ref.keys() == got.keys()
+    for n in ref:
+        assert rel(got[n], ref[n]) < 1e-5, (n, rel(got[n], ref[n]))
+    assert not grad_accum.in_scope() and not grad_accum.direct()
