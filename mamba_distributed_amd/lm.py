@@ -47,17 +47,31 @@ class LMHeadModel(MambaLMHeadModel):
 
     def forward(self, input_ids, targets=None, position_ids=None, inference_params=None,
                 num_last_tokens=0, return_logits=True, **mixer_kwargs):
+        par = getattr(self, "parallel", None)
+        if par is not None and targets is not None:
+            from .parallel.api import shard_batch
+            targets = shard_batch(self, targets)
         if targets is not None and not return_logits:
             h = self.backbone(input_ids, inference_params=inference_params, **mixer_kwargs)
             cd = torch.get_autocast_dtype("cuda") if (h.is_cuda and torch.is_autocast_enabled("cuda")) else h.dtype
             loss = fused_linear_cross_entropy(h, self.lm_head.weight, targets, compute_dtype=cd)
-            return None, loss
+            return None, self._parallel_loss(loss)
         logits = super().forward(input_ids, position_ids=position_ids, inference_params=inference_params,
                                  num_last_tokens=num_last_tokens, **mixer_kwargs).logits
         loss = None
         if targets is not None:
-            loss = cross_entropy(logits.reshape(-1, logits.size(-1)), targets.reshape(-1))
+            loss = self._parallel_loss(cross_entropy(logits.reshape(-1, logits.size(-1)), targets.reshape(-1)))
         return logits, loss
+
+    def _parallel_loss(self, loss):
+        """Sequence parallelism: every TP rank holds 1/tp of the tokens; return the TP-group mean
+        (forward all-reduce, identity backward -> each rank back-propagates its own mean / tp).
+        Context parallelism keeps the rank-local mean (DDP over DP x CP averages the gradients)."""
+        par = getattr(self, "parallel", None)
+        if par is None or not par.sequence_parallel:
+            return loss
+        from .parallel.comm import reduce_from_group
+        return reduce_from_group(loss, par.tp_group) / par.tp
 
     # ------------------------------------------------------------------------------------
     def top_k_sampling(self, logits: torch.Tensor, k: int = 50, seed: Optional[int] = 42,

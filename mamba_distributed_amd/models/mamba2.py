@@ -35,7 +35,7 @@ class Mamba2(nn.Module):
                  device=None, dtype=None):
         factory = {"device": device, "dtype": dtype}
         super().__init__()
-        assert process_group is None, "use parallel.tensor_parallel.Mamba2TP for head-sharded TP"
+        assert process_group is None, "head-sharded TP: parallel.tensor_parallel.Mamba2TP.from_full / parallel.parallelize"
         assert not D_has_hdim, "D_has_hdim is not supported"
         assert rmsnorm, "the gated RMSNorm output path is the only supported one"
         self.d_model = d_model
@@ -58,6 +58,7 @@ class Mamba2(nn.Module):
         self.chunk_size = chunk_size
         self.use_mem_eff_path = use_mem_eff_path
         self.layer_idx = layer_idx
+        self.cp_group = None  # context parallelism (parallel/api.py::parallelize sets it)
 
         d_in_proj = 2 * self.d_inner + 2 * ngroups * d_state + self.nheads
         self.in_proj = nn.Linear(d_model, d_in_proj, bias=bias, **factory)
@@ -93,7 +94,12 @@ class Mamba2(nn.Module):
                 out, _, _ = self.step(u, conv_state, ssm_state)
                 return out
         zxbcdt = linear(u, self.in_proj)
-        if conv_state is None:
+        if self.cp_group is not None and conv_state is None:
+            from ..parallel.context_parallel import mamba2_inner_parallel
+            y = mamba2_inner_parallel(zxbcdt, self.conv1d.weight, self.conv1d.bias, self.dt_bias, self.A_log,
+                                      self.D, self.norm.weight, self.norm.eps, self.headdim, self.ngroups,
+                                      self.d_state, self.dt_limit, self.cp_group, None, min(64, self.chunk_size))
+        elif conv_state is None:
             y = mamba2_inner_fn(zxbcdt, self.conv1d.weight, self.conv1d.bias, self.dt_bias, self.A_log, self.D,
                                 self.norm.weight, self.norm.eps, self.headdim, self.ngroups, self.d_state,
                                 self.dt_limit, self.norm_before_gate, ref_chunk_size=min(64, self.chunk_size),

@@ -152,6 +152,12 @@ class MixerModel(nn.Module):
                 for i, layer in enumerate(self.layers)}
 
     def forward(self, input_ids, inference_params=None, **mixer_kwargs):
+        ctx = getattr(self, "parallel", None)
+        if ctx is not None and inference_params is None:
+            # context / sequence parallelism (parallel/api.py): compute on this rank's token shard
+            from ..parallel.api import shard_batch
+            mixer_kwargs = dict(mixer_kwargs, seqlen=input_ids.shape[1] // max(1, ctx.cp))
+            input_ids = shard_batch(self, input_ids)
         hidden_states = self.embedding(input_ids)
         residual = None
         for layer in self.layers:

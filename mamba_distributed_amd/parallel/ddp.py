@@ -27,19 +27,22 @@ from .dist import DistInfo
 
 def wrap_ddp(model: torch.nn.Module, info: DistInfo, bucket_cap_mb: float = 100.0,
              grad_comm_dtype: str = "fp32", static_graph: bool = False,
-             gradient_as_bucket_view: bool = True):
+             gradient_as_bucket_view: bool = True, process_group=None):
+    """DDP over ``process_group`` (default: WORLD; the DP x CP group under tensor / context
+    parallelism, parallel/groups.py)."""
     if not info.ddp:
         return model
     device_ids = [info.local_rank] if info.device.startswith("cuda") else None
     m = DDP(model, device_ids=device_ids, bucket_cap_mb=bucket_cap_mb,
             gradient_as_bucket_view=gradient_as_bucket_view, static_graph=static_graph,
-            broadcast_buffers=False)
+            broadcast_buffers=False, process_group=process_group)
+    hook_group = process_group if process_group is not None else dist.group.WORLD
     if grad_comm_dtype == "bf16":
         from torch.distributed.algorithms.ddp_comm_hooks import default_hooks
-        m.register_comm_hook(dist.group.WORLD, default_hooks.bf16_compress_hook)
+        m.register_comm_hook(hook_group, default_hooks.bf16_compress_hook)
     elif grad_comm_dtype == "fp16":
         from torch.distributed.algorithms.ddp_comm_hooks import default_hooks
-        m.register_comm_hook(dist.group.WORLD, default_hooks.fp16_compress_hook)
+        m.register_comm_hook(hook_group, default_hooks.fp16_compress_hook)
     return m
 
 

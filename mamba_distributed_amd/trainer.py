@@ -35,7 +35,10 @@ from .data.loader import DataLoaderLite, SyntheticTokens
 from .ops import grad_accum
 from .lm import LMHeadModel
 from .parallel import ddp as ddp_mod
+from .parallel.api import clip_grad_norm_ as par_clip_grad_norm_
+from .parallel.api import full_state_dict, parallelize, sync_tp_grads
 from .parallel.dist import all_gather_object, all_reduce_avg, destroy, init_distributed
+from .parallel.groups import init_parallel_groups
 from .utils.checkpoint import latest_checkpoint, load_checkpoint, save_checkpoint, set_rng_state
 from .utils.lr import get_lr
 
@@ -74,6 +77,9 @@ class TrainArgs:
     sample_prompt: str = "Hello, I'm a language model,"
     device_type: str = "auto"
     tuned_gemms: bool = True             # replay the shipped gfx950 GEMM solution table
+    tp: int = 1                          # tensor parallel degree (Mamba-2 heads; parallel/tensor_parallel.py)
+    cp: int = 1                          # context parallel degree (sequence shards; parallel/context_parallel.py)
+    sequence_parallel: bool = False      # with tp > 1: shard the residual stream over tokens as well
 
 
 def build_config(a: TrainArgs) -> MambaConfig:
@@ -97,7 +103,10 @@ class Trainer:
         torch.manual_seed(a.seed)
         if torch.cuda.is_available():
             torch.cuda.manual_seed(a.seed)
-        world = self.info.world_size
+        self.groups = init_parallel_groups(a.tp, a.cp)
+        # ranks of one TP x CP group consume the same batch: the data-parallel world is dp
+        world, data_rank = self.groups.dp, self.groups.dp_rank
+        self.data_world = world
         assert a.total_batch_size % (a.B * a.T * world) == 0, \
             "make sure total_batch_size is divisible by B * T * ddp_world_size"
         self.grad_accum_steps = a.total_batch_size // (a.B * a.T * world)
@@ -106,13 +115,13 @@ class Trainer:
             print(f"=> calculated gradient accumulation steps: {self.grad_accum_steps}")
         self.config = build_config(a)
         if a.synthetic:
-            self.train_loader = SyntheticTokens(a.B, a.T, self.config.vocab_size, self.info.rank, world,
+            self.train_loader = SyntheticTokens(a.B, a.T, self.config.vocab_size, data_rank, world,
                                                 device=self.device, seed=a.seed)
-            self.val_loader = SyntheticTokens(a.B, a.T, self.config.vocab_size, self.info.rank, world,
+            self.val_loader = SyntheticTokens(a.B, a.T, self.config.vocab_size, data_rank, world,
                                               device=self.device, seed=a.seed + 1)
         else:
-            self.train_loader = DataLoaderLite(a.B, a.T, self.info.rank, world, "train", self.master, a.data_root)
-            self.val_loader = DataLoaderLite(a.B, a.T, self.info.rank, world, "val", self.master, a.data_root)
+            self.train_loader = DataLoaderLite(a.B, a.T, data_rank, world, "train", self.master, a.data_root)
+            self.val_loader = DataLoaderLite(a.B, a.T, data_rank, world, "val", self.master, a.data_root)
         if self.device_type == "cuda":
             torch.set_float32_matmul_precision("high")
             if a.tuned_gemms:
@@ -123,14 +132,23 @@ class Trainer:
         if self.master:
             total = int(sum(p.numel() for p in self.raw_model.parameters()) // 1e6)
             print(f"Total number of parameters: {total}M")
-        self.model = ddp_mod.wrap_ddp(self.raw_model, self.info, a.bucket_cap_mb, a.grad_comm_dtype)
-        self.optimizer = self.raw_model.configure_optimizers(a.weight_decay, a.max_lr, self.device_type, self.master)
         os.makedirs(a.log_dir, exist_ok=True)
         self.log_file = os.path.join(a.log_dir, "log.txt")
         self.start_step = 0
         self.resumed_at = None
-        if a.resume:
-            self._resume()
+        ck = self._load_model_checkpoint() if a.resume else None   # full layout: before sharding
+        self.parallel = a.tp > 1 or a.cp > 1
+        if self.parallel:
+            parallelize(self.raw_model, self.groups, a.sequence_parallel)
+            grp = self.groups.dp_cp_group
+            ddp_info = self.info if self.groups.dp * self.groups.cp > 1 else None
+            self.model = (ddp_mod.wrap_ddp(self.raw_model, ddp_info, a.bucket_cap_mb, a.grad_comm_dtype,
+                                           process_group=grp) if ddp_info is not None else self.raw_model)
+        else:
+            self.model = ddp_mod.wrap_ddp(self.raw_model, self.info, a.bucket_cap_mb, a.grad_comm_dtype)
+        self.optimizer = self.raw_model.configure_optimizers(a.weight_decay, a.max_lr, self.device_type, self.master)
+        if ck is not None:
+            self._resume_rest(ck)
         if self.master and self.start_step == 0:
             with open(self.log_file, "w"):
                 pass
@@ -149,19 +167,27 @@ class Trainer:
         x, y = loader.next_batch()
         return x.to(self.device, non_blocking=True), y.to(self.device, non_blocking=True)
 
-    def _resume(self):
+    def _load_model_checkpoint(self):
         path = latest_checkpoint(self.a.log_dir)
         if path is None:
-            return
+            return None
         ck = load_checkpoint(path, map_location=self.device)
         self.raw_model.load_state_dict(ck["model"])
-        if "optimizer" in ck:
+        ck["_path"] = path
+        return ck
+
+    def _resume_rest(self, ck):
+        path = ck["_path"]
+        if "optimizer" in ck and self.a.tp == 1:
             self.optimizer.load_state_dict(ck["optimizer"])
+        elif "optimizer" in ck and self.master:
+            print("note: tensor-parallel resume restarts the AdamW moments (checkpoints hold the full layout)")
         if "loader" in ck and hasattr(self.train_loader, "load_state_dict"):
             loaders = ck["loader"]
             if isinstance(loaders, list) and len(loaders) != self.info.world_size and self.master:
                 print(f"warning: checkpoint has {len(loaders)} loader states for world size {self.info.world_size}")
-            st = loaders[self.info.rank] if isinstance(loaders, list) and self.info.rank < len(loaders) else None
+            r = self.info.rank
+            st = loaders[r] if isinstance(loaders, list) and r < len(loaders) else None
             if st is not None:
                 self.train_loader.load_state_dict(st)
         if "rng" in ck:
@@ -188,6 +214,8 @@ class Trainer:
 
     @torch.no_grad()
     def sample(self, num_return_sequences=4, max_length=32):
+        if self.a.cp > 1 or self.a.sequence_parallel:
+            return  # the sharded forward needs full-length, divisible sequences
         self.model.eval()
         tokens = torch.tensor(self.enc.encode(self.a.sample_prompt), dtype=torch.long)
         xgen = tokens.unsqueeze(0).repeat(num_return_sequences, 1).to(self.device)
@@ -217,7 +245,11 @@ class Trainer:
                 loss_accum += loss.detach().float()
                 loss.backward()
         all_reduce_avg(loss_accum)
-        norm = torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.a.grad_clip)
+        if self.parallel:
+            sync_tp_grads(self.model, self.groups)
+            norm = par_clip_grad_norm_(self.model, self.a.grad_clip, self.groups)
+        else:
+            norm = torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.a.grad_clip)
         lr = self.lr(step)
         for g in self.optimizer.param_groups:
             g["lr"] = lr
@@ -228,12 +260,14 @@ class Trainer:
         """Collective (every rank calls it): gathers all ranks' loader positions, rank 0 writes."""
         st = self.train_loader.state_dict() if hasattr(self.train_loader, "state_dict") else None
         loader_states = all_gather_object(st)
+        full_sd = full_state_dict(self.raw_model) if self.a.tp > 1 else None   # collective over TP
         if not self.master:
             return None
         path = os.path.join(self.a.log_dir, f"model_{step:05d}.pt")
-        opt = self.optimizer if self.a.save_optimizer else None
+        opt = self.optimizer if (self.a.save_optimizer and self.a.tp == 1) else None
         save_checkpoint(path, self.raw_model, step, val_loss, optimizer=opt,
-                        loader_state=loader_states if st is not None else None, include_rng=True)
+                        loader_state=loader_states if st is not None else None, include_rng=True,
+                        model_state=full_sd)
         return path
 
     def _maybe_inject_fault(self, step):
@@ -270,7 +304,7 @@ class Trainer:
             if self.device_type == "cuda":
                 torch.cuda.synchronize()
             dt = time.time() - t0
-            tokens_processed = a.B * a.T * self.grad_accum_steps * self.info.world_size
+            tokens_processed = a.B * a.T * self.grad_accum_steps * self.data_world
             tps = tokens_processed / dt
             if not eval_step:
                 self.step_times.append(dt)
@@ -288,7 +322,7 @@ class Trainer:
             ts = sorted(self.step_times[1:] or self.step_times)
             med = ts[len(ts) // 2]
             print(f"steady-state median step {med*1000:.1f} ms, "
-                  f"{a.B * a.T * self.grad_accum_steps * self.info.world_size / med:.1f} tok/s "
+                  f"{a.B * a.T * self.grad_accum_steps * self.data_world / med:.1f} tok/s "
                   f"(excluding eval/sample steps)")
         if metrics:
             metrics.close()

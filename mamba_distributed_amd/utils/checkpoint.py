@@ -36,9 +36,12 @@ def set_rng_state(st):
 
 
 def save_checkpoint(path: str, model, step: int, val_loss: Optional[float] = None, optimizer=None,
-                    loader_state=None, extra=None, include_rng: bool = False):
+                    loader_state=None, extra=None, include_rng: bool = False, model_state=None):
+    """``model_state``: an explicit state dict (e.g. the reassembled full layout of a tensor-parallel
+    model, parallel/api.py::full_state_dict); default ``model.state_dict()``."""
     cfg = model.config.to_dict() if hasattr(model.config, "to_dict") else dict(model.config)
-    ckpt = {"model": model.state_dict(), "config": cfg, "step": step, "val_loss": val_loss}
+    sd = model_state if model_state is not None else model.state_dict()
+    ckpt = {"model": sd, "config": cfg, "step": step, "val_loss": val_loss}
     if optimizer is not None:
         ckpt["optimizer"] = optimizer.state_dict()
     if loader_state is not None:

@@ -428,3 +428,59 @@ def test_in_place_grad_accumulation_matches_autograd(cuda, layer):
     for n in ref:
         assert rel(got[n], ref[n]) < 1e-5, (n, rel(got[n], ref[n]))
     assert not grad_accum.in_scope() and not grad_accum.direct()
+
+
+def test_context_parallel_split_matches_full_sequence(cuda):
+    """The CP state hand-off (parallel/context_parallel.py) with the native SSD: scanning two halves from
+    zero and folding the first half's final state into the second (ssd_state_correction) equals the
+    native/reference scan of the whole sequence, forward and backward."""
+    from mamba_distributed_amd.ops.reference import ssd_dt_transform
+    from mamba_distributed_amd.ops.ssd import mamba_chunk_scan_combined
+    from mamba_distributed_amd.parallel.context_parallel import ssd_state_correction
+    x, dt, A, Bm, Cm, D, dt_bias = _ssd_inputs(cuda, 2, 256, 8, 1, 128, seed=11)
+    h = 128
+
+    def split(x, dt, Bm, Cm):
+        y1, s1 = mamba_chunk_scan_combined(x[:, :h], dt[:, :h], A, Bm[:, :h], Cm[:, :h], 64, D=D,
+                                           dt_bias=dt_bias, dt_softplus=True, return_final_states=True)
+        y2, _ = mamba_chunk_scan_combined(x[:, h:], dt[:, h:], A, Bm[:, h:], Cm[:, h:], 64, D=D,
+                                          dt_bias=dt_bias, dt_softplus=True, return_final_states=True)
+        cum2 = torch.cumsum(ssd_dt_transform(dt[:, h:], dt_bias) * A.float(), dim=1)
+        y2 = ssd_state_correction(y2, cum2, Cm[:, h:], s1).to(y1.dtype)
+        return torch.cat([y1, y2], 1)
+
+    def full(x, dt, Bm, Cm):
+        return mamba_chunk_scan_combined(x, dt, A, Bm, Cm, 64, D=D, dt_bias=dt_bias, dt_softplus=True)
+
+    on, orf, gn, gr = run_both(split, full, [x, dt, Bm, Cm])
+    assert rel(on, orf) < 2e-2, rel(on, orf)
+    for nm, a, b_ in zip(["x", "dt", "B", "C"], gn, gr):
+        assert rel(a, b_) < 3e-2, (nm, rel(a, b_))
+
+
+def test_unfused_parallel_inner_matches_fused(cuda):
+    """parallel.context_parallel.mamba2_inner_parallel (native conv1d / SSD / gated norm, unfused; the TP
+    and CP building block) == the fused native mamba2_inner_fn, forward and backward."""
+    from mamba_distributed_amd.ops.ssd import mamba2_inner_fn
+    from mamba_distributed_amd.parallel.context_parallel import mamba2_inner_parallel
+    torch.manual_seed(5)
+    b, L, H, P, N, G = 2, 256, 8, 64, 128, 1
+    di = H * P
+    zx = torch.randn(b, L, 2 * di + 2 * G * N + H, device=cuda).to(torch.bfloat16)
+    conv_w = torch.randn(di + 2 * G * N, 1, 4, device=cuda) * 0.3
+    conv_b = torch.randn(di + 2 * G * N, device=cuda) * 0.1
+    dt_bias = torch.randn(H, device=cuda) * 0.3
+    A_log = torch.log(torch.rand(H, device=cuda) * 8 + 0.5)
+    D = torch.randn(H, device=cuda)
+    nw = torch.rand(di, device=cuda) + 0.5
+    inputs = [zx, conv_w, conv_b, dt_bias, A_log, D, nw]
+    xa = [leaf(t) for t in inputs]
+    xb = [leaf(t) for t in inputs]
+    ya = mamba2_inner_parallel(*xa, 1e-5, P, G, N)
+    yb = mamba2_inner_fn(*xb, 1e-5, P, G, N, A_is_log=True)
+    assert rel(ya, yb) < 1e-2, rel(ya, yb)
+    go = torch.randn_like(yb.float()).to(yb.dtype)
+    ya.backward(go)
+    yb.backward(go)
+    for i, (a, b_) in enumerate(zip(xa, xb)):
+        assert rel(a.grad, b_.grad) < 2e-2, (i, rel(a.grad, b_.grad))
