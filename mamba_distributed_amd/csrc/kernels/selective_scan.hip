@@ -214,7 +214,7 @@ template <typename T, int N, bool VEC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void selscan_bwd_k(SelScanArgs a) {
   constexpr int NW = N >= SB_W ? N / SB_W : 1;
   constexpr int IT = SB_IT;
-  __shared__ float part[SB_W][3][SB_T];
+  __shared__ __attribute__((aligned(16))) float part[2][SB_W][3][SB_T];  // double-buffered per channel
   __shared__ __attribute__((aligned(16))) bf16_t BCs[2][N][SB_T];  // this tile's B, C (group of d0), bf16 as in HBM
   __shared__ float lamc[SB_KC][N];
   __shared__ float dAacc[SB_KC][N];
@@ -254,6 +254,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void s
     __syncthreads();
     // next channel's rows, fetched while the current one is processed (VEC path)
     uint2 nu = make_uint2(0, 0), nd = nu, ng = nu, nz = nu;
+    float4 nh = make_float4(0.f, 0.f, 0.f, 0.f);  // next channel's tile-start states (NW == 4)
     auto fetch = [&](int k) {
       if constexpr (VEC) {
         if (k < nch && tl < a.L) {
@@ -263,6 +264,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void s
           ng = *reinterpret_cast<const uint2*>(((const bf16_t*)a.dout_) + (int64_t)b * a.sgb + (int64_t)d * a.sgd + tl);
           if (a.z_) nz = *reinterpret_cast<const uint2*>(((const bf16_t*)a.z_) + (int64_t)b * a.szb + (int64_t)d * a.szd + tl);
         }
+        if (NW == 4 && k < nch)
+          nh = *reinterpret_cast<const float4*>(a.carries + (((int64_t)b * a.D + d0 + k) * ntl + tile) * N + w * NW);
       }
     };
     if (has_states) fetch(0);
@@ -274,6 +277,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void s
       const T* grow = ((const T*)a.dout_) + (int64_t)b * a.sgb + (int64_t)d * a.sgd;
       const T* zrow = a.z_ ? ((const T*)a.z_) + (int64_t)b * a.szb + (int64_t)d * a.szd : nullptr;
       const float bias = a.delta_bias ? a.delta_bias[d] : 0.f;
+      const int buf = k & 1;
+      uint2 craw = make_uint2(0, 0), cg = craw, cz = craw;  // this channel's raw delta / dout / z (VEC)
+      float hcv[4];
+      float uf[IT], dlf[IT];
       if (has_states) {
         const T* Bb = ((const T*)a.Bm_) + (int64_t)b * a.sBb + (int64_t)g * a.sBg;
         const T* Cb = ((const T*)a.Cm_) + (int64_t)b * a.sCb + (int64_t)g * a.sCg;
@@ -284,6 +291,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void s
             o[2] = __uint_as_float(v.y << 16); o[3] = __uint_as_float(v.y & 0xffff0000u);
           };
           unpack4(nu, u); unpack4(nd, dl); unpack4(ng, dy); unpack4(nz, zz);
+          craw = nd; cg = ng; cz = nz;
+          hcv[0] = nh.x; hcv[1] = nh.y; hcv[2] = nh.z; hcv[3] = nh.w;
           fetch(k + 1);
         } else {
           load_items<VEC, T, IT>(urow, tl, a.L, u);
@@ -331,8 +340,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void s
             cb = fmaf(av[i], cb, dl[i] * u[i] * Bv[i]);
             ca *= av[i];
           }
+          const float prod = ca;  // the lane's decay product also seeds the adjoint composition
           scan_prefix(ca, cb);
-          const float hc0 = a.carries[(((int64_t)b * a.D + d) * ntl + tile) * N + n];
+          const float hc0 = (VEC && NW == 4) ? hcv[0] : a.carries[(((int64_t)b * a.D + d) * ntl + tile) * N + n];
+          if constexpr (VEC && NW == 4) {  // rotate like the accumulators: the live one is slot 0
+            const float t0_ = hcv[0];
+            hcv[0] = hcv[1]; hcv[1] = hcv[2]; hcv[2] = hcv[3]; hcv[3] = t0_;
+          }
           const float hend = fmaf(ca, hc0, cb);
           float h = dppf<0x138>(hc0, hend);
 #pragma unroll
@@ -342,11 +356,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void s
             yv[i] = fmaf(Cv[i], h, yv[i]);
           }
           // adjoint: x_t = av_t (dy_t C_t + x_{t+1}),  lambda_t = dy_t C_t + x_{t+1}
-          float ma = 1.f, mb = 0.f;
+          float ma = prod, mb = 0.f;
 #pragma unroll
           for (int i = IT - 1; i >= 0; --i) {
             mb = av[i] * fmaf(dy[i], Cv[i], mb);
-            ma *= av[i];
           }
           scan_suffix(ma, mb);
           const float xc = lamc[k][n];
@@ -385,50 +398,118 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void s
         }
 #pragma unroll
         for (int i = 0; i < IT; ++i) {
-          part[w][0][lane * IT + i] = du[i] * dl[i];
-          part[w][1][lane * IT + i] = dd[i];
-          part[w][2][lane * IT + i] = yv[i];
+          uf[i] = u[i];
+          dlf[i] = dl[i];
+        }
+        if constexpr (VEC) {
+          *reinterpret_cast<float4*>(&part[buf][w][0][lane * IT]) = make_float4(du[0], du[1], du[2], du[3]);
+          *reinterpret_cast<float4*>(&part[buf][w][1][lane * IT]) = make_float4(dd[0], dd[1], dd[2], dd[3]);
+          *reinterpret_cast<float4*>(&part[buf][w][2][lane * IT]) = make_float4(yv[0], yv[1], yv[2], yv[3]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < IT; ++i) {
+            part[buf][w][0][lane * IT + i] = du[i] * dl[i];
+            part[buf][w][1][lane * IT + i] = dd[i];
+            part[buf][w][2][lane * IT + i] = yv[i];
+          }
         }
       } else {
 #pragma unroll
-        for (int i = 0; i < IT; ++i) part[w][0][lane * IT + i] = part[w][1][lane * IT + i] = part[w][2][lane * IT + i] = 0.f;
+        for (int i = 0; i < IT; ++i)
+          part[buf][w][0][lane * IT + i] = part[buf][w][1][lane * IT + i] = part[buf][w][2][lane * IT + i] = 0.f;
       }
       __syncthreads();
-      // finish item-parallel: thread j <-> step tile*SB_T + j
-      float dDp = 0.f, dbp = 0.f;
-      if (threadIdx.x < SB_T) {
-        const int j = threadIdx.x, t = tile * SB_T + j;
-        if (t < a.L) {
-          float sdu = 0.f, sdd = 0.f, sy = 0.f;
+      if constexpr (VEC) {
+        // one wave (rotating with the channel) finishes the channel from its registers: the other waves
+        // go straight on to the next channel (part[] is double-buffered, so the next channel's barrier
+        // orders this wave's reads before the buffer is rewritten two channels later)
+        if (w == (k & (SB_W - 1)) && has_states) {
+          float s1[IT], sdd[IT], sy[IT];
 #pragma unroll
-          for (int v = 0; v < SB_W; ++v) {
-            sdu += part[v][0][j];
-            sdd += part[v][1][j];
-            sy += part[v][2][j];
+          for (int q = 0; q < 3; ++q) {
+            float4 acc4 = *reinterpret_cast<const float4*>(&part[buf][0][q][lane * IT]);
+#pragma unroll
+            for (int v = 1; v < SB_W; ++v) {
+              const float4 o = *reinterpret_cast<const float4*>(&part[buf][v][q][lane * IT]);
+              acc4.x += o.x; acc4.y += o.y; acc4.z += o.z; acc4.w += o.w;
+            }
+            float* dst = q == 0 ? s1 : (q == 1 ? sdd : sy);
+            dst[0] = acc4.x; dst[1] = acc4.y; dst[2] = acc4.z; dst[3] = acc4.w;
           }
           const float Dd = a.D_ ? a.D_[d] : 0.f;
-          const float uu = ld(urow + t), raw = ld(drow + t) + bias, go = ld(grow + t);
-          float dyv = go, dz = 0.f;
-          if (zrow) {
-            const float zv = ld(zrow + t), sg = sigmoidf_(zv);
-            dyv = go * zv * sg;
-            dz = go * fmaf(Dd, uu, sy) * sg * (1.f + zv * (1.f - sg));
+          float gv[IT], zv[IT], rv[IT], o_du[IT], o_dd[IT], o_dz[IT];
+          auto unp = [](uint2 v, float (&o)[IT]) {
+            o[0] = __uint_as_float(v.x << 16); o[1] = __uint_as_float(v.x & 0xffff0000u);
+            o[2] = __uint_as_float(v.y << 16); o[3] = __uint_as_float(v.y & 0xffff0000u);
+          };
+          unp(cg, gv); unp(cz, zv); unp(craw, rv);
+          const bool inr = tl < a.L;
+          float dDp = 0.f, dbp = 0.f;
+#pragma unroll
+          for (int i = 0; i < IT; ++i) {
+            float dyv = gv[i];
+            o_dz[i] = 0.f;
+            if (zrow) {
+              const float sg = sigmoidf_(zv[i]);
+              dyv = gv[i] * zv[i] * sg;
+              o_dz[i] = gv[i] * fmaf(Dd, uf[i], sy[i]) * sg * (1.f + zv[i] * (1.f - sg));
+            }
+            o_du[i] = fmaf(dlf[i], s1[i], Dd * dyv);
+            o_dd[i] = inr ? sdd[i] * (a.softplus ? sigmoidf_(rv[i] + bias) : 1.f) : 0.f;
+            dDp = fmaf(dyv, uf[i], dDp);
+            dbp += o_dd[i];
           }
-          const float ddl = sdd * (a.softplus ? sigmoidf_(raw) : 1.f);
-          st(((T*)a.du_) + (int64_t)b * a.sdub + (int64_t)d * a.sdud + t, fmaf(Dd, dyv, sdu));
-          st(((T*)a.ddelta_) + (int64_t)b * a.sddb + (int64_t)d * a.sddd + t, ddl);
-          if (zrow && a.dz_) st(((T*)a.dz_) + (int64_t)b * a.sdzb + (int64_t)d * a.sdzd + t, dz);
-          dDp = dyv * uu;
-          dbp = ddl;
+          if (inr) {
+            auto pk = [](const float (&o)[IT]) { return make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3])); };
+            *reinterpret_cast<uint2*>(((bf16_t*)a.du_) + (int64_t)b * a.sdub + (int64_t)d * a.sdud + tl) = pk(o_du);
+            *reinterpret_cast<uint2*>(((bf16_t*)a.ddelta_) + (int64_t)b * a.sddb + (int64_t)d * a.sddd + tl) = pk(o_dd);
+            if (zrow && a.dz_)
+              *reinterpret_cast<uint2*>(((bf16_t*)a.dz_) + (int64_t)b * a.sdzb + (int64_t)d * a.sdzd + tl) = pk(o_dz);
+          }
+          dDp = wave_sum_dpp(dDp);
+          dbp = wave_sum_dpp(dbp);
+          if (lane == 0) {
+            dDacc[k][0] += dDp;
+            dbacc[k][0] += dbp;
+          }
         }
+      } else {
+        // finish item-parallel: thread j <-> step tile*SB_T + j
+        float dDp = 0.f, dbp = 0.f;
+        if (threadIdx.x < SB_T) {
+          const int j = threadIdx.x, t = tile * SB_T + j;
+          if (t < a.L) {
+            float sdu = 0.f, sdd = 0.f, sy = 0.f;
+#pragma unroll
+            for (int v = 0; v < SB_W; ++v) {
+              sdu += part[buf][v][0][j];
+              sdd += part[buf][v][1][j];
+              sy += part[buf][v][2][j];
+            }
+            const float Dd = a.D_ ? a.D_[d] : 0.f;
+            const float uu = ld(urow + t), raw = ld(drow + t) + bias, go = ld(grow + t);
+            float dyv = go, dz = 0.f;
+            if (zrow) {
+              const float zv = ld(zrow + t), sg = sigmoidf_(zv);
+              dyv = go * zv * sg;
+              dz = go * fmaf(Dd, uu, sy) * sg * (1.f + zv * (1.f - sg));
+            }
+            const float ddl = sdd * (a.softplus ? sigmoidf_(raw) : 1.f);
+            st(((T*)a.du_) + (int64_t)b * a.sdub + (int64_t)d * a.sdud + t, fmaf(Dd, dyv, sdu));
+            st(((T*)a.ddelta_) + (int64_t)b * a.sddb + (int64_t)d * a.sddd + t, ddl);
+            if (zrow && a.dz_) st(((T*)a.dz_) + (int64_t)b * a.sdzb + (int64_t)d * a.sdzd + t, dz);
+            dDp = dyv * uu;
+            dbp = ddl;
+          }
+        }
+        dDp = wave_sum_dpp(dDp);
+        dbp = wave_sum_dpp(dbp);
+        if (lane == 0) {
+          dDacc[k][w] += dDp;
+          dbacc[k][w] += dbp;
+        }
+        __syncthreads();  // part[] consumed before the next channel overwrites it
       }
-      dDp = wave_sum_dpp(dDp);
-      dbp = wave_sum_dpp(dbp);
-      if (lane == 0) {
-        dDacc[k][w] += dDp;
-        dbacc[k][w] += dbp;
-      }
-      __syncthreads();  // part[] consumed before the next channel overwrites it
     }
     // this tile's dB / dC partial for the group's channels (this wave's states)
     if (has_states) {
