@@ -599,6 +599,78 @@ Tensor gemm_wgrad(Tensor dY, Tensor X, optional<Tensor> out, bool accumulate) {
   return C;
 }
 
+// ---------------------------------------------------------------------------------------------
+// fused Mamba-2 decode step (kernels/decode.hip).  Every operand is preallocated by the caller
+// (inference.FusedMamba2Decoder) so the three launches per layer can be captured in one HIP graph.
+void chk_f32(const Tensor& t, int64_t n, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == n, "decode: ", name,
+              " must be a contiguous fp32 GPU tensor of ", n, " elements");
+}
+
+void decode_inproj(Tensor hn, Tensor W, Tensor zxbcdt, int64_t conv_lo, int64_t conv_hi, Tensor conv_state,
+                   Tensor conv_w, optional<Tensor> conv_b) {
+  check_cuda(hn, "hn");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(hn.device());
+  TORCH_CHECK(hn.dim() == 2 && hn.is_contiguous() && hn.scalar_type() == at::kBFloat16, "decode: hn must be (b, d) bf16");
+  const int64_t b = hn.size(0), d = hn.size(1);
+  TORCH_CHECK(W.scalar_type() == at::kBFloat16 && W.is_contiguous() && W.dim() == 2 && W.size(1) == d, "decode: W_in");
+  const int64_t n_out = W.size(0);
+  TORCH_CHECK(b <= mamba_amd::decode_max_batch() && d % 8 == 0 && b * d * 2 <= 65536, "decode: b*d too large");
+  chk_f32(zxbcdt, b * n_out, "zxbcdt");
+  const int64_t C = conv_hi - conv_lo;
+  TORCH_CHECK(conv_lo >= 0 && conv_hi <= n_out && C > 0, "decode: conv range");
+  TORCH_CHECK(conv_state.scalar_type() == at::kBFloat16 && conv_state.dim() == 3 && conv_state.size(0) == b &&
+              conv_state.size(1) == C && conv_state.stride(2) == 1, "decode: conv_state (b, C, W-1) bf16");
+  const int64_t Wd = conv_state.size(2) + 1;
+  chk_f32(conv_w, C * Wd, "conv_w");
+  const float* cb = nullptr;
+  if (conv_b.has_value() && conv_b->defined()) {
+    chk_f32(*conv_b, C, "conv_b");
+    cb = conv_b->data_ptr<float>();
+  }
+  HIPCHK(mamba_amd::launch_decode_inproj(hn.data_ptr(), W.data_ptr(), (int)n_out, (int)d, (int)b,
+                                         zxbcdt.data_ptr<float>(), (int)conv_lo, (int)conv_hi, conv_state.data_ptr(),
+                                         conv_state.stride(0), conv_state.stride(1), conv_w.data_ptr<float>(), cb,
+                                         (int)Wd, cur_stream()));
+}
+
+void decode_ssm(Tensor zxbcdt, Tensor state, Tensor A, optional<Tensor> D, optional<Tensor> dt_bias, int64_t ngroups,
+                Tensor g_out, Tensor part) {
+  check_cuda(state, "state");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(state.device());
+  TORCH_CHECK(state.dim() == 4 && state.is_contiguous() && state.scalar_type() == at::kFloat, "decode: state (b,h,p,n) fp32");
+  const int64_t b = state.size(0), H = state.size(1), P = state.size(2), N = state.size(3);
+  TORCH_CHECK(P % 16 == 0 && (N == 64 || N == 128 || N == 256) && H % ngroups == 0, "decode: ssm shape");
+  const int64_t n_out = 2 * H * P + 2 * ngroups * N + H;
+  chk_f32(zxbcdt, b * n_out, "zxbcdt");
+  chk_f32(A, H, "A");
+  const float* Dp = nullptr;
+  const float* bp = nullptr;
+  if (D.has_value() && D->defined()) { chk_f32(*D, H, "D"); Dp = D->data_ptr<float>(); }
+  if (dt_bias.has_value() && dt_bias->defined()) { chk_f32(*dt_bias, H, "dt_bias"); bp = dt_bias->data_ptr<float>(); }
+  TORCH_CHECK(g_out.is_cuda() && g_out.scalar_type() == at::kBFloat16 && g_out.is_contiguous() &&
+              g_out.numel() == b * H * P, "decode: g_out (b, di) bf16");
+  chk_f32(part, b * H * (P / 16), "part");
+  HIPCHK(mamba_amd::launch_decode_ssm(zxbcdt.data_ptr<float>(), (int)n_out, state.data_ptr<float>(), A.data_ptr<float>(),
+                                      Dp, bp, (int)H, (int)P, (int)ngroups, (int)N, (int)b, g_out.data_ptr(),
+                                      part.data_ptr<float>(), cur_stream()));
+}
+
+void decode_outproj(Tensor g, Tensor part, double eps, Tensor W, Tensor out) {
+  check_cuda(g, "g");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(g.device());
+  TORCH_CHECK(g.dim() == 2 && g.is_contiguous() && g.scalar_type() == at::kBFloat16, "decode: g (b, di) bf16");
+  const int64_t b = g.size(0), di = g.size(1);
+  TORCH_CHECK(W.scalar_type() == at::kBFloat16 && W.is_contiguous() && W.dim() == 2 && W.size(1) == di, "decode: W_out");
+  const int64_t d_out = W.size(0);
+  TORCH_CHECK(b <= mamba_amd::decode_max_batch() && di % 8 == 0 && b * di * 2 <= 65536, "decode: b*di too large");
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() && part.dim() == 2 &&
+              part.size(0) == b, "decode: part (b, nparts) fp32");
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 && out.is_contiguous() && out.numel() == b * d_out, "decode: out");
+  HIPCHK(mamba_amd::launch_decode_outproj(g.data_ptr(), part.data_ptr<float>(), (int)part.size(1), (float)eps,
+                                          W.data_ptr(), (int)d_out, (int)di, (int)b, out.data_ptr(), cur_stream()));
+}
+
 }  // namespace
 
 TORCH_LIBRARY(mamba_amd, m) {
@@ -635,6 +707,11 @@ TORCH_LIBRARY(mamba_amd, m) {
   m.def("gemm_wgrad(Tensor dY, Tensor X, Tensor(a!)? out=None, bool accumulate=False) -> Tensor");
   m.def("ssm_state_update(Tensor(a!) state, Tensor x, Tensor dt, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? z, "
         "Tensor? dt_bias, bool softplus) -> Tensor");
+  m.def("decode_inproj(Tensor hn, Tensor W, Tensor(a!) zxbcdt, int conv_lo, int conv_hi, Tensor(b!) conv_state, "
+        "Tensor conv_w, Tensor? conv_b) -> ()");
+  m.def("decode_ssm(Tensor zxbcdt, Tensor(a!) state, Tensor A, Tensor? D, Tensor? dt_bias, int ngroups, "
+        "Tensor(b!) g_out, Tensor(c!) part) -> ()");
+  m.def("decode_outproj(Tensor g, Tensor part, float eps, Tensor W, Tensor(a!) out) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(mamba_amd, CUDA, m) {
@@ -656,4 +733,7 @@ TORCH_LIBRARY_IMPL(mamba_amd, CUDA, m) {
   m.impl("selscan_bwd", &selscan_bwd);
   m.impl("selscan_bwd_into", &selscan_bwd_into);
   m.impl("ssm_state_update", &ssm_state_update);
+  m.impl("decode_inproj", &decode_inproj);
+  m.impl("decode_ssm", &decode_ssm);
+  m.impl("decode_outproj", &decode_outproj);
 }

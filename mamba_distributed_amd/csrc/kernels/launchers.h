@@ -63,4 +63,15 @@ int gemm_wgrad_splits(int M, int P, int Q);
 hipError_t launch_gemm_wgrad(const void* dY, int64_t ldy, const void* X, int64_t ldx, float* part, float* out,
                              int M, int P, int Q, bool accumulate, hipStream_t st);
 
+// ---- decode.hip (fused single-token Mamba-2 layer step; buffers preallocated, graph-capturable) --------
+int decode_max_batch();
+hipError_t launch_decode_inproj(const void* hn, const void* W, int n_out, int d, int b, float* zxbcdt, int conv_lo,
+                                int conv_hi, void* conv_state, int64_t csb, int64_t csc, const float* cw,
+                                const float* cb, int Wd, hipStream_t st);
+hipError_t launch_decode_ssm(const float* zxbcdt, int n_out, float* state, const float* A, const float* D,
+                             const float* dt_bias, int H, int P, int G, int N, int b, void* g_out, float* part,
+                             hipStream_t st);  // g_out bf16
+hipError_t launch_decode_outproj(const void* g, const float* part, int nparts, float eps, const void* W, int d_out,
+                                 int di, int b, void* out, hipStream_t st);  // W = W_out diag(gate-norm weight)
+
 }  // namespace mamba_amd

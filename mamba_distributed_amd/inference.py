@@ -10,6 +10,11 @@ state updates and norms per layer), so host launch overhead, not the GPU, sets t
 
 Only pure Mamba stacks are graphed: attention layers index their KV cache by a Python-side offset
 that changes every token.
+
+For pure Mamba-2 stacks in bf16 the step is additionally FUSED (``fused=None`` -> automatic): each
+layer runs four native kernels (residual-add+RMSNorm, then csrc/kernels/decode.hip: in_proj GEMV+conv
+window, SSM state update+gate, gated-norm+out_proj GEMV) on fp32 parameter copies prepared once,
+instead of ~7 library / elementwise kernels plus per-call parameter casts.
 """
 from __future__ import annotations
 
@@ -20,9 +25,86 @@ import torch
 from .models.mixer_seq import InferenceParams, MambaLMHeadModel
 
 
+class _FusedMamba2Step:
+    """Buffers + fp32 parameter copies for the fused per-layer decode kernels (decode.hip)."""
+
+    def __init__(self, model: MambaLMHeadModel, params: InferenceParams, batch_size: int):
+        dev = next(model.parameters()).device
+        bb = model.backbone
+        self.model, self.params, self.b = model, params, batch_size
+        f32 = lambda t: None if t is None else t.detach().float().contiguous()  # noqa: E731
+        bf = lambda t: t.detach().to(torch.bfloat16).contiguous()  # noqa: E731
+        self.layers = []
+        for i, blk in enumerate(bb.layers):
+            m = blk.mixer
+            H, P, G, N = m.nheads, m.headdim, m.ngroups, m.d_state
+            di = m.d_inner
+            conv_state, ssm_state = params.key_value_memory_dict[i]
+            self.layers.append(dict(
+                norm_w=f32(blk.norm.weight), eps=float(blk.norm.eps), W_in=bf(m.in_proj.weight),
+                conv_lo=di, conv_hi=2 * di + 2 * G * N, conv_w=f32(m.conv1d.weight.reshape(m.conv1d.weight.shape[0], -1)),
+                conv_b=f32(m.conv1d.bias), A=(-torch.exp(m.A_log.detach().float())).contiguous(), D=f32(m.D),
+                dt_bias=f32(m.dt_bias), G=G, geps=float(m.norm.eps),
+                # gate-norm weight folded into out_proj (decode.hip K3 applies rstd in its epilogue)
+                W_out=bf(m.out_proj.weight.float() * m.norm.weight.float()[None, :]),
+                conv_state=conv_state, ssm_state=ssm_state, n_out=m.in_proj.weight.shape[0], di=di, nparts=H * (P // 16)))
+        d = bb.embedding.weight.shape[1]
+        n_out = max(l["n_out"] for l in self.layers)
+        di = max(l["di"] for l in self.layers)
+        nparts = max(l["nparts"] for l in self.layers)
+        b = batch_size
+        self.h = [torch.empty(b, d, device=dev, dtype=torch.bfloat16) for _ in range(2)]
+        self.zx = torch.empty(b * n_out, device=dev, dtype=torch.float32)
+        self.g = torch.empty(b * di, device=dev, dtype=torch.bfloat16)
+        self.part = torch.empty(b * nparts, device=dev, dtype=torch.float32)
+        self.norm_f = bb.norm_f
+        self.norm_f_w = f32(bb.norm_f.weight)
+
+    @staticmethod
+    def supported(model: MambaLMHeadModel, batch_size: int) -> bool:
+        from .models.mamba2 import Mamba2
+        from .ops import _ext
+        bb = model.backbone
+        dev = next(model.parameters()).device
+        if dev.type != "cuda" or not _ext.use_native(next(model.parameters())) or batch_size > 16:
+            return False
+        if not (bb.fused_add_norm and bb.residual_in_fp32) or bb.embedding.weight.dtype != torch.bfloat16:
+            return False
+        d = bb.embedding.weight.shape[1]
+        if d % 8 or batch_size * d * 2 > 65536:
+            return False
+        for blk in bb.layers:
+            m = blk.mixer
+            if type(m) is not Mamba2 or blk.mlp is not None or m.norm_before_gate or m.in_proj.bias is not None \
+                    or m.out_proj.bias is not None or getattr(m, "cp_group", None) is not None:
+                return False
+            if m.conv1d.weight.dtype != torch.bfloat16 or m.headdim % 16 or m.d_state not in (64, 128, 256):
+                return False
+            if m.d_inner % 8 or batch_size * m.d_inner * 2 > 65536 or m.d_ssm != m.d_inner:
+                return False
+        return True
+
+    def __call__(self, tok: torch.Tensor) -> torch.Tensor:
+        ops = torch.ops.mamba_amd
+        b = self.b
+        h = self.model.backbone.embedding(tok.reshape(b)).to(torch.bfloat16)
+        res = None
+        for i, L in enumerate(self.layers):
+            zx = self.zx[: b * L["n_out"]]
+            g = self.g[: b * L["di"]].view(b, L["di"])
+            part = self.part[: b * L["nparts"]].view(b, L["nparts"])
+            hn, res, _ = ops.add_rmsnorm_fwd(h, res, L["norm_w"], L["eps"], torch.bfloat16, torch.float32)
+            ops.decode_inproj(hn, L["W_in"], zx, L["conv_lo"], L["conv_hi"], L["conv_state"], L["conv_w"], L["conv_b"])
+            ops.decode_ssm(zx, L["ssm_state"], L["A"], L["D"], L["dt_bias"], L["G"], g, part)
+            h = self.h[i % 2]
+            ops.decode_outproj(g, part, L["geps"], L["W_out"], h)
+        hn, _, _ = ops.add_rmsnorm_fwd(h, res, self.norm_f_w, self.norm_f.eps, torch.bfloat16, torch.float32)
+        return torch.nn.functional.linear(hn, self.model.lm_head.weight)
+
+
 class GraphedDecoder:
     def __init__(self, model: MambaLMHeadModel, batch_size: int = 1, max_seqlen: int = 2048,
-                 use_graph: Optional[bool] = None):
+                 use_graph: Optional[bool] = None, fused: Optional[bool] = None):
         self.model = model
         self.device = next(model.parameters()).device
         attn = getattr(model.config, "attn_layer_idx", None)
@@ -37,6 +119,9 @@ class GraphedDecoder:
         self.tok = torch.zeros(batch_size, 1, dtype=torch.long, device=self.device)
         self.graph = None
         self.out = None
+        if fused is None:
+            fused = _FusedMamba2Step.supported(model, batch_size)
+        self.fused = _FusedMamba2Step(model, self.params, batch_size) if fused else None
 
     def _states(self):
         return [t for v in self.params.key_value_memory_dict.values() for t in v]
@@ -57,6 +142,8 @@ class GraphedDecoder:
         return logits[:, -1]
 
     def _eager_step(self) -> torch.Tensor:
+        if self.fused is not None:
+            return self.fused(self.tok)
         return MambaLMHeadModel.forward(self.model, self.tok, inference_params=self.params).logits[:, -1]
 
     def _capture(self):

@@ -30,8 +30,11 @@ def main():
     m = LMHeadModel(cfg, device="cuda").to(torch.bfloat16).eval()
     for bs in a.batch:
         ids = torch.randint(0, cfg.vocab_size, (bs, a.prompt), device="cuda")
-        for mode in ("eager", "graph"):
-            dec = GraphedDecoder(m, batch_size=bs, max_seqlen=a.prompt + a.tokens + 8, use_graph=mode == "graph")
+        for mode in ("eager", "graph_unfused", "graph"):
+            # eager / graph: fused Mamba-2 decode kernels (decode.hip) when supported; graph_unfused: the
+            # per-op cached step (library GEMVs + separate conv / SSM / norm kernels) in one HIP graph
+            dec = GraphedDecoder(m, batch_size=bs, max_seqlen=a.prompt + a.tokens + 8, use_graph=mode != "eager",
+                                 fused=False if mode == "graph_unfused" else None)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             logits = dec.prefill(ids)
@@ -46,7 +49,8 @@ def main():
                 tok = dec.step(tok).argmax(-1)
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
-            print(json.dumps({"model": a.model, "batch": bs, "mode": mode, "prompt": a.prompt,
+            print(json.dumps({"model": a.model, "batch": bs, "mode": mode, "fused": dec.fused is not None,
+                              "prompt": a.prompt,
                               "prefill_ms": round(t_prefill * 1e3, 2),
                               "ms_per_token": round(dt * 1e3 / a.tokens, 3),
                               "tokens_per_s": round(bs * a.tokens / dt, 1)}), flush=True)

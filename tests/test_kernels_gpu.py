@@ -349,6 +349,32 @@ def test_graphed_decode_matches_eager(cuda, layer):
     assert rel(lg, full) < 1e-3
 
 
+@pytest.mark.parametrize("batch", [1, 3])
+def test_fused_decode_matches_unfused(cuda, batch):
+    """The fused 3-kernel Mamba-2 decode layer (csrc/kernels/decode.hip), HIP-graph replayed, tracks the
+    unfused cached step of a bf16 model (logits and SSM states) and the full bf16 recompute."""
+    from mamba_distributed_amd import LMHeadModel, MambaConfig
+    from mamba_distributed_amd.inference import GraphedDecoder
+    torch.manual_seed(0)
+    cfg = MambaConfig(d_model=256, n_layer=4, vocab_size=1024, ssm_cfg={"layer": "Mamba2"})
+    m = LMHeadModel(cfg, device=cuda).to(torch.bfloat16).eval()
+    ids = torch.randint(0, 1024, (batch, 48), device=cuda)
+    f = GraphedDecoder(m, batch_size=batch, max_seqlen=64, use_graph=True)
+    u = GraphedDecoder(m, batch_size=batch, max_seqlen=64, use_graph=False, fused=False)
+    assert f.fused is not None and u.fused is None
+    lf, lu = f.prefill(ids[:, :32]), u.prefill(ids[:, :32])
+    torch.testing.assert_close(lf, lu)
+    for t in range(32, 48):
+        lf, lu = f.step(ids[:, t]), u.step(ids[:, t])
+        assert rel(lf, lu) < 3e-2, (t, rel(lf, lu))
+    assert f.graph is not None
+    for (cf, sf), (cu, su) in zip(f.params.key_value_memory_dict.values(), u.params.key_value_memory_dict.values()):
+        assert rel(sf, su) < 3e-2 and rel(cf, cu) < 3e-2
+    with torch.no_grad():
+        full = m(ids)[0][:, -1]
+    assert rel(lf, full) < 5e-2
+
+
 @pytest.mark.parametrize("layer", ["Mamba1", "Mamba2"])
 def test_fp32_forward_on_gpu_matches_cpu(cuda, layer):
     """The reference's HellaSwag eval runs the model in fp32 without autocast: the GPU path must
