@@ -42,6 +42,10 @@ def enable_tuned_gemms(path: Optional[str] = None, tune: bool = False, max_tunin
     tunable.enable(True)
     tunable.set_filename(path)
     tunable.tuning_enable(tune)
+    # replay is read-only: never rewrite the shipped table at exit (every DDP rank would race on it);
+    # older torch has no switch and only writes when tuning found new results
+    if hasattr(tunable, "write_file_on_exit"):
+        tunable.write_file_on_exit(bool(tune))
     if tune:
         tunable.set_max_tuning_duration(max_tuning_ms)
         tunable.set_max_tuning_iterations(100)
