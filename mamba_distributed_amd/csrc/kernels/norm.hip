@@ -12,6 +12,8 @@
 //    per block is written; a second kernel sums the partials column-wise in a fixed order
 //    (bitwise deterministic, no float atomics).
 // Reference semantics: upstream ops/triton/layer_norm.py and layernorm_gated.py.
+#include <cstdlib>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -463,6 +465,173 @@ __global__ __launch_bounds__(256) void gated_rmsnorm_bwd_bf16_k(
 }
 
 // ------------------------------------------------------------------------------------------
+// 16-byte fast path of the gated norm (bf16 x / z / y, one norm group per row, norm_before_gate=False,
+// D % 512 == 0, 16-B aligned rows): each lane owns NCH chunks of 8 consecutive columns
+// (col = 8 (lane + 64 c)), so every load / store is one dwordx4 per lane and a wave instruction moves
+// 1 KiB of a row.  The Mamba-2 shape (D = 1536, z a strided slice of zxbcdt) runs here.
+__device__ __forceinline__ void unpack8f(uint4 v, float (&o)[8]) {
+  const unsigned q[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    o[2 * j] = __uint_as_float(q[j] << 16);
+    o[2 * j + 1] = __uint_as_float(q[j] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ uint4 pack8f(const float (&o)[8]) {
+  return make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7]));
+}
+
+template <int NCH>
+__global__ __launch_bounds__(256) void gated_rmsnorm_fwd_v8_k(const bf16_t* __restrict__ x, int64_t sx,
+                                                              const bf16_t* __restrict__ z, int64_t sz,
+                                                              const float* __restrict__ w, bf16_t* __restrict__ y,
+                                                              float* __restrict__ rstd, int64_t M, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  uint4 px[NCH], pz[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = (lane + 64 * c) * 8;
+    px[c] = *reinterpret_cast<const uint4*>(x + row * sx + col);
+    pz[c] = *reinterpret_cast<const uint4*>(z + row * sz + col);
+  }
+  float g[NCH][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    float xv[8], zv[8];
+    unpack8f(px[c], xv);
+    unpack8f(pz[c], zv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      g[c][j] = xv[j] * siluf_(zv[j]);
+      ss = fmaf(g[c][j], g[c][j], ss);
+    }
+  }
+  ss = wave_sum(ss);
+  const float rs = rsqrtf(ss / (float)D + eps);
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = (lane + 64 * c) * 8;
+    const float4 w0 = *reinterpret_cast<const float4*>(w + col), w1 = *reinterpret_cast<const float4*>(w + col + 4);
+    const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = g[c][j] * rs * wv[j];
+    *reinterpret_cast<uint4*>(y + row * D + col) = pack8f(o);
+  }
+  if (lane == 0) rstd[row] = rs;
+}
+
+template <int NCH>
+__global__ __launch_bounds__(256) void gated_rmsnorm_bwd_v8_k(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, int64_t sx, const bf16_t* __restrict__ z,
+    int64_t sz, const float* __restrict__ w, const float* __restrict__ rstd, bf16_t* __restrict__ dx, int64_t sdx,
+    bf16_t* __restrict__ dz, int64_t sdz, float* __restrict__ part, int64_t M, int D) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float acc[NCH][8];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[c][j] = 0.f;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + wave; row < M; row += (int64_t)gridDim.x * 4) {
+    uint4 pg[NCH], px[NCH], pz[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = (lane + 64 * c) * 8;
+      pg[c] = *reinterpret_cast<const uint4*>(dy + row * D + col);
+      px[c] = *reinterpret_cast<const uint4*>(x + row * sx + col);
+      pz[c] = *reinterpret_cast<const uint4*>(z + row * sz + col);
+    }
+    const float rs = rstd[row];
+    float dot = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = (lane + 64 * c) * 8;
+      const float4 w0 = *reinterpret_cast<const float4*>(w + col), w1 = *reinterpret_cast<const float4*>(w + col + 4);
+      const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      float gv[8], xv[8], zv[8];
+      unpack8f(pg[c], gv);
+      unpack8f(px[c], xv);
+      unpack8f(pz[c], zv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float xh = xv[j] * siluf_(zv[j]) * rs;
+        dot = fmaf(gv[j] * wv[j], xh, dot);
+        acc[c][j] = fmaf(gv[j], xh, acc[c][j]);
+      }
+    }
+    // keep the packed inputs opaque across the reduction so pass 2 recomputes from them instead of
+    // holding ~3 unpacked fp32 copies of every element (register pressure -> occupancy)
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+      asm volatile("" : "+v"(pg[c].x), "+v"(pg[c].y), "+v"(pg[c].z), "+v"(pg[c].w), "+v"(px[c].x), "+v"(px[c].y),
+                   "+v"(px[c].z), "+v"(px[c].w), "+v"(pz[c].x), "+v"(pz[c].y), "+v"(pz[c].z), "+v"(pz[c].w));
+    dot = wave_sum(dot) / (float)D;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = (lane + 64 * c) * 8;
+      const float4 w0 = *reinterpret_cast<const float4*>(w + col), w1 = *reinterpret_cast<const float4*>(w + col + 4);
+      const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      float gv[8], xv[8], zv[8], ox[8], oz[8];
+      unpack8f(pg[c], gv);
+      unpack8f(px[c], xv);
+      unpack8f(pz[c], zv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float sg = sigmoidf_(zv[j]);
+        const float sl = zv[j] * sg;
+        const float dsilu = sg * (1.f + zv[j] * (1.f - sg));
+        const float xh = xv[j] * sl * rs;
+        const float dbase = (gv[j] * wv[j] - xh * dot) * rs;
+        ox[j] = dbase * sl;
+        oz[j] = dbase * xv[j] * dsilu;
+      }
+      *reinterpret_cast<uint4*>(dx + row * sdx + col) = pack8f(ox);
+      *reinterpret_cast<uint4*>(dz + row * sdz + col) = pack8f(oz);
+    }
+  }
+  // per-block dw partial: the 4 waves' accumulators summed through LDS in wave order
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = (lane + 64 * c) * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) lds[wave * D + col + j] = acc[c][j];
+  }
+  __syncthreads();
+  for (int col = threadIdx.x; col < D; col += blockDim.x)
+    part[(int64_t)blockIdx.x * D + col] = lds[col] + lds[D + col] + lds[2 * D + col] + lds[3 * D + col];
+}
+
+#define NCH8_SWITCH(D, ...)                                         \
+  do {                                                              \
+    switch ((D) / 512) {                                            \
+      case 1: { constexpr int NCH = 1; __VA_ARGS__; break; }        \
+      case 2: { constexpr int NCH = 2; __VA_ARGS__; break; }        \
+      case 3: { constexpr int NCH = 3; __VA_ARGS__; break; }        \
+      case 4: { constexpr int NCH = 4; __VA_ARGS__; break; }        \
+      case 6: { constexpr int NCH = 6; __VA_ARGS__; break; }        \
+      case 8: { constexpr int NCH = 8; __VA_ARGS__; break; }        \
+      case 10: { constexpr int NCH = 10; __VA_ARGS__; break; }      \
+      default: return hipErrorInvalidValue;                         \
+    }                                                               \
+  } while (0)
+
+static bool gated_v8_ok(int D, int G, bool nbg, int xdt, int zdt, int64_t sx, int64_t sz, const void* x,
+                        const void* z) {
+  static const bool off = [] {
+    const char* e = std::getenv("MAMBA_AMD_GNORM_V8");
+    return e && std::atoi(e) == 0;
+  }();
+  if (off) return false;
+  const int q = D / 512;
+  return !nbg && G == D && D % 512 == 0 && (q <= 4 || q == 6 || q == 8 || q == 10) && xdt == kBF16 &&
+         zdt == kBF16 && sx % 8 == 0 && sz % 8 == 0 && (uintptr_t)x % 16 == 0 && (uintptr_t)z % 16 == 0;
+}
+
+// ------------------------------------------------------------------------------------------
 // host launchers
 #define NCH_SWITCH(D, ...)                                               \
   do {                                                                   \
@@ -513,6 +682,11 @@ hipError_t launch_gated_rmsnorm_fwd(const void* x, int xdt, int64_t sx, const vo
                                     float eps, bool nbg, hipStream_t st) {
   if (M == 0) return hipSuccess;
   dim3 grid((unsigned)((M + 3) / 4)), block(256);
+  if (ydt == kBF16 && gated_v8_ok(D, G, nbg, xdt, zdt, sx, sz, x, z) && (uintptr_t)y % 16 == 0) {
+    NCH8_SWITCH(D, hipLaunchKernelGGL((gated_rmsnorm_fwd_v8_k<NCH>), grid, block, 0, st, (const bf16_t*)x, sx,
+                                      (const bf16_t*)z, sz, w, (bf16_t*)y, rstd, M, D, eps));
+    return hipGetLastError();
+  }
   if (nbg) {
     NCH_SWITCH(D, hipLaunchKernelGGL((gated_rmsnorm_fwd_k<NCH, true>), grid, block, 0, st, x, xdt, sx, z, zdt, sz,
                                      w, y, ydt, rstd, M, D, G, eps));
@@ -530,7 +704,12 @@ hipError_t launch_gated_rmsnorm_bwd(const void* dy, int ydt, const void* x, int 
   const int g = bwd_grid(M);
   const size_t lds = 4 * (size_t)D * sizeof(float);
   const bool fast = ydt == kBF16 && xdt == kBF16 && zdt == kBF16;
-  if (fast && nbg) {
+  if (fast && gated_v8_ok(D, G, nbg, xdt, zdt, sx, sz, x, z) && sdx % 8 == 0 && sdz % 8 == 0 &&
+      (uintptr_t)dx % 16 == 0 && (uintptr_t)dz % 16 == 0 && (uintptr_t)dy % 16 == 0) {
+    NCH8_SWITCH(D, hipLaunchKernelGGL((gated_rmsnorm_bwd_v8_k<NCH>), dim3(g), dim3(256), lds, st, (const bf16_t*)dy,
+                                      (const bf16_t*)x, sx, (const bf16_t*)z, sz, w, rstd, (bf16_t*)dx, sdx,
+                                      (bf16_t*)dz, sdz, part, M, D));
+  } else if (fast && nbg) {
     NCH_SWITCH(D, hipLaunchKernelGGL((gated_rmsnorm_bwd_bf16_k<NCH, true>), dim3(g), dim3(256), lds, st,
                                      (const bf16_t*)dy, (const bf16_t*)x, sx, (const bf16_t*)z, sz, w, rstd,
                                      (bf16_t*)dx, sdx, (bf16_t*)dz, sdz, part, M, D, G));
