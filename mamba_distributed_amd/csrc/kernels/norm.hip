@@ -650,8 +650,12 @@ static bool gated_v8_ok(int D, int G, bool nbg, int xdt, int zdt, int64_t sx, in
   } while (0)
 
 static int bwd_grid(int64_t M) {
+  static const int cap = [] {
+    const char* e = std::getenv("MAMBA_AMD_NORM_BWD_GRID");
+    return e ? std::atoi(e) : 2048;
+  }();
   int64_t g = (M + 3) / 4;
-  return (int)(g < 2048 ? (g < 1 ? 1 : g) : 2048);
+  return (int)(g < cap ? (g < 1 ? 1 : g) : cap);
 }
 
 hipError_t launch_add_rmsnorm_fwd(const void* x, int xdt, int64_t sx, const void* res, int rdt, int64_t sr,

@@ -27,6 +27,8 @@ import torch
 
 _scope_depth = 0
 _direct = False
+_side = {}            # device index -> side stream for in-place weight-gradient GEMMs
+_side_dirty = set()   # devices whose side stream has work the main stream has not waited for
 _pending: List[Tuple[torch.Tensor, torch.Tensor]] = []
 _flush_queued = False
 _wcache: Dict[Tuple[int, torch.dtype], Tuple[torch.Tensor, torch.Tensor]] = {}
@@ -44,12 +46,41 @@ def accumulation_scope():
         if _scope_depth == 0:
             _direct = False
             _wcache.clear()
+            join_side()
 
 
 def set_direct(enabled: bool) -> None:
     """Called per micro-step (parallel/ddp.py::set_grad_sync): True on the no-sync micro-steps."""
     global _direct
     _direct = bool(enabled) and _scope_depth > 0
+    if not _direct:
+        join_side()  # the sync micro-step's autograd accumulation must see every in-place wgrad
+
+
+def side_stream(device: torch.device):
+    """Stream for the no-sync micro-steps' in-place weight-gradient GEMMs.  They have no autograd
+    consumer (they add straight into p.grad), so they can run beside the rest of the backward: the
+    compute-bound wgrad GEMMs overlap the memory- / latency-bound norm, conv and scan kernels of the
+    main stream.  Returns None when disabled (MAMBA_AMD_WGRAD_STREAM=0)."""
+    import os
+    if os.environ.get("MAMBA_AMD_WGRAD_STREAM", "1") == "0" or device.type != "cuda":
+        return None
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    s = _side.get(idx)
+    if s is None:
+        s = torch.cuda.Stream(device=idx)
+        _side[idx] = s
+    _side_dirty.add(idx)
+    return s
+
+
+def join_side() -> None:
+    """Make every device's current stream wait for its side stream's queued weight-gradient work."""
+    if not _side_dirty:
+        return
+    for idx in list(_side_dirty):
+        torch.cuda.current_stream(idx).wait_stream(_side[idx])
+    _side_dirty.clear()
 
 
 def in_scope() -> bool:

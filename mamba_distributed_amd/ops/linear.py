@@ -56,8 +56,17 @@ class _ProjFn(torch.autograd.Function):
             native = _native_ok(dy2, x2)
             if (native and grad_accum.accumulable(p) and p.grad.dtype == torch.float32 and p.grad.is_contiguous()
                     and p.grad.shape == w.shape):
-                # no-sync micro-step: the split-K reduction adds straight into p.grad
-                _ext.ops().gemm_wgrad(dy2, x2, p.grad, True)
+                # no-sync micro-step: the split-K reduction adds straight into p.grad, on a side stream
+                # beside the rest of the backward (grad_accum.side_stream; joined before the sync step)
+                side = grad_accum.side_stream(dy2.device)
+                if side is None:
+                    _ext.ops().gemm_wgrad(dy2, x2, p.grad, True)
+                else:
+                    side.wait_stream(torch.cuda.current_stream(dy2.device))
+                    with torch.cuda.stream(side):
+                        _ext.ops().gemm_wgrad(dy2, x2, p.grad, True)
+                    dy2.record_stream(side)
+                    x2.record_stream(side)
             else:
                 dw = _ext.ops().gemm_wgrad(dy2, x2, None, False) if native else torch.mm(dy2.t(), x2)
                 dw = grad_accum.defer(p, dw.to(ctx.wdtype))
