@@ -41,6 +41,7 @@ def main():
     p.add_argument("--no-fused-ce", action="store_true")
     p.add_argument("--no-tuned-gemms", action="store_true", help="library-default GEMM solutions")
     p.add_argument("--profile-steps", type=int, default=0, help="torch.profiler trace of N extra steps")
+    p.add_argument("--no-overlap", action="store_true", help="run the micro-steps strictly one after another")
     a = p.parse_args()
     if a.reference_ops:
         os.environ["MAMBA_AMD_FORCE_REFERENCE"] = "1"
@@ -49,6 +50,7 @@ def main():
     from mamba_distributed_amd.data.loader import SyntheticTokens
     from mamba_distributed_amd.ops import grad_accum
     from mamba_distributed_amd.parallel import ddp as ddp_mod
+    from mamba_distributed_amd.parallel.microbatch import run_micro_batches
     from mamba_distributed_amd.parallel.dist import all_reduce_avg, all_reduce_max, barrier, destroy, init_distributed
 
     info = init_distributed("auto")
@@ -66,18 +68,17 @@ def main():
     loader = SyntheticTokens(a.B, a.T, cfg.vocab_size, info.rank, world, device=dev)
     fused = not a.no_fused_ce
 
+    def compute_loss(x, y):
+        with torch.autocast(device_type="cuda", dtype=torch.bfloat16):
+            _, loss = dmodel(x, y, return_logits=not fused)
+        return loss / accum
+
     def step():
         opt.zero_grad(set_to_none=True)
-        loss_acc = torch.zeros((), device=dev)
         with grad_accum.accumulation_scope():
-            for micro in range(accum):
-                x, y = loader.next_batch()
-                ddp_mod.set_grad_sync(dmodel, micro == accum - 1)
-                with torch.autocast(device_type="cuda", dtype=torch.bfloat16):
-                    _, loss = dmodel(x, y, return_logits=not fused)
-                loss = loss / accum
-                loss_acc += loss.detach().float()
-                loss.backward()
+            # micro-batch k+1's forward runs on a second stream beside micro-batch k's backward
+            loss_acc = run_micro_batches(dmodel, loader.next_batch, accum, compute_loss,
+                                         overlap=not a.no_overlap)
         all_reduce_avg(loss_acc)
         torch.nn.utils.clip_grad_norm_(dmodel.parameters(), 1.0)
         opt.step()
@@ -132,6 +133,7 @@ def main():
                 "parallelism": f"dp{world}",
                 "ops": "pytorch-reference" if a.reference_ops else "native-hip",
                 "gemm_table": "tunableop-gfx950" if tuned else "library-default",
+                "microbatch_overlap": not a.no_overlap,
                 "final_loss": round(loss_v, 4),
             },
         }

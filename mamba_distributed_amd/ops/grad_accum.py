@@ -110,26 +110,36 @@ def accumulable(param) -> bool:
             and param.grad is not None)
 
 
+_pending_stream = None  # stream the queued gradients were produced on (the backward's stream)
+
+
 def _flush() -> None:
-    global _flush_queued
+    global _flush_queued, _pending_stream
     _flush_queued = False
     if _pending:
         dst = [d for d, _ in _pending]
         src = [s for _, s in _pending]
         _pending.clear()
-        torch._foreach_add_(dst, src)
+        st, _pending_stream = _pending_stream, None
+        if st is not None:
+            with torch.cuda.stream(st):  # the callback thread's current stream may be another one
+                torch._foreach_add_(dst, src)
+        else:
+            torch._foreach_add_(dst, src)
 
 
 def defer(param, grad):
     """Return value for ``param``'s slot in an autograd backward: ``grad`` itself on the normal
     path, or None after queueing it for the batched accumulation at the end of this backward."""
-    global _flush_queued
+    global _flush_queued, _pending_stream
     if grad is None or not accumulable(param):
         return grad
     g = param.grad
     if g.shape != grad.shape or g.dtype != grad.dtype or g.device != grad.device:
         return grad
     _pending.append((g, grad))
+    if grad.is_cuda and _pending_stream is None:
+        _pending_stream = torch.cuda.current_stream(grad.device)
     if not _flush_queued:
         torch.autograd.Variable._execution_engine.queue_callback(_flush)
         _flush_queued = True

@@ -1,0 +1,97 @@
+"""Gradient-accumulation loop with the next micro-batch's forward overlapped on a second HIP stream.
+
+The reference runs its micro-steps strictly one after the other (train.py:205-219).  Within one
+optimizer step the weights are frozen, so micro-batch k+1's forward depends on nothing that micro-batch
+k's backward produces.  Here it is enqueued on a second stream right before backward k, so the
+GEMM- and MFMA-heavy forward fills the CUs the memory- and latency-bound backward kernels (norms,
+conv, scan) leave idle:
+
+    stream A:  fwd0 | bwd0 ......... | fwd2 | (wait bwd1) bwd2 ...
+    stream B:       | (wait fwd0) fwd1 | (wait bwd0) bwd1 | fwd3 ...
+
+Ordering rules, each enforced with one stream wait:
+  * backward k waits for backward k-1 (they accumulate into the same ``p.grad``), captured BEFORE
+    forward k+1 is enqueued behind backward k-1, so forward k+1 still runs beside backward k;
+  * forward 1 waits for forward 0, which builds the step's bf16 weight casts (ops/grad_accum.py);
+  * the last micro-step runs on the caller's stream; under DDP its forward (which arms the
+    gradient-reduction hooks) is only issued after every earlier backward has been enqueued;
+  * the caller's stream waits for the other stream before returning.
+Every micro-step's reductions happen in the same order as in the sequential loop, so the gradients
+are bitwise identical (tests/test_kernels_gpu.py::test_microbatch_overlap_is_bitwise_identical).
+"""
+from __future__ import annotations
+
+from typing import Callable, Dict
+
+import torch
+
+from ..ops import grad_accum
+
+_OTHER: Dict[int, "torch.cuda.Stream"] = {}
+
+
+def _is_ddp(model) -> bool:
+    from torch.nn.parallel import DistributedDataParallel as DDP
+    return isinstance(model, DDP)
+
+
+def _set_ddp_sync(model, enabled: bool) -> None:
+    if _is_ddp(model):
+        model.require_backward_grad_sync = enabled
+
+
+def run_micro_batches(model, next_batch: Callable, accum: int, compute_loss: Callable,
+                      overlap: bool = True) -> torch.Tensor:
+    """Forward + backward of ``accum`` micro-batches for ONE optimizer step; returns the summed
+    (already 1/accum-scaled by ``compute_loss``) loss as an fp32 scalar tensor.
+
+    ``next_batch() -> (x, y)``; ``compute_loss(x, y) -> loss`` runs the forward (with autocast).
+    Must be called inside ``grad_accum.accumulation_scope()``."""
+    cuda = torch.cuda.is_available() and torch.cuda.is_initialized()
+    if not overlap or not cuda or accum < 2:
+        total = None
+        for k in range(accum):
+            sync = k == accum - 1
+            _set_ddp_sync(model, sync)
+            grad_accum.set_direct(not sync)
+            x, y = next_batch()
+            loss = compute_loss(x, y)
+            total = loss.detach().float() if total is None else total + loss.detach().float()
+            loss.backward()
+        return total
+    ddp = _is_ddp(model)
+    main = torch.cuda.current_stream()
+    dev = main.device.index if main.device.index is not None else torch.cuda.current_device()
+    other = _OTHER.get(dev)
+    if other is None:
+        other = _OTHER[dev] = torch.cuda.Stream(device=dev)
+    streams = [main if (accum - 1 - k) % 2 == 0 else other for k in range(accum)]
+    losses = [None] * accum
+
+    def forward(k):
+        with torch.cuda.stream(streams[k]):
+            _set_ddp_sync(model, k == accum - 1)
+            x, y = next_batch()
+            losses[k] = compute_loss(x, y)
+
+    forward(0)
+    streams[1].wait_stream(streams[0])  # forward 0 built the step's cached weight casts
+    for k in range(accum):
+        nxt = k + 1
+        if k > 0:
+            streams[k].wait_stream(streams[k - 1])  # after backward k-1 (forward k+1 is not queued yet)
+        early = nxt < accum and (not ddp or nxt < accum - 1)
+        if early:
+            forward(nxt)  # on streams[k-1] (or the other stream for k = 0): beside backward k
+        grad_accum.set_direct(k != accum - 1)
+        with torch.cuda.stream(streams[k]):
+            losses[k].backward()
+        if nxt < accum and not early:
+            # DDP's sync forward arms the reducer hooks: only after every earlier backward is queued
+            streams[nxt].wait_stream(streams[k])
+            forward(nxt)
+    main.wait_stream(other)
+    total = losses[0].detach().float()
+    for l in losses[1:]:
+        total = total + l.detach().float()
+    return total

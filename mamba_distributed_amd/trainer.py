@@ -39,6 +39,7 @@ from .parallel.api import clip_grad_norm_ as par_clip_grad_norm_
 from .parallel.api import full_state_dict, parallelize, sync_tp_grads
 from .parallel.dist import all_gather_object, all_reduce_avg, destroy, init_distributed
 from .parallel.groups import init_parallel_groups
+from .parallel.microbatch import run_micro_batches
 from .utils.checkpoint import latest_checkpoint, load_checkpoint, save_checkpoint, set_rng_state
 from .utils.lr import get_lr
 
@@ -80,6 +81,7 @@ class TrainArgs:
     tp: int = 1                          # tensor parallel degree (Mamba-2 heads; parallel/tensor_parallel.py)
     cp: int = 1                          # context parallel degree (sequence shards; parallel/context_parallel.py)
     sequence_parallel: bool = False      # with tp > 1: shard the residual stream over tokens as well
+    overlap_microbatches: bool = True    # next micro-batch's forward beside the current backward (GPU)
 
 
 def build_config(a: TrainArgs) -> MambaConfig:
@@ -234,16 +236,17 @@ class Trainer:
     def train_step(self, step):
         self.model.train()
         self.optimizer.zero_grad(set_to_none=True)
-        loss_accum = torch.zeros((), device=self.device)
+        def compute_loss(x, y):
+            with self._autocast():
+                _, loss = self.model(x, y, return_logits=not self.a.fused_ce)
+            return loss / self.grad_accum_steps
+
+        # overlap micro-batch k+1's forward with k's backward on a second stream (parallel/microbatch.py);
+        # not under TP/CP, whose per-layer collectives must be issued on one stream per communicator
+        overlap = self.a.overlap_microbatches and self.device_type == "cuda" and not self.parallel
         with grad_accum.accumulation_scope():  # weights are frozen until optimizer.step()
-            for micro_step in range(self.grad_accum_steps):
-                x, y = self._batch(self.train_loader)
-                ddp_mod.set_grad_sync(self.model, micro_step == self.grad_accum_steps - 1)
-                with self._autocast():
-                    _, loss = self.model(x, y, return_logits=not self.a.fused_ce)
-                loss = loss / self.grad_accum_steps
-                loss_accum += loss.detach().float()
-                loss.backward()
+            loss_accum = run_micro_batches(self.model, lambda: self._batch(self.train_loader), self.grad_accum_steps,
+                                           compute_loss, overlap=overlap)
         all_reduce_avg(loss_accum)
         if self.parallel:
             sync_tp_grads(self.model, self.groups)

@@ -510,3 +510,39 @@ def test_unfused_parallel_inner_matches_fused(cuda):
     yb.backward(go)
     for i, (a, b_) in enumerate(zip(xa, xb)):
         assert rel(a.grad, b_.grad) < 2e-2, (i, rel(a.grad, b_.grad))
+
+
+@pytest.mark.parametrize("layer", ["Mamba1", "Mamba2"])
+def test_microbatch_overlap_is_bitwise_identical(cuda, layer):
+    """parallel.microbatch: micro-batch k+1's forward on a second stream beside backward k (plus the
+    side-stream in-place weight-gradient GEMMs) gives bitwise the same gradients and loss as the
+    strictly sequential accumulation loop."""
+    from mamba_distributed_amd import LMHeadModel, MambaConfig
+    from mamba_distributed_amd.ops import grad_accum
+    from mamba_distributed_amd.parallel.microbatch import run_micro_batches
+    torch.manual_seed(0)
+    cfg = MambaConfig(d_model=256, n_layer=4, vocab_size=1024, ssm_cfg={"layer": layer})
+    m = LMHeadModel(cfg, device=cuda)
+    accum = 5
+    g = torch.Generator(device=cuda).manual_seed(1)
+    data = [(torch.randint(0, 1024, (2, 256), device=cuda, generator=g),
+             torch.randint(0, 1024, (2, 256), device=cuda, generator=g)) for _ in range(accum)]
+
+    def run(overlap):
+        m.zero_grad(set_to_none=True)
+        it = iter(data)
+
+        def loss_fn(x, y):
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                return m(x, y, return_logits=False)[1] / accum
+
+        with grad_accum.accumulation_scope():
+            loss = run_micro_batches(m, lambda: next(it), accum, loss_fn, overlap=overlap)
+        torch.cuda.synchronize()
+        return loss, {k: p.grad.clone() for k, p in m.named_parameters()}
+
+    l0, g0 = run(False)
+    l1, g1 = run(True)
+    assert torch.equal(l0, l1), (l0, l1)
+    for k in g0:
+        assert torch.equal(g0[k], g1[k]), k
