@@ -6,7 +6,7 @@
 
 Config = BASELINE.json's headline: Mamba-2 280M (d_model 768, 64 layers, vocab 50304), seq 1024,
 micro-batch 32, global batch 524,288 tokens (= 512 sequences; grad-accum 16/N), bf16 autocast,
-fused AdamW, grad clip 1.0, DDP over RCCL.  Synthetic tokens, random init (no dataset/weights
+fused AdamW, grad clip 1.0, data parallel over RCCL (native bucketed reducer; --dp-impl ddp = torch DDP).  Synthetic tokens, random init (no dataset/weights
 on the box).  A "step" is one full optimizer step (all micro-batches + all-reduce + clip + AdamW).
 W untimed warmup steps, then exactly K steps between barrier+synchronize pairs; the MAX elapsed
 over ranks is reported; rank 0 prints one JSON line.
@@ -42,6 +42,8 @@ def main():
     p.add_argument("--no-tuned-gemms", action="store_true", help="library-default GEMM solutions")
     p.add_argument("--profile-steps", type=int, default=0, help="torch.profiler trace of N extra steps")
     p.add_argument("--no-overlap", action="store_true", help="run the micro-steps strictly one after another")
+    p.add_argument("--dp-impl", default="native", choices=["native", "ddp"],
+                   help="gradient all-reduce: native bucketed reducer (parallel/reducer.py) or torch DDP")
     a = p.parse_args()
     if a.reference_ops:
         os.environ["MAMBA_AMD_FORCE_REFERENCE"] = "1"
@@ -63,7 +65,7 @@ def main():
     torch.manual_seed(1337)
     cfg = preset(a.model)
     model = LMHeadModel(cfg, device=dev)
-    dmodel = ddp_mod.wrap_ddp(model, info, a.bucket_cap_mb, a.grad_comm_dtype)
+    dmodel = ddp_mod.wrap_data_parallel(model, info, a.dp_impl, a.bucket_cap_mb, a.grad_comm_dtype)
     opt = model.configure_optimizers(0.1, 6e-4, "cuda" if dev.startswith("cuda") else "cpu", False)
     loader = SyntheticTokens(a.B, a.T, cfg.vocab_size, info.rank, world, device=dev)
     fused = not a.no_fused_ce
@@ -74,7 +76,7 @@ def main():
         return loss / accum
 
     def step():
-        opt.zero_grad(set_to_none=True)
+        ddp_mod.zero_grad(dmodel, opt)
         with grad_accum.accumulation_scope():
             # micro-batch k+1's forward runs on a second stream beside micro-batch k's backward
             loss_acc = run_micro_batches(dmodel, loader.next_batch, accum, compute_loss,
@@ -134,6 +136,7 @@ def main():
                 "ops": "pytorch-reference" if a.reference_ops else "native-hip",
                 "gemm_table": "tunableop-gfx950" if tuned else "library-default",
                 "microbatch_overlap": not a.no_overlap,
+                "dp_impl": a.dp_impl if world > 1 else "none",
                 "final_loss": round(loss_v, 4),
             },
         }

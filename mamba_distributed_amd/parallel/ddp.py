@@ -46,17 +46,59 @@ def wrap_ddp(model: torch.nn.Module, info: DistInfo, bucket_cap_mb: float = 100.
     return m
 
 
+def wrap_data_parallel(model: torch.nn.Module, info: DistInfo, impl: str = "native", bucket_cap_mb: float = 100.0,
+                       grad_comm_dtype: str = "fp32", process_group=None):
+    """Data-parallel wrapper: ``impl="native"`` -> parallel/reducer.py (flat gradient buffer,
+    explicitly armed buckets; lets every micro-batch forward overlap the previous backward),
+    ``impl="ddp"`` -> torch DDP exactly as the reference uses it."""
+    if not info.ddp:
+        return model
+    if impl == "native":
+        from .reducer import wrap_reducer
+        return wrap_reducer(model, process_group, bucket_cap_mb, grad_comm_dtype)
+    assert impl == "ddp", impl
+    return wrap_ddp(model, info, bucket_cap_mb, grad_comm_dtype, process_group=process_group)
+
+
+def _reducer(model):
+    from .reducer import ReducedModule
+    return model.reducer if isinstance(model, ReducedModule) else None
+
+
 def unwrap(model):
-    return model.module if isinstance(model, DDP) else model
+    from .reducer import ReducedModule
+    return model.module if isinstance(model, (DDP, ReducedModule)) else model
+
+
+def zero_grad(model, optimizer) -> None:
+    """Start of an optimizer step: the native reducer keeps .grad as views of its flat buffer and
+    zeroes that; otherwise gradients are dropped (set_to_none) like the reference."""
+    r = _reducer(model)
+    if r is not None:
+        r.zero_grad()
+    else:
+        optimizer.zero_grad(set_to_none=True)
 
 
 def set_grad_sync(model, enabled: bool):
     """Per micro-step: True only on the last one (reference train.py:209-210).  Also tells the native
-    ops whether they may accumulate parameter gradients in place (ops/grad_accum.py)."""
+    ops whether they may accumulate parameter gradients in place (ops/grad_accum.py).  With the
+    native reducer, True arms its bucket hooks for the next backward; call ``finish_grad_sync``
+    after that backward."""
     from ..ops import grad_accum
     grad_accum.set_direct(not enabled)
     if isinstance(model, DDP):
         model.require_backward_grad_sync = enabled
+    r = _reducer(model)
+    if r is not None and enabled:
+        r.arm()
+
+
+def finish_grad_sync(model) -> None:
+    """Wait for the native reducer's bucket all-reduces (no-op for DDP / single process)."""
+    r = _reducer(model)
+    if r is not None:
+        r.finish()
 
 
 def params_in_sync(model, atol: float = 0.0) -> bool:

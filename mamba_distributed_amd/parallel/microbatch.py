@@ -13,8 +13,10 @@ Ordering rules, each enforced with one stream wait:
   * backward k waits for backward k-1 (they accumulate into the same ``p.grad``), captured BEFORE
     forward k+1 is enqueued behind backward k-1, so forward k+1 still runs beside backward k;
   * forward 1 waits for forward 0, which builds the step's bf16 weight casts (ops/grad_accum.py);
-  * the last micro-step runs on the caller's stream; under DDP its forward (which arms the
-    gradient-reduction hooks) is only issued after every earlier backward has been enqueued;
+  * the last micro-step runs on the caller's stream; under torch DDP its forward (which arms the
+    gradient-reduction hooks) is only issued after every earlier backward has been enqueued; the
+    native reducer (parallel/reducer.py) is armed right before the last backward instead, so with
+    it every forward -- the sync one included -- overlaps the previous backward;
   * the caller's stream waits for the other stream before returning.
 Every micro-step's reductions happen in the same order as in the sequential loop, so the gradients
 are bitwise identical (tests/test_kernels_gpu.py::test_microbatch_overlap_is_bitwise_identical).
@@ -40,14 +42,21 @@ def _set_ddp_sync(model, enabled: bool) -> None:
         model.require_backward_grad_sync = enabled
 
 
+def _reducer(model):
+    from .reducer import ReducedModule
+    return model.reducer if isinstance(model, ReducedModule) else None
+
+
 def run_micro_batches(model, next_batch: Callable, accum: int, compute_loss: Callable,
                       overlap: bool = True) -> torch.Tensor:
     """Forward + backward of ``accum`` micro-batches for ONE optimizer step; returns the summed
     (already 1/accum-scaled by ``compute_loss``) loss as an fp32 scalar tensor.
 
     ``next_batch() -> (x, y)``; ``compute_loss(x, y) -> loss`` runs the forward (with autocast).
-    Must be called inside ``grad_accum.accumulation_scope()``."""
+    Must be called inside ``grad_accum.accumulation_scope()``.  With the native reducer
+    (parallel/reducer.py) the gradients are averaged over the data-parallel group on return."""
     cuda = torch.cuda.is_available() and torch.cuda.is_initialized()
+    reducer = _reducer(model)
     if not overlap or not cuda or accum < 2:
         total = None
         for k in range(accum):
@@ -57,7 +66,11 @@ def run_micro_batches(model, next_batch: Callable, accum: int, compute_loss: Cal
             x, y = next_batch()
             loss = compute_loss(x, y)
             total = loss.detach().float() if total is None else total + loss.detach().float()
+            if sync and reducer is not None:
+                reducer.arm()
             loss.backward()
+        if reducer is not None:
+            reducer.finish()
         return total
     ddp = _is_ddp(model)
     main = torch.cuda.current_stream()
@@ -84,6 +97,8 @@ def run_micro_batches(model, next_batch: Callable, accum: int, compute_loss: Cal
         if early:
             forward(nxt)  # on streams[k-1] (or the other stream for k = 0): beside backward k
         grad_accum.set_direct(k != accum - 1)
+        if k == accum - 1 and reducer is not None:
+            reducer.arm()
         with torch.cuda.stream(streams[k]):
             losses[k].backward()
         if nxt < accum and not early:
@@ -91,6 +106,8 @@ def run_micro_batches(model, next_batch: Callable, accum: int, compute_loss: Cal
             streams[nxt].wait_stream(streams[k])
             forward(nxt)
     main.wait_stream(other)
+    if reducer is not None:
+        reducer.finish()
     total = losses[0].detach().float()
     for l in losses[1:]:
         total = total + l.detach().float()

@@ -1,0 +1,153 @@
+"""Native bucketed gradient all-reduce (the framework's replacement for torch DDP's reducer).
+
+Reference: ``DDP(model, device_ids=[local_rank])`` with default 25 MB buckets (train.py:86; SURVEY.md
+§2.6-2.7, C2-C3).  Same semantics -- parameters broadcast from rank 0 once, gradients averaged over
+the data-parallel group with bucketed all-reduces that overlap the last micro-step's backward -- but
+built around how this framework accumulates gradients:
+
+  * every parameter's ``.grad`` is a persistent view into ONE flat fp32 buffer laid out in reverse
+    registration order (about the order the backward produces them), so a bucket is a contiguous
+    slice of it: the all-reduce runs in place, with no copy into or out of bucket storage;
+  * the micro-steps accumulate straight into those views (ops/grad_accum.py's in-place weight
+    gradients and batched adds); ``zero_grad`` zeroes the buffer;
+  * the bucket hooks are armed explicitly for the sync micro-step only (``arm``).  Unlike DDP's
+    forward-armed reducer this lets the next micro-batch's forward -- including the sync one -- run
+    on a second stream beside the previous backward (parallel/microbatch.py), at every DP size;
+  * buckets launch strictly in index order on every rank (a bucket completes -> every consecutive
+    ready bucket from the next unlaunched one is launched), so ranks issue identical collective
+    sequences.  ``bucket_cap_mb`` defaults to 100 MB: on the 8-GPU xGMI mesh a 100 MB all-reduce
+    is well into the bandwidth-bound regime (scripts/comm_bench.py), and ~11 buckets for the 280M
+    model keep the exposed tail (the last bucket after the backward ends) short.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+class GradReducer:
+    def __init__(self, module: torch.nn.Module, process_group=None, bucket_cap_mb: float = 100.0,
+                 broadcast_params: bool = True, comm_dtype: str = "fp32"):
+        self.group = process_group
+        # "bf16" / "fp16": each bucket is pre-divided by the world size and cast before the
+        # all-reduce (half the bytes on the links), like DDP's bf16/fp16 compress hooks
+        self.comm_dtype = {"fp32": None, "bf16": torch.bfloat16, "fp16": torch.float16}[comm_dtype]
+        self.world = dist.get_world_size(process_group)
+        params = [p for p in module.parameters() if p.requires_grad]
+        assert params, "no trainable parameters"
+        dtypes = {p.dtype for p in params}
+        assert dtypes == {torch.float32}, f"GradReducer keeps fp32 gradients for fp32 parameters, got {dtypes}"
+        order = list(reversed(params))
+        total = sum(p.numel() for p in order)
+        self.flat = torch.zeros(total, dtype=torch.float32, device=params[0].device)
+        cap = max(1, int(bucket_cap_mb * 2**20 / 4))
+        self.buckets: List[tuple] = []  # (start, end, n_params)
+        self._bucket_of: Dict[int, int] = {}
+        self._offset: Dict[int, int] = {}
+        off, start, count = 0, 0, 0
+        for p in order:
+            self._offset[id(p)] = off
+            self._bucket_of[id(p)] = len(self.buckets)
+            off += p.numel()
+            count += 1
+            if off - start >= cap:
+                self.buckets.append((start, off, count))
+                start, count = off, 0
+        if count:
+            self.buckets.append((start, off, count))
+        self._params = params
+        for p in params:
+            self._attach(p)
+        self._hooks = [p.register_post_accumulate_grad_hook(self._hook) for p in params]
+        self._armed = False
+        self._left: List[int] = []
+        self._next = 0
+        self._works = []
+        if broadcast_params and self.world > 1:
+            src = dist.get_global_rank(process_group, 0) if process_group is not None else 0
+            with torch.no_grad():
+                for p in module.parameters():
+                    dist.broadcast(p.data, src=src, group=process_group)
+                for b in module.buffers():
+                    dist.broadcast(b.data, src=src, group=process_group)
+
+    def _attach(self, p) -> None:
+        off = self._offset[id(p)]
+        p.grad = self.flat[off:off + p.numel()].view_as(p)
+
+    # ------------------------------------------------------------------------------------------
+    def zero_grad(self) -> None:
+        """Zero every gradient, keeping (or restoring) the .grad views into the flat buffer."""
+        base = self.flat.data_ptr()
+        for p in self._params:
+            if p.grad is None or p.grad.data_ptr() != base + 4 * self._offset[id(p)]:
+                self._attach(p)
+        self.flat.zero_()
+
+    def arm(self) -> None:
+        """Call right before the sync micro-step's backward: its gradient hooks launch the buckets."""
+        self._armed = True
+        self._left = [n for _, _, n in self.buckets]
+        self._next = 0
+        self._works = []
+
+    def _hook(self, p) -> None:
+        if not self._armed:
+            return
+        self._left[self._bucket_of[id(p)]] -= 1
+        while self._next < len(self.buckets) and self._left[self._next] == 0:
+            s, e, _ = self.buckets[self._next]
+            self._works.append(self._all_reduce(self.flat[s:e]))
+            self._next += 1
+
+    def _all_reduce(self, t: torch.Tensor):
+        if self.world == 1:
+            return None
+        if self.comm_dtype is None:
+            return (dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True), None, None)
+        tmp = t.mul(1.0 / self.world).to(self.comm_dtype)
+        return (dist.all_reduce(tmp, op=dist.ReduceOp.SUM, group=self.group, async_op=True), t, tmp)
+
+    def finish(self) -> None:
+        """After the sync backward: launch any bucket not launched yet, wait for all, average."""
+        if not self._armed:
+            return
+        while self._next < len(self.buckets):  # parameters that got no gradient this step
+            s, e, _ = self.buckets[self._next]
+            self._works.append(self._all_reduce(self.flat[s:e]))
+            self._next += 1
+        for w in self._works:
+            if w is not None:
+                w[0].wait()
+                if w[1] is not None:
+                    w[1].copy_(w[2])
+        if self.world > 1 and self.comm_dtype is None:
+            self.flat.mul_(1.0 / self.world)
+        self._armed = False
+        self._works = []
+
+    def remove(self) -> None:
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+
+
+class ReducedModule(torch.nn.Module):
+    """Wrapper exposing ``.module`` (like DDP, so callers that unwrap keep working) and ``.reducer``."""
+
+    def __init__(self, module: torch.nn.Module, reducer: GradReducer):
+        super().__init__()
+        self.module = module
+        self.reducer = reducer
+
+    def forward(self, *args, **kwargs):
+        return self.module(*args, **kwargs)
+
+
+def wrap_reducer(module: torch.nn.Module, process_group=None, bucket_cap_mb: float = 100.0,
+                 comm_dtype: str = "fp32") -> Optional[ReducedModule]:
+    if not (dist.is_available() and dist.is_initialized()):
+        return None
+    return ReducedModule(module, GradReducer(module, process_group, bucket_cap_mb, comm_dtype=comm_dtype))

@@ -71,6 +71,7 @@ class TrainArgs:
     backend: str = "auto"
     bucket_cap_mb: float = 100.0
     grad_comm_dtype: str = "fp32"
+    dp_impl: str = "native"              # "native" bucketed reducer (parallel/reducer.py) or "ddp"
     resume: bool = False
     fused_ce: bool = True
     save_optimizer: bool = True
@@ -144,10 +145,12 @@ class Trainer:
             parallelize(self.raw_model, self.groups, a.sequence_parallel)
             grp = self.groups.dp_cp_group
             ddp_info = self.info if self.groups.dp * self.groups.cp > 1 else None
-            self.model = (ddp_mod.wrap_ddp(self.raw_model, ddp_info, a.bucket_cap_mb, a.grad_comm_dtype,
-                                           process_group=grp) if ddp_info is not None else self.raw_model)
+            self.model = (ddp_mod.wrap_data_parallel(self.raw_model, ddp_info, a.dp_impl, a.bucket_cap_mb,
+                                                     a.grad_comm_dtype, process_group=grp)
+                          if ddp_info is not None else self.raw_model)
         else:
-            self.model = ddp_mod.wrap_ddp(self.raw_model, self.info, a.bucket_cap_mb, a.grad_comm_dtype)
+            self.model = ddp_mod.wrap_data_parallel(self.raw_model, self.info, a.dp_impl, a.bucket_cap_mb,
+                                                    a.grad_comm_dtype)
         self.optimizer = self.raw_model.configure_optimizers(a.weight_decay, a.max_lr, self.device_type, self.master)
         if ck is not None:
             self._resume_rest(ck)
@@ -235,7 +238,7 @@ class Trainer:
 
     def train_step(self, step):
         self.model.train()
-        self.optimizer.zero_grad(set_to_none=True)
+        ddp_mod.zero_grad(self.model, self.optimizer)
         def compute_loss(x, y):
             with self._autocast():
                 _, loss = self.model(x, y, return_logits=not self.a.fused_ce)

@@ -56,14 +56,17 @@ def _losses(stdout):
     return [float(l.split("loss: ")[1].split(" ")[0]) for l in stdout.splitlines() if l.startswith("step ")]
 
 
-def test_ddp_gloo_world2_matches_single_process(tmp_path):
+@pytest.mark.parametrize("dp_impl,bucket_mb", [("native", "100"), ("native", "0.05"), ("ddp", "100")])
+def test_ddp_gloo_world2_matches_single_process(tmp_path, dp_impl, bucket_mb):
+    """Both data-parallel implementations (parallel/reducer.py, torch DDP) -- and the native one with
+    tiny buckets, so many in-order bucket launches happen during the backward -- match 1 process."""
     data = str(tmp_path / "data")
     write_synthetic_shards(data, n_train=1, n_val=1, tokens_per_shard=1 << 14, vocab_size=50304)
     sd_single, out_single = _run_single(tmp_path, data, B=4)
     log = str(tmp_path / "ddp")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "train.py"), *COMMON,
-           "--B", "2", "--data-root", data, "--log-dir", log]
+           "--B", "2", "--data-root", data, "--log-dir", log, "--dp-impl", dp_impl, "--bucket-cap-mb", bucket_mb]
     r = subprocess.run(cmd, capture_output=True, text=True, env=_env(), timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     assert "=> calculated gradient accumulation steps: 2" in r.stdout
