@@ -42,6 +42,8 @@ def main():
     p.add_argument("--no-tuned-gemms", action="store_true", help="library-default GEMM solutions")
     p.add_argument("--profile-steps", type=int, default=0, help="torch.profiler trace of N extra steps")
     p.add_argument("--no-overlap", action="store_true", help="run the micro-steps strictly one after another")
+    p.add_argument("--trace-loss", action="store_true",
+                   help="diagnostics: print every step's loss and grad norm (syncs each step; not for timing)")
     p.add_argument("--dp-impl", default="native", choices=["native", "ddp"],
                    help="gradient all-reduce: native bucketed reducer (parallel/reducer.py) or torch DDP")
     a = p.parse_args()
@@ -82,8 +84,10 @@ def main():
             loss_acc = run_micro_batches(dmodel, loader.next_batch, accum, compute_loss,
                                          overlap=not a.no_overlap)
         all_reduce_avg(loss_acc)
-        torch.nn.utils.clip_grad_norm_(dmodel.parameters(), 1.0)
+        norm = torch.nn.utils.clip_grad_norm_(dmodel.parameters(), 1.0)
         opt.step()
+        if a.trace_loss and info.master:
+            print(f"step loss {loss_acc.item():.5f} grad_norm {norm.item():.4f}", flush=True)
         return loss_acc
 
     for _ in range(a.warmup):

@@ -10,6 +10,7 @@ conv, scan) leave idle:
     stream B:       | (wait fwd0) fwd1 | (wait bwd0) bwd1 | fwd3 ...
 
 Ordering rules, each enforced with one stream wait:
+  * the other stream waits for the caller's stream on entry (the previous optimizer step);
   * backward k waits for backward k-1 (they accumulate into the same ``p.grad``), captured BEFORE
     forward k+1 is enqueued behind backward k-1, so forward k+1 still runs beside backward k;
   * forward 1 waits for forward 0, which builds the step's bf16 weight casts (ops/grad_accum.py);
@@ -79,6 +80,11 @@ def run_micro_batches(model, next_batch: Callable, accum: int, compute_loss: Cal
     if other is None:
         other = _OTHER[dev] = torch.cuda.Stream(device=dev)
     streams = [main if (accum - 1 - k) % 2 == 0 else other for k in range(accum)]
+    # everything the caller queued on ``main`` (the previous optimizer step updating the weights and
+    # reading the gradients that zero_grad just released) precedes the first forward when that runs
+    # on the other stream (even ``accum``): without this wait, blocks freed by zero_grad are handed
+    # to forward 0's activations while AdamW may still be reading them as gradients
+    other.wait_stream(main)
     losses = [None] * accum
 
     def forward(k):

@@ -1,0 +1,81 @@
+"""torchrun worker for tests/test_kernels_gpu.py::test_native_reducer_two_ranks_one_gpu (no test_ prefix:
+not collected by pytest).
+
+Two gloo ranks share cuda:0 (RCCL refuses two ranks on one device; gloo moves CUDA tensors through
+host memory on its own streams, ordered against the caller's stream exactly as RCCL's are).  Each
+rank runs ONE optimizer step's micro-batches through parallel/reducer.py with the two-stream
+micro-batch overlap (parallel/microbatch.py) and tiny buckets, so many bucket all-reduces launch
+while the sync backward is still producing gradients.  A bucket launched before its gradients were
+accumulated would miss that micro-step's contribution (an O(1/accum) relative error); the averaged
+gradients must instead match the single-process accumulation over the whole global batch.
+"""
+import argparse
+import copy
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from mamba_distributed_amd import LMHeadModel, MambaConfig  # noqa: E402
+from mamba_distributed_amd.ops import grad_accum  # noqa: E402
+from mamba_distributed_amd.parallel import ddp as ddp_mod  # noqa: E402
+from mamba_distributed_amd.parallel.microbatch import run_micro_batches  # noqa: E402
+from mamba_distributed_amd.parallel.reducer import wrap_reducer  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--layer", default="Mamba2")
+    ap.add_argument("--accum", type=int, default=3)
+    ap.add_argument("--bucket-mb", type=float, default=0.25)
+    ap.add_argument("--comm-dtype", default="fp32")
+    a = ap.parse_args()
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    dev = "cuda:0"
+    torch.cuda.set_device(0)
+    torch.manual_seed(0)
+    cfg = MambaConfig(d_model=256, n_layer=4, vocab_size=1024, ssm_cfg={"layer": a.layer})
+    ref = LMHeadModel(cfg, device=dev)
+    model = copy.deepcopy(ref)
+    n_micro = a.accum * world
+    g = torch.Generator(device=dev).manual_seed(1)
+    data = [(torch.randint(0, 1024, (2, 256), device=dev, generator=g),
+             torch.randint(0, 1024, (2, 256), device=dev, generator=g)) for _ in range(n_micro)]
+
+    def loss_fn(m, n):
+        def f(x, y):
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                return m(x, y, return_logits=False)[1] / n
+        return f
+
+    # single-process reference: every micro-batch of the global batch, strictly sequential
+    it = iter(data)
+    with grad_accum.accumulation_scope():
+        run_micro_batches(ref, lambda: next(it), n_micro, loss_fn(ref, n_micro), overlap=False)
+
+    dm = wrap_reducer(model, None, a.bucket_mb, comm_dtype=a.comm_dtype)
+    assert len(dm.reducer.buckets) > 4, len(dm.reducer.buckets)
+    mine = iter(data[rank::world])
+    for rep in range(2):  # a second step checks zero_grad + re-arming
+        ddp_mod.zero_grad(dm, None)
+        with grad_accum.accumulation_scope():
+            run_micro_batches(dm, lambda: next(mine), a.accum, loss_fn(dm, a.accum), overlap=True)
+        torch.cuda.synchronize()
+        tol = 2e-3 if a.comm_dtype == "fp32" else 2e-2
+        worst = 0.0
+        for (k, p), (_, q) in zip(model.named_parameters(), ref.named_parameters()):
+            err = ((p.grad - q.grad).norm() / (q.grad.norm() + 1e-12)).item()
+            worst = max(worst, err)
+            assert err < tol, (rep, k, err)
+        print(f"rank {rank} step {rep}: buckets={len(dm.reducer.buckets)} worst_rel_err={worst:.2e}", flush=True)
+        mine = iter(data[rank::world])
+    dist.destroy_process_group()
+    print(f"rank {rank} OK", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -546,3 +546,68 @@ def test_microbatch_overlap_is_bitwise_identical(cuda, layer):
     assert torch.equal(l0, l1), (l0, l1)
     for k in g0:
         assert torch.equal(g0[k], g1[k]), k
+
+
+@pytest.mark.parametrize("layer,comm", [("Mamba2", "fp32"), ("Mamba1", "fp32"), ("Mamba2", "bf16")])
+def test_native_reducer_two_ranks_one_gpu(cuda, layer, comm):
+    """parallel/reducer.py on real HIP streams: two gloo ranks on cuda:0, overlapped micro-batches,
+    tiny buckets; the averaged gradients match the single-process global-batch gradients
+    (tests/reducer_worker.py)."""
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(root, "tests", "reducer_worker.py"), "--layer", layer, "--comm-dtype", comm]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110,
+                       env=dict(os.environ, PYTHONPATH=root, OMP_NUM_THREADS="4"))
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    assert r.stdout.count("OK") == 2, r.stdout
+
+
+@pytest.mark.parametrize("accum", [4, 5])
+def test_microbatch_overlap_across_optimizer_steps(cuda, accum):
+    """Several full optimizer steps (zero_grad -> overlapped micro-steps -> clip -> fused AdamW) with
+    an even and an odd micro-step count: the parameters stay bitwise equal to the sequential loop's.
+    With an even count forward 0 runs on the second stream, which must wait for the previous
+    AdamW step (it reads the weights, and zero_grad has just released the gradient blocks)."""
+    from mamba_distributed_amd import LMHeadModel, MambaConfig
+    from mamba_distributed_amd.ops import grad_accum
+    from mamba_distributed_amd.parallel.microbatch import run_micro_batches
+    cfg = MambaConfig(d_model=256, n_layer=4, vocab_size=1024, ssm_cfg={"layer": "Mamba2"})
+    g = torch.Generator(device=cuda).manual_seed(1)
+    steps = 4
+    data = [(torch.randint(0, 1024, (2, 256), device=cuda, generator=g),
+             torch.randint(0, 1024, (2, 256), device=cuda, generator=g)) for _ in range(accum * steps)]
+
+    def train(overlap):
+        torch.manual_seed(0)
+        m = LMHeadModel(cfg, device=cuda)
+        opt = m.configure_optimizers(0.1, 3e-3, "cuda", False)
+        it = iter(data)
+
+        def loss_fn(x, y):
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                return m(x, y, return_logits=False)[1] / accum
+
+        losses = []
+        for _ in range(steps):
+            opt.zero_grad(set_to_none=True)
+            with grad_accum.accumulation_scope():
+                losses.append(run_micro_batches(m, lambda: next(it), accum, loss_fn, overlap=overlap))
+            torch.nn.utils.clip_grad_norm_(m.parameters(), 1.0)
+            opt.step()
+        torch.cuda.synchronize()
+        return torch.stack(losses), {k: p.detach().clone() for k, p in m.named_parameters()}
+
+    l0, p0 = train(False)
+    l1, p1 = train(True)
+    assert torch.isfinite(l0).all(), l0
+    assert torch.equal(l0, l1), (l0, l1)
+    for k in p0:
+        assert torch.equal(p0[k], p1[k]), k
