@@ -413,7 +413,7 @@ void selscan_common(mamba_amd::SelScanArgs& a, const Tensor& u, const Tensor& de
   TORCH_CHECK(a.N == 16 || a.N == 8 || a.N == 4, "native selective scan supports d_state 4/8/16");
   TORCH_CHECK(a.D % a.G == 0 && Bm.size(3) == a.L && Cm.sizes() == Bm.sizes(), "B/C shape");
   a.dtype = dcode(u.scalar_type());
-  a.Kc = 64;
+  a.Kc = mamba_amd::selscan_bwd_kc();
   a.softplus = softplus;
   auto v8 = [&](const Tensor& t, int64_t s0, int64_t s1) {
     return a.dtype == mamba_amd::kBF16 && (uintptr_t)t.data_ptr() % 16 == 0 && s0 % 8 == 0 && s1 % 8 == 0;

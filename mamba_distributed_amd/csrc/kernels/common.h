@@ -83,10 +83,18 @@ __device__ __forceinline__ float softplusf_(float x) { return x <= 20.f ? log1pf
 // softplus with hardware exp/log: log1p(y) = log(1+y) * y / ((1+y)-1) recovers the bits of y lost in
 // 1+y, so the result keeps ~fp32 relative accuracy for very negative x (used where libm log1pf's
 // register footprint would cost occupancy)
+// Branch-free: softplus(x) = max(x, 0) + log1p(e^{-|x|}) -- inside unrolled per-element loops a
+// branchy form costs an exec-mask diamond per element.
+// Hardware v_exp_f32 / v_log_f32 (base 2) directly: the arguments never reach the denormal range
+// the library wrappers guard against (-|x| log2e <= 0 -> y in (0, 1]; u in [1, 2]).
 __device__ __forceinline__ float softplus_fast(float x) {
-  if (x > 20.f) return x;
-  const float y = __expf(x), u = 1.f + y;
-  return u == 1.f ? y : __logf(u) * y * __builtin_amdgcn_rcpf(u - 1.f);
+  const float y = __builtin_amdgcn_exp2f(-1.4426950408889634f * fabsf(x)), u = 1.f + y;
+  const float l = __builtin_amdgcn_logf(u) * 0.6931471805599453f * y * __builtin_amdgcn_rcpf(u - 1.f);
+  return fmaxf(x, 0.f) + (u == 1.f ? y : l);
+}
+// logistic with the hardware exp2 (exp2 -> +inf for very negative x gives rcp(inf) = 0)
+__device__ __forceinline__ float sigmoid_fast(float x) {
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-1.4426950408889634f * x));
 }
 
 // XCD-aware remap of a linear block id (bijective for any grid size; MI355X has 8 XCDs and

@@ -46,6 +46,7 @@ struct SSMUpdateArgs {
 hipError_t launch_selscan_fwd(const SelScanArgs& a, hipStream_t st);
 hipError_t launch_selscan_bwd(const SelScanArgs& a, hipStream_t st);
 int selscan_ntiles(int L);
+int selscan_bwd_kc();  // channels per backward workgroup (SelScanArgs::Kc)
 hipError_t launch_ssm_update(const SSMUpdateArgs& a, hipStream_t st);
 
 }  // namespace mamba_amd

@@ -20,9 +20,10 @@ namespace mamba_amd {
 
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr int SF_IT = 16, SF_T = 64 * SF_IT;  // forward: one wave walks a row in 1024-step tiles
-constexpr int SB_IT = 4, SB_T = 64 * SB_IT;   // backward tiles; also the saved-carry granularity
+constexpr int SB_IT = 8, SB_T = 64 * SB_IT;   // backward tiles; also the saved-carry granularity
 constexpr int SB_W = 4;                       // waves per backward workgroup
-constexpr int SB_KC = 64;                     // channels per backward workgroup
+constexpr int SB_KC = 32;                     // channels per backward workgroup (3 rounds of 2 WGs/CU at 280M)
+static_assert(SF_T % SB_T == 0, "forward tiles must hold whole backward tiles");
 
 // ---- item I/O: IT consecutive steps of one (b, d) row (16-B vectors when aligned) -------------
 // VEC: every row segment is a whole number of 16-B vectors inside [0, L) or entirely outside
@@ -321,13 +322,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void s
           const float A2 = An * kLog2e;
           float Bv[IT], Cv[IT], av[IT], hs[IT];
           if (g == g0) {
-            static_assert(IT == 4, "LDS B/C reads are one 8-byte read per lane");
-            const uint2 bq = *reinterpret_cast<const uint2*>(&BCs[0][n][lane * IT]);
-            const uint2 cq = *reinterpret_cast<const uint2*>(&BCs[1][n][lane * IT]);
-            Bv[0] = __uint_as_float(bq.x << 16); Bv[1] = __uint_as_float(bq.x & 0xffff0000u);
-            Bv[2] = __uint_as_float(bq.y << 16); Bv[3] = __uint_as_float(bq.y & 0xffff0000u);
-            Cv[0] = __uint_as_float(cq.x << 16); Cv[1] = __uint_as_float(cq.x & 0xffff0000u);
-            Cv[2] = __uint_as_float(cq.y << 16); Cv[3] = __uint_as_float(cq.y & 0xffff0000u);
+            static_assert(IT == 8, "LDS B/C reads are one 16-byte read per lane");
+            ld8bf(&BCs[0][n][lane * IT], Bv);
+            ld8bf(&BCs[1][n][lane * IT], Cv);
           } else {
             load_items<VEC, T, IT>(Bb + (int64_t)n * a.sBn, tl, a.L, Bv);
             load_items<VEC, T, IT>(Cb + (int64_t)n * a.sCn, tl, a.L, Cv);
@@ -476,8 +473,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void s
       } else {
         // finish item-parallel: thread j <-> step tile*SB_T + j
         float dDp = 0.f, dbp = 0.f;
-        if (threadIdx.x < SB_T) {
-          const int j = threadIdx.x, t = tile * SB_T + j;
+        for (int j = threadIdx.x; j < SB_T; j += 64 * SB_W) {  // SB_T = 2 x the workgroup size
+          const int t = tile * SB_T + j;
           if (t < a.L) {
             float sdu = 0.f, sdd = 0.f, sy = 0.f;
 #pragma unroll
@@ -498,8 +495,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void s
             st(((T*)a.du_) + (int64_t)b * a.sdub + (int64_t)d * a.sdud + t, fmaf(Dd, dyv, sdu));
             st(((T*)a.ddelta_) + (int64_t)b * a.sddb + (int64_t)d * a.sddd + t, ddl);
             if (zrow && a.dz_) st(((T*)a.dz_) + (int64_t)b * a.sdzb + (int64_t)d * a.sdzd + t, dz);
-            dDp = dyv * uu;
-            dbp = ddl;
+            dDp = fmaf(dyv, uu, dDp);
+            dbp += ddl;
           }
         }
         dDp = wave_sum_dpp(dDp);
@@ -519,8 +516,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void s
         float* pb = a.part_dB + (((int64_t)b * ndg + dg) * N + n) * a.L;
         float* pc = a.part_dC + (((int64_t)b * ndg + dg) * N + n) * a.L;
         if (tl + IT <= a.L && (a.L % 4) == 0) {
-          *reinterpret_cast<float4*>(pb + tl) = make_float4(accB[nn][0], accB[nn][1], accB[nn][2], accB[nn][3]);
-          *reinterpret_cast<float4*>(pc + tl) = make_float4(accC[nn][0], accC[nn][1], accC[nn][2], accC[nn][3]);
+#pragma unroll
+          for (int q = 0; q < IT / 4; ++q) {
+            *reinterpret_cast<float4*>(pb + tl + 4 * q) =
+                make_float4(accB[nn][4 * q], accB[nn][4 * q + 1], accB[nn][4 * q + 2], accB[nn][4 * q + 3]);
+            *reinterpret_cast<float4*>(pc + tl + 4 * q) =
+                make_float4(accC[nn][4 * q], accC[nn][4 * q + 1], accC[nn][4 * q + 2], accC[nn][4 * q + 3]);
+          }
         } else {
 #pragma unroll
           for (int i = 0; i < IT; ++i)
@@ -528,6 +530,311 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void s
               pb[tl + i] = accB[nn][i];
               pc[tl + i] = accC[nn][i];
             }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int v = threadIdx.x; v < nch * N; v += 64 * SB_W)
+    a.part_dA[((int64_t)b * a.D + d0 + v / N) * N + v % N] = dAacc[v / N][v % N];
+  for (int v = threadIdx.x; v < nch; v += 64 * SB_W) {
+    float sD = 0.f, sb = 0.f;
+#pragma unroll
+    for (int q = 0; q < SB_W; ++q) {
+      sD += dDacc[v][q];
+      sb += dbacc[v][q];
+    }
+    a.part_dD[(int64_t)b * a.D + d0 + v] = sD;
+    a.part_dbias[(int64_t)b * a.D + d0 + v] = sb;
+  }
+}
+
+// ---- backward, bf16 fast path ------------------------------------------------------------------
+// Same decomposition as selscan_bwd_k (a 4-wave workgroup owns SB_KC channels of one batch row and
+// walks the 512-step tiles backwards; wave w owns states [w NW, (w+1) NW)), reorganised so the VALU
+// work per state-step is close to the arithmetic of the recurrence itself:
+//  * 8 steps per lane (the two DPP scans per state and channel are amortised over 512 steps);
+//  * the NW states of a wave are fully unrolled, so the register-resident dB/dC accumulators are
+//    indexed statically (the runtime state loop of the generic kernel had to rotate them);
+//  * xb_t = dt_t u_t B_t is computed once and reused by the replay and by the adjoint, whose terms
+//    share S1_t = sum_n lam B:  du = dt S1 + D dy,  ddelta = (u S1 + sum_n A_n lam (h_t - xb_t)) sp',
+//    dA_n = sum_t dt lam (h_t - xb_t)   (lam (h_t - xb_t) = lam a_t h_{t-1});
+//  * the sums over states (S1, S2, y) meet in ONE single-buffered LDS block, and all four waves
+//    finish the channel together, wave w taking steps 2w, 2w+1 of every lane's segment;
+//  * B, C of the tile sit in LDS as bf16 [n][t]: one 16-B read per lane per state.
+// LDS ~66 KB and <= 256 VGPRs: two workgroups per CU.  Deterministic: every partial has one writer.
+template <int N>
+__global__ __launch_bounds__(256) void selscan_bwd_fast_k(SelScanArgs a) {
+  constexpr int NW = N / SB_W;
+  constexpr int IT = SB_IT;
+  static_assert(NW >= 1 && IT == 8, "bf16 fast path: 8 steps per lane, >= 1 state per wave");
+  __shared__ __attribute__((aligned(16))) float part[SB_W][3][SB_T];
+  __shared__ __attribute__((aligned(16))) bf16_t BCs[2][N][SB_T];
+  __shared__ float lamc[SB_KC][N];
+  __shared__ float dAacc[SB_KC][N];
+  __shared__ float dDacc[SB_KC][SB_W], dbacc[SB_KC][SB_W];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int dg = blockIdx.x, b = blockIdx.y;
+  const int d0 = dg * SB_KC, nch = min(SB_KC, a.D - d0);
+  const int ntl = (a.L + SB_T - 1) / SB_T;
+  const int ndg = (a.D + SB_KC - 1) / SB_KC;
+  const int dpg = a.D / a.G;
+  for (int v = threadIdx.x; v < SB_KC * N; v += 64 * SB_W) {
+    (&lamc[0][0])[v] = 0.f;
+    (&dAacc[0][0])[v] = 0.f;
+  }
+  for (int v = threadIdx.x; v < SB_KC * SB_W; v += 64 * SB_W) {
+    (&dDacc[0][0])[v] = 0.f;
+    (&dbacc[0][0])[v] = 0.f;
+  }
+  const bf16_t* ub = ((const bf16_t*)a.u_) + (int64_t)b * a.sub;
+  const bf16_t* db_ = ((const bf16_t*)a.delta_) + (int64_t)b * a.sdb;
+  const bf16_t* gb = ((const bf16_t*)a.dout_) + (int64_t)b * a.sgb;
+  const bf16_t* zb = a.z_ ? ((const bf16_t*)a.z_) + (int64_t)b * a.szb : nullptr;
+  for (int tile = ntl - 1; tile >= 0; --tile) {
+    const int tl = tile * SB_T + lane * IT;
+    const bool inr = tl < a.L;  // L % 8 == 0: a lane's 8 steps are all inside or all outside
+    float accB[NW][IT], accC[NW][IT];
+#pragma unroll
+    for (int nn = 0; nn < NW; ++nn)
+#pragma unroll
+      for (int i = 0; i < IT; ++i) accB[nn][i] = accC[nn][i] = 0.f;
+    const int g0 = d0 / dpg;
+    __syncthreads();  // previous tile's readers of BCs are done
+    {
+      const bf16_t* Bb = ((const bf16_t*)a.Bm_) + (int64_t)b * a.sBb + (int64_t)g0 * a.sBg;
+      const bf16_t* Cb = ((const bf16_t*)a.Cm_) + (int64_t)b * a.sCb + (int64_t)g0 * a.sCg;
+      for (int v = threadIdx.x; v < N * (SB_T / 8); v += 64 * SB_W) {
+        const int n = v / (SB_T / 8), c8 = (v % (SB_T / 8)) * 8, t = tile * SB_T + c8;
+        uint4 bq = make_uint4(0, 0, 0, 0), cq = bq;
+        if (t < a.L) {
+          bq = *reinterpret_cast<const uint4*>(Bb + (int64_t)n * a.sBn + t);
+          cq = *reinterpret_cast<const uint4*>(Cb + (int64_t)n * a.sCn + t);
+        }
+        *reinterpret_cast<uint4*>(&BCs[0][n][c8]) = bq;
+        *reinterpret_cast<uint4*>(&BCs[1][n][c8]) = cq;
+      }
+    }
+    __syncthreads();
+    uint4 nu = make_uint4(0, 0, 0, 0), nd = nu, ng = nu, nz = nu;
+    float nh[NW], nA[NW];
+    auto fetch = [&](int k) {
+      if (k < nch) {
+        const int d = d0 + k;
+        if (inr) {
+          nu = *reinterpret_cast<const uint4*>(ub + (int64_t)d * a.sud + tl);
+          nd = *reinterpret_cast<const uint4*>(db_ + (int64_t)d * a.sdd + tl);
+          ng = *reinterpret_cast<const uint4*>(gb + (int64_t)d * a.sgd + tl);
+          if (zb) nz = *reinterpret_cast<const uint4*>(zb + (int64_t)d * a.szd + tl);
+        }
+        const float* cp = a.carries + (((int64_t)b * a.D + d) * ntl + tile) * N + w * NW;
+#pragma unroll
+        for (int nn = 0; nn < NW; ++nn) {
+          nh[nn] = cp[nn];
+          nA[nn] = a.A[d * N + w * NW + nn];
+        }
+      }
+    };
+    fetch(0);
+    for (int k = 0; k < nch; ++k) {
+      const int d = d0 + k;
+      const int g = d / dpg;
+      // everything this channel reads from memory is in flight before the next channel's prefetch is
+      // issued, so the waits below never cover the prefetch (vmcnt counts in issue order)
+      const float bias = a.delta_bias ? a.delta_bias[d] : 0.f;
+      const float Dd = a.D_ ? a.D_[d] : 0.f;
+      // the bf16 pairs of steps 2w, 2w+1 this wave finishes stay live packed (4 registers); the fp32
+      // working set is dl, dy, dlu
+      const uint4 cu = nu, craw = nd, cg = ng, cz = nz;
+      unsigned wu = cu.x, wr = craw.x, wg = cg.x, wz = cz.x;
+#pragma unroll
+      for (int ww = 1; ww < SB_W; ++ww)
+        if (w == ww) {
+          wu = (&cu.x)[ww]; wr = (&craw.x)[ww]; wg = (&cg.x)[ww]; wz = (&cz.x)[ww];
+        }
+      float hc[NW], Ac[NW];
+#pragma unroll
+      for (int nn = 0; nn < NW; ++nn) {
+        hc[nn] = nh[nn];
+        Ac[nn] = nA[nn];
+      }
+      fetch(k + 1);
+      float dl[IT], dy[IT], dlu[IT];
+      {
+        float u[IT], raw[IT], go[IT], zz[IT];
+        ld8bf(reinterpret_cast<const bf16_t*>(&cu), u);
+        ld8bf(reinterpret_cast<const bf16_t*>(&craw), raw);
+        ld8bf(reinterpret_cast<const bf16_t*>(&cg), go);
+        ld8bf(reinterpret_cast<const bf16_t*>(&cz), zz);
+#pragma unroll
+        for (int i = 0; i < IT; ++i) {  // branch-free: both forms computed, then selected
+          const float v = raw[i] + bias;
+          const float sp = softplus_fast(v);
+          dl[i] = inr ? (a.softplus ? sp : v) : 0.f;
+          const float gate = zz[i] * sigmoid_fast(zz[i]);
+          dy[i] = go[i] * (zb ? gate : 1.f);
+          dlu[i] = dl[i] * u[i];
+        }
+      }
+      float S1[IT], S2[IT], yv[IT];
+#pragma unroll
+      for (int i = 0; i < IT; ++i) S1[i] = S2[i] = yv[i] = 0.f;
+      // runtime loop over the wave's states (one state's working set live at a time); its dB / dC
+      // contributions are added to the statically indexed accumulators through a uniform switch
+#pragma unroll 1
+      for (int nn = 0; nn < NW; ++nn) {
+        const int n = w * NW + nn;
+        float hcn = hc[0], An = Ac[0];
+#pragma unroll
+        for (int q = 1; q < NW; ++q)
+          if (nn == q) {
+            hcn = hc[q];
+            An = Ac[q];
+          }
+        const float A2 = An * kLog2e;
+        float Bv[IT], Cv[IT], av[IT], xb[IT], hs[IT], cB[IT], cC[IT];
+        if (g == g0) {
+          ld8bf(&BCs[0][n][lane * IT], Bv);
+          ld8bf(&BCs[1][n][lane * IT], Cv);
+        } else {
+          load_items<true, bf16_t, IT>(((const bf16_t*)a.Bm_) + (int64_t)b * a.sBb + (int64_t)g * a.sBg +
+                                       (int64_t)n * a.sBn, tl, a.L, Bv);
+          load_items<true, bf16_t, IT>(((const bf16_t*)a.Cm_) + (int64_t)b * a.sCb + (int64_t)g * a.sCg +
+                                       (int64_t)n * a.sCn, tl, a.L, Cv);
+        }
+        // forward replay from the saved tile-start state
+        float ca = 1.f, cb = 0.f;
+#pragma unroll
+        for (int i = 0; i < IT; ++i) {
+          av[i] = __builtin_amdgcn_exp2f(dl[i] * A2);
+          xb[i] = dlu[i] * Bv[i];
+          cb = fmaf(av[i], cb, xb[i]);
+          ca *= av[i];
+        }
+        const float prod = ca;
+        scan_prefix(ca, cb);
+        const float hend = fmaf(ca, hcn, cb);
+        float h = dppf<0x138>(hcn, hend);  // wave_shr:1 -> state before this lane's first step
+#pragma unroll
+        for (int i = 0; i < IT; ++i) {
+          h = fmaf(av[i], h, xb[i]);
+          hs[i] = h;
+          yv[i] = fmaf(Cv[i], h, yv[i]);
+        }
+        // adjoint x_t = a_t (dy_t C_t + x_{t+1}) as a suffix scan of affine maps
+        float ma = prod, mb = 0.f;
+#pragma unroll
+        for (int i = IT - 1; i >= 0; --i) mb = av[i] * fmaf(dy[i], Cv[i], mb);
+        scan_suffix(ma, mb);
+        const float xc = lamc[k][n];
+        const float xfirst = fmaf(ma, xc, mb);
+        float x = dppf<0x130>(xc, xfirst);  // wave_shl:1 -> adjoint after this lane's last step
+        const float xnew = readlanef(xfirst, 0);
+        float dAp = 0.f;
+#pragma unroll
+        for (int i = IT - 1; i >= 0; --i) {
+          const float lam = fmaf(dy[i], Cv[i], x);
+          x = av[i] * lam;
+          cB[i] = lam * dlu[i];
+          cC[i] = dy[i] * hs[i];
+          S1[i] = fmaf(lam, Bv[i], S1[i]);
+          const float t1 = lam * (hs[i] - xb[i]);  // lam a_t h_{t-1}
+          S2[i] = fmaf(An, t1, S2[i]);
+          dAp = fmaf(dl[i], t1, dAp);
+        }
+#pragma unroll
+        for (int q = 0; q < NW; ++q)
+          if (nn == q) {
+#pragma unroll
+            for (int i = 0; i < IT; ++i) {
+              accB[q][i] += cB[i];
+              accC[q][i] += cC[i];
+            }
+          }
+        dAp = wave_sum_dpp(dAp);
+        if (lane == 0) {
+          lamc[k][n] = xnew;
+          dAacc[k][n] += dAp;
+        }
+      }
+      float* pw = &part[w][0][lane * IT];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        *reinterpret_cast<float4*>(pw + 4 * q) = make_float4(S1[4 * q], S1[4 * q + 1], S1[4 * q + 2], S1[4 * q + 3]);
+        *reinterpret_cast<float4*>(pw + SB_T + 4 * q) =
+            make_float4(S2[4 * q], S2[4 * q + 1], S2[4 * q + 2], S2[4 * q + 3]);
+        *reinterpret_cast<float4*>(pw + 2 * SB_T + 4 * q) =
+            make_float4(yv[4 * q], yv[4 * q + 1], yv[4 * q + 2], yv[4 * q + 3]);
+      }
+      __syncthreads();
+      // finish the channel: wave w takes steps 2w, 2w+1 of every lane (uniform select of the pair)
+      float2 su = make_float2(0.f, 0.f), s2 = su, sy = su;
+#pragma unroll
+      for (int v = 0; v < SB_W; ++v) {
+        const float2 p0 = *reinterpret_cast<const float2*>(&part[v][0][lane * IT + 2 * w]);
+        const float2 p1 = *reinterpret_cast<const float2*>(&part[v][1][lane * IT + 2 * w]);
+        const float2 p2 = *reinterpret_cast<const float2*>(&part[v][2][lane * IT + 2 * w]);
+        su.x += p0.x; su.y += p0.y;
+        s2.x += p1.x; s2.y += p1.y;
+        sy.x += p2.x; sy.y += p2.y;
+      }
+      float pu[2], pdl[2], pdy[2], pr[2], pg[2], pz[2];
+      {
+        pu[0] = __uint_as_float(wu << 16); pu[1] = __uint_as_float(wu & 0xffff0000u);
+        pr[0] = __uint_as_float(wr << 16); pr[1] = __uint_as_float(wr & 0xffff0000u);
+        pg[0] = __uint_as_float(wg << 16); pg[1] = __uint_as_float(wg & 0xffff0000u);
+        pz[0] = __uint_as_float(wz << 16); pz[1] = __uint_as_float(wz & 0xffff0000u);
+        pdl[0] = dl[0]; pdl[1] = dl[1]; pdy[0] = dy[0]; pdy[1] = dy[1];
+#pragma unroll
+        for (int ww = 1; ww < SB_W; ++ww)
+          if (w == ww) {
+            pdl[0] = dl[2 * ww]; pdl[1] = dl[2 * ww + 1]; pdy[0] = dy[2 * ww]; pdy[1] = dy[2 * ww + 1];
+          }
+      }
+      const float s1v[2] = {su.x, su.y}, s2v[2] = {s2.x, s2.y}, syv[2] = {sy.x, sy.y};
+      float o_du[2], o_dd[2], o_dz[2];
+      float dDp = 0.f, dbp = 0.f;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        o_du[j] = fmaf(pdl[j], s1v[j], Dd * pdy[j]);
+        const float dds = fmaf(pu[j], s1v[j], s2v[j]);
+        const float sd = sigmoid_fast(pr[j] + bias), sg = sigmoid_fast(pz[j]);
+        o_dd[j] = inr ? dds * (a.softplus ? sd : 1.f) : 0.f;
+        o_dz[j] = pg[j] * fmaf(Dd, pu[j], syv[j]) * sg * (1.f + pz[j] * (1.f - sg));
+        dDp = fmaf(pdy[j], pu[j], dDp);
+        dbp += o_dd[j];
+      }
+      if (inr) {
+        const int64_t t = tl + 2 * w;
+        *reinterpret_cast<unsigned*>(((bf16_t*)a.du_) + (int64_t)b * a.sdub + (int64_t)d * a.sdud + t) =
+            pack2(o_du[0], o_du[1]);
+        *reinterpret_cast<unsigned*>(((bf16_t*)a.ddelta_) + (int64_t)b * a.sddb + (int64_t)d * a.sddd + t) =
+            pack2(o_dd[0], o_dd[1]);
+        if (zb && a.dz_)
+          *reinterpret_cast<unsigned*>(((bf16_t*)a.dz_) + (int64_t)b * a.sdzb + (int64_t)d * a.sdzd + t) =
+              pack2(o_dz[0], o_dz[1]);
+      }
+      dDp = wave_sum_dpp(dDp);
+      dbp = wave_sum_dpp(dbp);
+      if (lane == 0) {
+        dDacc[k][w] += dDp;
+        dbacc[k][w] += dbp;
+      }
+      __syncthreads();  // part[] consumed before the next channel rewrites it
+    }
+    // this tile's dB / dC partial for the group's channels (this wave's states)
+    if (inr) {
+#pragma unroll
+      for (int nn = 0; nn < NW; ++nn) {
+        const int n = w * NW + nn;
+        float* pb = a.part_dB + (((int64_t)b * ndg + dg) * N + n) * a.L + tl;
+        float* pc = a.part_dC + (((int64_t)b * ndg + dg) * N + n) * a.L + tl;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          *reinterpret_cast<float4*>(pb + 4 * q) =
+              make_float4(accB[nn][4 * q], accB[nn][4 * q + 1], accB[nn][4 * q + 2], accB[nn][4 * q + 3]);
+          *reinterpret_cast<float4*>(pc + 4 * q) =
+              make_float4(accC[nn][4 * q], accC[nn][4 * q + 1], accC[nn][4 * q + 2], accC[nn][4 * q + 3]);
         }
       }
     }
@@ -592,13 +899,20 @@ hipError_t launch_selscan_fwd(const SelScanArgs& a, hipStream_t st) {
 }
 
 int selscan_ntiles(int L) { return (L + SB_T - 1) / SB_T; }
+int selscan_bwd_kc() { return SB_KC; }
 
 hipError_t launch_selscan_bwd(const SelScanArgs& a, hipStream_t st) {
   if (a.Kc != SB_KC) return hipErrorInvalidValue;
   dim3 grid((a.D + SB_KC - 1) / SB_KC, a.B), block(64 * SB_W);
   const bool v = a.dtype == kBF16 && a.vec && a.vecbc && a.vecg && (!a.z_ || a.vecz) && a.L % 8 == 0;
-  if (v) SS_DISPATCH(hipLaunchKernelGGL((selscan_bwd_k<TT, NN, true>), grid, block, 0, st, a));
-  else SS_DISPATCH(hipLaunchKernelGGL((selscan_bwd_k<TT, NN, false>), grid, block, 0, st, a));
+  if (v) {
+    if (a.N == 16) hipLaunchKernelGGL(selscan_bwd_fast_k<16>, grid, block, 0, st, a);
+    else if (a.N == 8) hipLaunchKernelGGL(selscan_bwd_fast_k<8>, grid, block, 0, st, a);
+    else if (a.N == 4) hipLaunchKernelGGL(selscan_bwd_fast_k<4>, grid, block, 0, st, a);
+    else return hipErrorInvalidValue;
+  } else {
+    SS_DISPATCH(hipLaunchKernelGGL((selscan_bwd_k<TT, NN, false>), grid, block, 0, st, a));
+  }
   MAMBA_HIP_CHECK(hipGetLastError());
   const int64_t total = (int64_t)a.B * a.G * a.N * a.L;
   if (a.dtype == kBF16)

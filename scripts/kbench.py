@@ -62,23 +62,23 @@ def main():
         res["conv_cl_bwd"] = (t, 3 * out.numel() * 2)
     if "gemm" in only:
         import torch.nn.functional as F
-        for (M, N, K, tag) in [(B * L, dproj, 768, "in_proj"), (B * L, 768, di, "out_proj")]:
+        for (M, Nn, K, tag) in [(B * L, dproj, 768, "in_proj"), (B * L, 768, di, "out_proj")]:
             A = torch.randn(M, K, device=dev).to(torch.bfloat16)
-            W = torch.randn(N, K, device=dev).to(torch.bfloat16)
+            W = torch.randn(Nn, K, device=dev).to(torch.bfloat16)
             t = timeit(lambda: F.linear(A, W), a.reps)
             res[f"gemm_{tag}_hipblaslt"] = (t, 0)
-            print(f"{tag}: hipBLASLt {2 * M * N * K / t / 1e9:.0f} TF/s", flush=True)
+            print(f"{tag}: hipBLASLt {2 * M * Nn * K / t / 1e9:.0f} TF/s", flush=True)
             t = timeit(lambda: ops.gemm_tn(A, W, None), a.reps)
             res[f"gemm_{tag}_native"] = (t, 0)
-            print(f"{tag}: native    {2 * M * N * K / t / 1e9:.0f} TF/s", flush=True)
+            print(f"{tag}: native    {2 * M * Nn * K / t / 1e9:.0f} TF/s", flush=True)
             # weight gradient dW (N, K) = dY^T (N, M) . X (M, K)
-            dY = torch.randn(M, N, device=dev).to(torch.bfloat16)
+            dY = torch.randn(M, Nn, device=dev).to(torch.bfloat16)
             t = timeit(lambda: torch.mm(dY.t(), A).float(), a.reps)
             res[f"wgrad_{tag}_hipblaslt"] = (t, 0)
-            print(f"{tag} wgrad: hipBLASLt(+fp32 cast) {2 * M * N * K / t / 1e9:.0f} TF/s", flush=True)
+            print(f"{tag} wgrad: hipBLASLt(+fp32 cast) {2 * M * Nn * K / t / 1e9:.0f} TF/s", flush=True)
             t = timeit(lambda: ops.gemm_wgrad(dY, A, None, False), a.reps)
             res[f"wgrad_{tag}_native"] = (t, 0)
-            print(f"{tag} wgrad: native fp32          {2 * M * N * K / t / 1e9:.0f} TF/s", flush=True)
+            print(f"{tag} wgrad: native fp32          {2 * M * Nn * K / t / 1e9:.0f} TF/s", flush=True)
     if "ssd" in only:
         xc = torch.randn(B, L, conv_dim, device=dev).to(torch.bfloat16)
         x = xc[..., :di].unflatten(-1, (H, P))
