@@ -91,16 +91,30 @@ __device__ __forceinline__ float readlanef(float v, int l) {
     b = fmaf(a, pb, b);                                                         \
     a *= pa;                                                                    \
   }
+// One combine step fused into the DPP ALU ops themselves: v_fmac_f32_dpp b += b[src] * a, then
+// v_mul_f32_dpp a = a[src] * a.  Without bound_ctrl a lane whose source is out of its row (or whose
+// row is masked off) is simply not written, which is exactly the identity map (1, 0) -- so no
+// constant "old" registers and no separate DPP moves (2 VALU ops per step instead of 6).  The
+// s_nop 1 before each op covers the VALU-write -> DPP-read hazard (2 wait states) of the asm block.
+#define SS_DPP2(CTRL)                                                                    \
+  "s_nop 1\n\tv_fmac_f32_dpp %1, %1, %0 " CTRL "\n\t"                              \
+  "s_nop 1\n\tv_mul_f32_dpp %0, %0, %0 " CTRL "\n\t"
 // inclusive prefix over lanes 0..i of the maps h -> a h + b (lane 0 applied first):
 // row_shr 1/2/4/8 inside each 16-lane row, then row_bcast:15 / row_bcast:31 across rows
 __device__ __forceinline__ void scan_prefix(float& a, float& b) {
-  SS_STEP(0x111, 0xF) SS_STEP(0x112, 0xF) SS_STEP(0x114, 0xF) SS_STEP(0x118, 0xF)
-  SS_STEP(0x142, 0xA) SS_STEP(0x143, 0xC)
+  asm volatile(SS_DPP2("row_shr:1 row_mask:0xf bank_mask:0xf") SS_DPP2("row_shr:2 row_mask:0xf bank_mask:0xf")
+               SS_DPP2("row_shr:4 row_mask:0xf bank_mask:0xf") SS_DPP2("row_shr:8 row_mask:0xf bank_mask:0xf")
+               SS_DPP2("row_bcast:15 row_mask:0xa bank_mask:0xf") SS_DPP2("row_bcast:31 row_mask:0xc bank_mask:0xf")
+               "s_nop 1"
+               : "+v"(a), "+v"(b));
 }
 // inclusive suffix over lanes i..63 (lane 63 applied first): row_shl inside rows, then the
 // four row totals (lanes 0/16/32/48) are composed through readlane
 __device__ __forceinline__ void scan_suffix(float& a, float& b) {
-  SS_STEP(0x101, 0xF) SS_STEP(0x102, 0xF) SS_STEP(0x104, 0xF) SS_STEP(0x108, 0xF)
+  asm volatile(SS_DPP2("row_shl:1 row_mask:0xf bank_mask:0xf") SS_DPP2("row_shl:2 row_mask:0xf bank_mask:0xf")
+               SS_DPP2("row_shl:4 row_mask:0xf bank_mask:0xf") SS_DPP2("row_shl:8 row_mask:0xf bank_mask:0xf")
+               "s_nop 1"
+               : "+v"(a), "+v"(b));
   const float a1 = readlanef(a, 16), b1 = readlanef(b, 16);
   const float a2 = readlanef(a, 32), b2 = readlanef(b, 32);
   const float a3 = readlanef(a, 48), b3 = readlanef(b, 48);
@@ -113,6 +127,7 @@ __device__ __forceinline__ void scan_suffix(float& a, float& b) {
   a *= ca;
 }
 #undef SS_STEP
+#undef SS_DPP2
 __device__ __forceinline__ float wave_sum_dpp(float v) {
   v += dppf<0x111>(0.f, v);
   v += dppf<0x112>(0.f, v);
@@ -212,7 +227,7 @@ __global__ __launch_bounds__(256) void selscan_fwd_k(SelScanArgs a) {
 // Sums over n (du, ddelta, y for dz) go through one LDS row per wave and are finished item-parallel
 // (thread = time step, fixed-order sum over the 8 rows, coalesced I/O).
 template <typename T, int N, bool VEC>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void selscan_bwd_k(SelScanArgs a) {
+__global__ __launch_bounds__(256) void selscan_bwd_k(SelScanArgs a) {
   constexpr int NW = N >= SB_W ? N / SB_W : 1;
   constexpr int IT = SB_IT;
   __shared__ __attribute__((aligned(16))) float part[2][SB_W][3][SB_T];  // double-buffered per channel
