@@ -167,24 +167,44 @@ __global__ __launch_bounds__(256) void selscan_fwd_k(SelScanArgs a) {
     float u[SF_IT], dl[SF_IT], y[SF_IT];
     load_items<VEC, T, SF_IT>(urow, tl, a.L, u);
     load_items<VEC, T, SF_IT>(drow, tl, a.L, dl);
+    // u is only needed as dt*u (per state) and D*u (y's skip term): fold both in up front
 #pragma unroll
     for (int i = 0; i < SF_IT; ++i) {
-      float v = dl[i] + bias;
-      v = a.softplus ? softplus_fast(v) : v;
-      dl[i] = (tl + i < a.L) ? v : 0.f;
-      y[i] = 0.f;
+      const float v = dl[i] + bias;
+      const float sp = softplus_fast(v);
+      dl[i] = (tl + i < a.L) ? (a.softplus ? sp : v) : 0.f;
+      y[i] = Dd * u[i];
+      u[i] *= dl[i];
     }
+    // vector path: B/C rows are read at a clamped (always legal) offset without a guard; lanes past
+    // L have dt = 0, i.e. the identity map, so whatever they read never reaches a stored value
+    const int tc = VEC ? min(tl, a.L - SF_IT) : tl;
 #pragma unroll 1
     for (int n = 0; n < N; ++n) {  // keep each state's loads in its own iteration (bounded registers)
       const float A2 = a.A[d * N + n] * kLog2e;
       float Bv[SF_IT], Cv[SF_IT], av[SF_IT], xb[SF_IT];
-      load_items<VEC, T, SF_IT>(Bb + (int64_t)n * a.sBn, tl, a.L, Bv);
-      load_items<VEC, T, SF_IT>(Cb + (int64_t)n * a.sCn, tl, a.L, Cv);
+      if constexpr (VEC) {
+        static_assert(SF_IT % 8 == 0, "16-byte B/C loads");
+#pragma unroll
+        for (int q = 0; q < SF_IT / 8; ++q) {
+          float tb[8], tcv[8];
+          ld8bf(reinterpret_cast<const bf16_t*>(Bb + (int64_t)n * a.sBn) + tc + 8 * q, tb);
+          ld8bf(reinterpret_cast<const bf16_t*>(Cb + (int64_t)n * a.sCn) + tc + 8 * q, tcv);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            Bv[8 * q + j] = tb[j];
+            Cv[8 * q + j] = tcv[j];
+          }
+        }
+      } else {
+        load_items<VEC, T, SF_IT>(Bb + (int64_t)n * a.sBn, tl, a.L, Bv);
+        load_items<VEC, T, SF_IT>(Cb + (int64_t)n * a.sCn, tl, a.L, Cv);
+      }
       float ca = 1.f, cb = 0.f;
 #pragma unroll
       for (int i = 0; i < SF_IT; ++i) {
         av[i] = __builtin_amdgcn_exp2f(dl[i] * A2);
-        xb[i] = dl[i] * u[i] * Bv[i];
+        xb[i] = u[i] * Bv[i];  // u holds dt * u
         cb = fmaf(av[i], cb, xb[i]);
         ca *= av[i];
       }
@@ -205,11 +225,8 @@ __global__ __launch_bounds__(256) void selscan_fwd_k(SelScanArgs a) {
     float zz[SF_IT];
     if (zrow) load_items<VEC, T, SF_IT>(zrow, tl, a.L, zz);
 #pragma unroll
-    for (int i = 0; i < SF_IT; ++i) {
-      float o = fmaf(Dd, u[i], y[i]);
-      if (zrow) o *= siluf_(zz[i]);
-      y[i] = o;
-    }
+    for (int i = 0; i < SF_IT; ++i)
+      if (zrow) y[i] *= siluf_(zz[i]);
     store_items<VEC, T, SF_IT>(orow, tl, a.L, y);
   }
   if (a.last_state && lane < N) a.last_state[(int64_t)row * N + lane] = hc[lane];
