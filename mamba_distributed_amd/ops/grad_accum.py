@@ -113,19 +113,35 @@ def accumulable(param) -> bool:
 _pending_stream = None  # stream the queued gradients were produced on (the backward's stream)
 
 
+def _foreach_accumulate(pairs) -> None:
+    """dst += src for every pair with ONE multi-tensor kernel.  torch's fused foreach route needs
+    every tensor of both lists dense with identical strides (and one dtype); a single odd gradient
+    (a strided view, a broadcast) silently drops the whole call to one add kernel per tensor, so
+    non-contiguous sources are made contiguous first and odd destinations are added one by one."""
+    by_dtype = {}
+    for d, s in pairs:
+        if d.is_contiguous():
+            by_dtype.setdefault(d.dtype, ([], []))
+            by_dtype[d.dtype][0].append(d)
+            by_dtype[d.dtype][1].append(s if s.is_contiguous() else s.contiguous())
+        else:
+            d.add_(s)
+    for dst, src in by_dtype.values():
+        torch._foreach_add_(dst, src)
+
+
 def _flush() -> None:
     global _flush_queued, _pending_stream
     _flush_queued = False
     if _pending:
-        dst = [d for d, _ in _pending]
-        src = [s for _, s in _pending]
+        pairs = list(_pending)
         _pending.clear()
         st, _pending_stream = _pending_stream, None
         if st is not None:
             with torch.cuda.stream(st):  # the callback thread's current stream may be another one
-                torch._foreach_add_(dst, src)
+                _foreach_accumulate(pairs)
         else:
-            torch._foreach_add_(dst, src)
+            _foreach_accumulate(pairs)
 
 
 def defer(param, grad):
