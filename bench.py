@@ -41,7 +41,10 @@ def main():
     p.add_argument("--no-fused-ce", action="store_true")
     p.add_argument("--no-tuned-gemms", action="store_true", help="library-default GEMM solutions")
     p.add_argument("--profile-steps", type=int, default=0, help="torch.profiler trace of N extra steps")
-    p.add_argument("--no-overlap", action="store_true", help="run the micro-steps strictly one after another")
+    p.add_argument("--overlap", default="auto", choices=["auto", "on", "off"],
+                   help="next micro-batch's forward on a second stream beside the backward "
+                        "(auto: d_model <= 1024, parallel/microbatch.py::auto_overlap)")
+    p.add_argument("--no-overlap", action="store_true", help="same as --overlap off")
     p.add_argument("--trace-loss", action="store_true",
                    help="diagnostics: print every step's loss and grad norm (syncs each step; not for timing)")
     p.add_argument("--dp-impl", default="native", choices=["native", "ddp"],
@@ -54,7 +57,7 @@ def main():
     from mamba_distributed_amd.data.loader import SyntheticTokens
     from mamba_distributed_amd.ops import grad_accum
     from mamba_distributed_amd.parallel import ddp as ddp_mod
-    from mamba_distributed_amd.parallel.microbatch import run_micro_batches
+    from mamba_distributed_amd.parallel.microbatch import resolve_overlap, run_micro_batches
     from mamba_distributed_amd.parallel.dist import all_reduce_avg, all_reduce_max, barrier, destroy, init_distributed
 
     info = init_distributed("auto")
@@ -71,6 +74,7 @@ def main():
     opt = model.configure_optimizers(0.1, 6e-4, "cuda" if dev.startswith("cuda") else "cpu", False)
     loader = SyntheticTokens(a.B, a.T, cfg.vocab_size, info.rank, world, device=dev)
     fused = not a.no_fused_ce
+    overlap = resolve_overlap("off" if a.no_overlap else a.overlap, cfg)
 
     def compute_loss(x, y):
         with torch.autocast(device_type="cuda", dtype=torch.bfloat16):
@@ -82,7 +86,7 @@ def main():
         with grad_accum.accumulation_scope():
             # micro-batch k+1's forward runs on a second stream beside micro-batch k's backward
             loss_acc = run_micro_batches(dmodel, loader.next_batch, accum, compute_loss,
-                                         overlap=not a.no_overlap)
+                                         overlap=overlap)
         all_reduce_avg(loss_acc)
         norm = torch.nn.utils.clip_grad_norm_(dmodel.parameters(), 1.0)
         opt.step()
@@ -139,7 +143,7 @@ def main():
                 "parallelism": f"dp{world}",
                 "ops": "pytorch-reference" if a.reference_ops else "native-hip",
                 "gemm_table": "tunableop-gfx950" if tuned else "library-default",
-                "microbatch_overlap": not a.no_overlap,
+                "microbatch_overlap": overlap,
                 "dp_impl": a.dp_impl if world > 1 else "none",
                 "final_loss": round(loss_v, 4),
             },

@@ -39,7 +39,7 @@ from .parallel.api import clip_grad_norm_ as par_clip_grad_norm_
 from .parallel.api import full_state_dict, parallelize, sync_tp_grads
 from .parallel.dist import all_gather_object, all_reduce_avg, destroy, init_distributed
 from .parallel.groups import init_parallel_groups
-from .parallel.microbatch import run_micro_batches
+from .parallel.microbatch import resolve_overlap, run_micro_batches
 from .utils.checkpoint import latest_checkpoint, load_checkpoint, save_checkpoint, set_rng_state
 from .utils.lr import get_lr
 
@@ -82,7 +82,8 @@ class TrainArgs:
     tp: int = 1                          # tensor parallel degree (Mamba-2 heads; parallel/tensor_parallel.py)
     cp: int = 1                          # context parallel degree (sequence shards; parallel/context_parallel.py)
     sequence_parallel: bool = False      # with tp > 1: shard the residual stream over tokens as well
-    overlap_microbatches: bool = True    # next micro-batch's forward beside the current backward (GPU)
+    overlap_microbatches: str = "auto"   # next micro-batch's forward beside the current backward (GPU):
+                                         # auto (d_model <= 1024, parallel/microbatch.py::auto_overlap) / on / off
 
 
 def build_config(a: TrainArgs) -> MambaConfig:
@@ -246,7 +247,8 @@ class Trainer:
 
         # overlap micro-batch k+1's forward with k's backward on a second stream (parallel/microbatch.py);
         # not under TP/CP, whose per-layer collectives must be issued on one stream per communicator
-        overlap = self.a.overlap_microbatches and self.device_type == "cuda" and not self.parallel
+        overlap = (resolve_overlap(self.a.overlap_microbatches, self.raw_model.config) and self.device_type == "cuda"
+                   and not self.parallel)
         with grad_accum.accumulation_scope():  # weights are frozen until optimizer.step()
             loss_accum = run_micro_batches(self.model, lambda: self._batch(self.train_loader), self.grad_accum_steps,
                                            compute_loss, overlap=overlap)

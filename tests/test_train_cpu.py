@@ -65,3 +65,14 @@ def test_train_cli_help_and_tiny_run(tmp_path):
                        capture_output=True, text=True, env=env, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     assert "step     1 | loss:" in r.stdout
+
+
+def test_overlap_policy_by_width():
+    """parallel/microbatch.py::resolve_overlap: auto = on for d_model <= 1024 (measured crossover)."""
+    from mamba_distributed_amd import preset
+    from mamba_distributed_amd.parallel.microbatch import resolve_overlap
+    assert resolve_overlap("auto", preset("mamba2-280m")) is True
+    assert resolve_overlap("auto", preset("mamba2-1.4b")) is False
+    assert resolve_overlap("off", preset("mamba2-280m")) is False
+    assert resolve_overlap("on", preset("mamba2-1.4b")) is True
+    assert resolve_overlap(True, None) is True
