@@ -101,7 +101,9 @@ def run_micro_batches(model, next_batch: Callable, accum: int, compute_loss: Cal
     dev = main.device.index if main.device.index is not None else torch.cuda.current_device()
     other = _OTHER.get(dev)
     if other is None:
-        other = _OTHER[dev] = torch.cuda.Stream(device=dev)
+        # same priority as the caller's stream (a high-priority compute stream makes both micro-batch
+        # streams outrank the weight-gradient side stream, ops/grad_accum.py)
+        other = _OTHER[dev] = torch.cuda.Stream(device=dev, priority=main.priority)
     streams = [main if (accum - 1 - k) % 2 == 0 else other for k in range(accum)]
     # everything the caller queued on ``main`` (the previous optimizer step updating the weights and
     # reading the gradients that zero_grad just released) precedes the first forward when that runs
