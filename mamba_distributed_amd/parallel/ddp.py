@@ -94,6 +94,18 @@ def set_grad_sync(model, enabled: bool):
         r.arm()
 
 
+def clip_grad_norm_(model, max_norm: float) -> torch.Tensor:
+    """``torch.nn.utils.clip_grad_norm_`` (reference train.py:222).  Under the native reducer every
+    gradient is a view into one flat fp32 buffer, so the global 2-norm and the rescale are one
+    reduction and one scale kernel over that buffer instead of per-tensor foreach launches."""
+    r = _reducer(model)
+    if r is None:
+        return torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm)
+    total = torch.linalg.vector_norm(r.flat, 2.0)
+    r.flat.mul_(torch.clamp(max_norm / (total + 1e-6), max=1.0))
+    return total
+
+
 def finish_grad_sync(model) -> None:
     """Wait for the native reducer's bucket all-reduces (no-op for DDP / single process)."""
     r = _reducer(model)

@@ -257,7 +257,7 @@ class Trainer:
             sync_tp_grads(self.model, self.groups)
             norm = par_clip_grad_norm_(self.model, self.a.grad_clip, self.groups)
         else:
-            norm = torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.a.grad_clip)
+            norm = ddp_mod.clip_grad_norm_(self.model, self.a.grad_clip)
         lr = self.lr(step)
         for g in self.optimizer.param_groups:
             g["lr"] = lr
