@@ -47,6 +47,8 @@ def main():
     p.add_argument("--no-overlap", action="store_true", help="same as --overlap off")
     p.add_argument("--trace-loss", action="store_true",
                    help="diagnostics: print every step's loss and grad norm (syncs each step; not for timing)")
+    p.add_argument("--activation-checkpointing", type=int, default=0,
+                   help="recompute every N-th block in the backward (memory for long sequences; 0 = off)")
     p.add_argument("--dp-impl", default="native", choices=["native", "ddp"],
                    help="gradient all-reduce: native bucketed reducer (parallel/reducer.py) or torch DDP")
     a = p.parse_args()
@@ -70,6 +72,8 @@ def main():
     torch.manual_seed(1337)
     cfg = preset(a.model)
     model = LMHeadModel(cfg, device=dev)
+    if a.activation_checkpointing:
+        model.set_activation_checkpointing(a.activation_checkpointing)
     dmodel = ddp_mod.wrap_data_parallel(model, info, a.dp_impl, a.bucket_cap_mb, a.grad_comm_dtype)
     opt = model.configure_optimizers(0.1, 6e-4, "cuda" if dev.startswith("cuda") else "cpu", False)
     loader = SyntheticTokens(a.B, a.T, cfg.vocab_size, info.rank, world, device=dev)
@@ -106,6 +110,7 @@ def main():
     elapsed = torch.tensor(time.perf_counter() - t0, device=dev, dtype=torch.float64)
     all_reduce_max(elapsed)
     elapsed = float(elapsed.item())
+    peak_gb = torch.cuda.max_memory_allocated() / 2**30 if dev.startswith("cuda") else 0.0
     loss_v = float(last.item())
     if a.profile_steps and info.master:
         from torch.profiler import ProfilerActivity, profile
@@ -145,7 +150,9 @@ def main():
                 "gemm_table": "tunableop-gfx950" if tuned else "library-default",
                 "microbatch_overlap": overlap,
                 "dp_impl": a.dp_impl if world > 1 else "none",
+                "activation_checkpointing": a.activation_checkpointing,
                 "final_loss": round(loss_v, 4),
+                "peak_mem_gb": round(peak_gb, 1),
             },
         }
         print(json.dumps(out), flush=True)

@@ -21,6 +21,7 @@ from functools import partial
 from typing import Optional
 
 import torch
+import torch.utils.checkpoint
 import torch.nn as nn
 import torch.nn.functional as F
 
@@ -160,9 +161,16 @@ class MixerModel(nn.Module):
             input_ids = shard_batch(self, input_ids)
         hidden_states = self.embedding(input_ids)
         residual = None
-        for layer in self.layers:
-            hidden_states, residual = layer(hidden_states, residual, inference_params=inference_params,
-                                            **mixer_kwargs)
+        every = getattr(self, "checkpoint_every", 0)
+        recompute = every > 0 and inference_params is None and self.training and torch.is_grad_enabled()
+        for i, layer in enumerate(self.layers):
+            if recompute and i % every == 0:
+                # activation checkpointing: keep only the block inputs, recompute the block in backward
+                hidden_states, residual = torch.utils.checkpoint.checkpoint(
+                    layer, hidden_states, residual, use_reentrant=False, **mixer_kwargs)
+            else:
+                hidden_states, residual = layer(hidden_states, residual, inference_params=inference_params,
+                                                **mixer_kwargs)
         if self.fused_add_norm:
             return rms_norm_fn(hidden_states, self.norm_f.weight, None, residual=residual, prenorm=False,
                                residual_in_fp32=self.residual_in_fp32, eps=self.norm_f.eps)
@@ -194,6 +202,14 @@ class MambaLMHeadModel(nn.Module):
 
     def allocate_inference_cache(self, batch_size, max_seqlen, dtype=None, **kw):
         return self.backbone.allocate_inference_cache(batch_size, max_seqlen, dtype=dtype, **kw)
+
+    def set_activation_checkpointing(self, every: int = 1) -> None:
+        """Recompute every ``every``-th block in the backward instead of keeping its activations
+        (0 = off).  The memory/compute trade upstream exposes as the fused ops' ``checkpoint_lvl``,
+        applied per block: at T = 8192+ or large micro-batches it bounds activation memory to the
+        block inputs plus one block's working set.  Gradients are unchanged: the native kernels
+        are deterministic, so the recomputed forward is bitwise the original."""
+        self.backbone.checkpoint_every = int(every)
 
     def forward_hidden(self, input_ids, inference_params=None, **mixer_kwargs):
         return self.backbone(input_ids, inference_params=inference_params, **mixer_kwargs)

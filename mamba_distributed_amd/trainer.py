@@ -82,6 +82,7 @@ class TrainArgs:
     tp: int = 1                          # tensor parallel degree (Mamba-2 heads; parallel/tensor_parallel.py)
     cp: int = 1                          # context parallel degree (sequence shards; parallel/context_parallel.py)
     sequence_parallel: bool = False      # with tp > 1: shard the residual stream over tokens as well
+    activation_checkpointing: int = 0   # recompute every N-th block in the backward (0 = off)
     overlap_microbatches: str = "auto"   # next micro-batch's forward beside the current backward (GPU):
                                          # auto (d_model <= 1024, parallel/microbatch.py::auto_overlap) / on / off
 
@@ -133,6 +134,8 @@ class Trainer:
                 enable_tuned_gemms()
         self.raw_model = LMHeadModel(self.config, device=self.device)
         self.raw_model.to(self.device)
+        if a.activation_checkpointing:
+            self.raw_model.set_activation_checkpointing(a.activation_checkpointing)
         if self.master:
             total = int(sum(p.numel() for p in self.raw_model.parameters()) // 1e6)
             print(f"Total number of parameters: {total}M")

@@ -611,3 +611,39 @@ def test_microbatch_overlap_across_optimizer_steps(cuda, accum):
     assert torch.equal(l0, l1), (l0, l1)
     for k in p0:
         assert torch.equal(p0[k], p1[k]), k
+
+
+@pytest.mark.parametrize("layer", ["Mamba1", "Mamba2"])
+def test_activation_checkpointing_bitwise_on_gpu(cuda, layer):
+    """Per-block recompute (set_activation_checkpointing) with the native kernels, the two-stream
+    micro-batch overlap and in-place gradient accumulation: loss and gradients bitwise unchanged."""
+    import copy
+    from mamba_distributed_amd import LMHeadModel, MambaConfig
+    from mamba_distributed_amd.ops import grad_accum
+    from mamba_distributed_amd.parallel.microbatch import run_micro_batches
+    torch.manual_seed(0)
+    cfg = MambaConfig(d_model=256, n_layer=4, vocab_size=1024, ssm_cfg={"layer": layer})
+    m0 = LMHeadModel(cfg, device=cuda)
+    m1 = copy.deepcopy(m0)
+    m1.set_activation_checkpointing(1)
+    accum = 4
+    g = torch.Generator(device=cuda).manual_seed(1)
+    data = [(torch.randint(0, 1024, (2, 256), device=cuda, generator=g),
+             torch.randint(0, 1024, (2, 256), device=cuda, generator=g)) for _ in range(accum)]
+
+    def run(m):
+        it = iter(data)
+
+        def loss_fn(x, y):
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                return m(x, y, return_logits=False)[1] / accum
+
+        with grad_accum.accumulation_scope():
+            loss = run_micro_batches(m, lambda: next(it), accum, loss_fn, overlap=True)
+        torch.cuda.synchronize()
+        return loss
+
+    l0, l1 = run(m0), run(m1)
+    assert torch.equal(l0, l1), (l0, l1)
+    for (k, p), q in zip(m1.named_parameters(), m0.parameters()):
+        assert torch.equal(p.grad, q.grad), k

@@ -92,3 +92,25 @@ def test_hybrid_config_builds_and_runs():
     loss.backward()
     assert logits.shape == (2, 40, 512)
     assert m.backbone.layers[1].mixer.__class__.__name__ == "MHA"
+
+
+@pytest.mark.parametrize("every", [1, 2])
+def test_activation_checkpointing_same_loss_and_grads(every):
+    """MambaLMHeadModel.set_activation_checkpointing: recomputing blocks in the backward leaves the
+    loss and every gradient unchanged (reference ops, fp32)."""
+    import copy
+    from mamba_distributed_amd import LMHeadModel, MambaConfig
+    torch.manual_seed(0)
+    cfg = MambaConfig(d_model=64, n_layer=3, vocab_size=128, ssm_cfg={"layer": "Mamba2", "headdim": 16})
+    m0 = LMHeadModel(cfg, device="cpu", enc=object())
+    m1 = copy.deepcopy(m0)
+    m1.set_activation_checkpointing(every)
+    x = torch.randint(0, 128, (2, 40))
+    y = torch.randint(0, 128, (2, 40))
+    l0 = m0(x, y)[1]
+    l1 = m1(x, y)[1]
+    l0.backward()
+    l1.backward()
+    torch.testing.assert_close(l1, l0, rtol=0, atol=0)
+    for (k, p), q in zip(m1.named_parameters(), m0.parameters()):
+        torch.testing.assert_close(p.grad, q.grad, rtol=1e-6, atol=1e-7, msg=k)
