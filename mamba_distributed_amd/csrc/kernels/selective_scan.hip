@@ -84,13 +84,7 @@ __device__ __forceinline__ float dppf(float old, float src) {
 __device__ __forceinline__ float readlanef(float v, int l) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
 }
-// combine the map held `off` lanes away (applied first) into (a, b): (a, b) <- (a*pa, a*pb + b)
-#define SS_STEP(CTRL, RM)                                                       \
-  {                                                                             \
-    const float pa = dppf<CTRL, RM>(1.f, a), pb = dppf<CTRL, RM>(0.f, b);       \
-    b = fmaf(a, pb, b);                                                         \
-    a *= pa;                                                                    \
-  }
+// Combining the map held `off` lanes away (applied first) into (a, b): (a, b) <- (a*pa, a*pb + b).
 // One combine step fused into the DPP ALU ops themselves: v_fmac_f32_dpp b += b[src] * a, then
 // v_mul_f32_dpp a = a[src] * a.  Without bound_ctrl a lane whose source is out of its row (or whose
 // row is masked off) is simply not written, which is exactly the identity map (1, 0) -- so no
@@ -126,7 +120,6 @@ __device__ __forceinline__ void scan_suffix(float& a, float& b) {
   b = fmaf(a, cb, b);
   a *= ca;
 }
-#undef SS_STEP
 #undef SS_DPP2
 __device__ __forceinline__ float wave_sum_dpp(float v) {
   v += dppf<0x111>(0.f, v);
