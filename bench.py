@@ -80,8 +80,15 @@ def main():
     fused = not a.no_fused_ce
     overlap = resolve_overlap("off" if a.no_overlap else a.overlap, cfg)
 
+    on_gpu = dev.startswith("cuda")
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
+
     def compute_loss(x, y):
-        with torch.autocast(device_type="cuda", dtype=torch.bfloat16):
+        # bf16 autocast on the GPU; the CPU path (gloo rehearsal of the multi-rank flow) stays fp32
+        with torch.autocast(device_type="cuda" if on_gpu else "cpu", dtype=torch.bfloat16, enabled=on_gpu):
             _, loss = dmodel(x, y, return_logits=not fused)
         return loss / accum
 
@@ -101,12 +108,12 @@ def main():
     for _ in range(a.warmup):
         step()
     barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         last = step()
     barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = torch.tensor(time.perf_counter() - t0, device=dev, dtype=torch.float64)
     all_reduce_max(elapsed)
     elapsed = float(elapsed.item())
@@ -135,7 +142,7 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": round(value / BASELINE_TOK_S, 3),
-            "dtype": "bf16",
+            "dtype": "bf16" if on_gpu else "fp32",
             "data": "synthetic (uniform random tokens, random-init weights)",
             "config": {
                 "model": f"{a.model} (d_model={cfg.d_model}, n_layer={cfg.n_layer}, vocab={cfg.vocab_size}, "
@@ -146,7 +153,7 @@ def main():
                 "grad_accum": accum,
                 "seq_len": a.T,
                 "parallelism": f"dp{world}",
-                "ops": "pytorch-reference" if a.reference_ops else "native-hip",
+                "ops": "pytorch-reference" if (a.reference_ops or not on_gpu) else "native-hip",
                 "gemm_table": "tunableop-gfx950" if tuned else "library-default",
                 "microbatch_overlap": overlap,
                 "dp_impl": a.dp_impl if world > 1 else "none",

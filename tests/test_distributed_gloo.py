@@ -5,6 +5,7 @@ plumbing config) must produce the same parameters as a single process that sees 
 batch (DDP averages gradients; DataLoaderLite's rank striding splits the global batch exactly).
 A second test runs two torchrun "nodes" on localhost (--nnodes 2 --node-rank i).
 """
+import math
 import os
 import socket
 import subprocess
@@ -134,3 +135,24 @@ def test_elastic_restart_resumes_from_checkpoint(tmp_path):
     assert sorted(la) == list(range(6)) and sorted(lb) == list(range(6)), (la, lb)
     for s in (2, 3, 4, 5):
         assert abs(la[s] - lb[s]) <= 1e-6 * abs(la[s]), (s, la[s], lb[s])
+
+
+@pytest.mark.parametrize("dp_impl", ["native", "ddp"])
+def test_bench_multi_rank_flow_on_cpu(dp_impl):
+    """bench.py exactly as the round driver launches it for N > 1 (torch.distributed.run, one rank
+    per device, 127.0.0.1 rendezvous), rehearsed on CPU with gloo and the tiny model: every rank
+    runs the same steps through the data-parallel wrapper, and rank 0 prints ONE JSON line."""
+    import json
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--model", "mamba2-tiny", "--B", "2", "--T", "64", "--global-batch-tokens", "512",
+           "--steps", "2", "--warmup", "1", "--dp-impl", dp_impl]
+    r = subprocess.run(cmd, capture_output=True, text=True, env=_env(), timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["warmup"] == 1 and d["scaling"] == "strong"
+    assert d["config"]["parallelism"] == "dp2" and d["config"]["dp_impl"] == dp_impl
+    assert d["config"]["grad_accum"] == 2 and d["value"] > 0
+    assert math.isfinite(d["config"]["final_loss"]), d
