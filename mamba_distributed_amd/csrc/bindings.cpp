@@ -578,6 +578,28 @@ Tensor gemm_tn(Tensor A, Tensor B, optional<Tensor> out) {
   return C;
 }
 
+// C (N, M) (+)= A (N, K) . B (K, M) for the channel-major Mamba-1 projections (x_proj / dt_proj and their
+// input gradients); B / out rows are contiguous along M and may be row-strided views (x_dbl[:R])
+Tensor gemm_skinny(Tensor A, Tensor B, optional<Tensor> out, bool accumulate) {
+  check_cuda(A, "A");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(A.device());
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(0), "gemm_skinny: A (N,K), B (K,M)");
+  TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "gemm_skinny: bf16 operands");
+  TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1, "gemm_skinny: unit inner strides");
+  const int64_t N = A.size(0), K = A.size(1), M = B.size(1);
+  Tensor C = out.has_value() && out->defined() ? *out : at::empty({N, M}, B.options());
+  TORCH_CHECK(C.dim() == 2 && C.size(0) == N && C.size(1) == M && C.stride(1) == 1 && C.scalar_type() == at::kBFloat16,
+              "gemm_skinny: out (N,M) bf16 with unit column stride");
+  TORCH_CHECK(!accumulate || (out.has_value() && out->defined()), "gemm_skinny: accumulate needs out");
+  TORCH_CHECK((uintptr_t)A.data_ptr() % 16 == 0 && (uintptr_t)B.data_ptr() % 16 == 0 && (uintptr_t)C.data_ptr() % 16 == 0,
+              "gemm_skinny: 16-B aligned operands");
+  TORCH_CHECK(mamba_amd::gemm_skinny_supported((int)N, (int)K, (int)M, A.stride(0), B.stride(0), C.stride(0)),
+              "gemm_skinny: needs K % 8 == 0, M % 8 == 0, row strides % 8 == 0");
+  HIPCHK(mamba_amd::launch_gemm_skinny(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0),
+                                       (int)N, (int)K, (int)M, accumulate, cur_stream()));
+  return C;
+}
+
 // dW (fp32, (P, Q)) = dY^T X for token-major bf16 dY (M, P), X (M, Q); out optional (accumulate=True
 // adds into it, e.g. an existing fp32 .grad)
 Tensor gemm_wgrad(Tensor dY, Tensor X, optional<Tensor> out, bool accumulate) {
@@ -705,6 +727,7 @@ TORCH_LIBRARY(mamba_amd, m) {
         "-> Tensor[]");
   m.def("gemm_tn(Tensor A, Tensor B, Tensor(a!)? out=None) -> Tensor");
   m.def("gemm_wgrad(Tensor dY, Tensor X, Tensor(a!)? out=None, bool accumulate=False) -> Tensor");
+  m.def("gemm_skinny(Tensor A, Tensor B, Tensor(a!)? out=None, bool accumulate=False) -> Tensor");
   m.def("ssm_state_update(Tensor(a!) state, Tensor x, Tensor dt, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? z, "
         "Tensor? dt_bias, bool softplus) -> Tensor");
   m.def("decode_inproj(Tensor hn, Tensor W, Tensor(a!) zxbcdt, int conv_lo, int conv_hi, Tensor(b!) conv_state, "
@@ -718,6 +741,7 @@ TORCH_LIBRARY_IMPL(mamba_amd, CUDA, m) {
   m.impl("add_rmsnorm_fwd", &add_rmsnorm_fwd);
   m.impl("gemm_tn", &gemm_tn);
   m.impl("gemm_wgrad", &gemm_wgrad);
+  m.impl("gemm_skinny", &gemm_skinny);
   m.impl("add_rmsnorm_bwd", &add_rmsnorm_bwd);
   m.impl("gated_rmsnorm_fwd", &gated_rmsnorm_fwd);
   m.impl("gated_rmsnorm_bwd", &gated_rmsnorm_bwd);

@@ -390,6 +390,126 @@ hipError_t launch_gemm_wgrad(const void* dY, int64_t ldy, const void* X, int64_t
   return hipGetLastError();
 }
 
+// ================================ small-K / small-N "skinny" GEMM ===================================
+// C[N, M] (+)= A[N, K] . B[K, M] with a small weight A (K-contiguous) and activation / output rows
+// that run along the token dimension M (the channel-major Mamba-1 layout, models/mamba1.py):
+//   x_dbl = W_x (80 x 1536) . conv_out      delta = W_dt (1536 x 48) . x_dbl[:48]
+//   dx_dbl[:48] = W_dt^T . ddelta           dconv_out += W_x^T (1536 x 80) . dx_dbl
+// One side of every product is tiny (K = 48 / 80 or N = 48 / 80), so the work is a streaming pass over
+// the M-long rows; hipBLASLt runs these 2-4x slower than the bytes allow.  Workgroup = TN rows of C x
+// TM tokens; 4 waves split TM; K in steps of 32 through LDS (A tile [TN][32], B tile [32][TM], zero
+// padded past K / N); B fragments via ds_read_b64_tr_b16 (K runs down the rows); the epilogue is staged
+// through LDS so every global load / store is a 16-B vector along M (ACC adds into C in fp32).
+namespace {
+constexpr int SK_TN = 64;
+}
+
+// BK = K-depth per LDS stage: 32 for the small-K products (one MFMA step), 128 for the long-K ones
+// (x_dbl, dx_dbl: 12 stages instead of 48, 4x the bytes in flight per barrier)
+template <int TM, int BK, bool ACC>
+__global__ __launch_bounds__(256) void gemm_skinny_k(const bf16_t* __restrict__ A, int64_t lda,
+                                                     const bf16_t* __restrict__ B, int64_t ldb,
+                                                     bf16_t* __restrict__ C, int64_t ldc, int N, int K, int M) {
+  constexpr int LDA_ = BK + 8, LDB_ = TM + 8, LDC_ = TM + 8;
+  constexpr int WM = TM / 4, NJ = WM / 16, MI = SK_TN / 16;
+  constexpr int AB = SK_TN * LDA_ * 2, BB = BK * LDB_ * 2, CB = SK_TN * LDC_ * 2;
+  constexpr int SMEM = (AB + BB) > CB ? (AB + BB) : CB;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  bf16_t* As = reinterpret_cast<bf16_t*>(smem);
+  bf16_t* Bs = reinterpret_cast<bf16_t*>(smem + AB);
+  const int m0 = blockIdx.x * TM, n0 = blockIdx.y * SK_TN;
+  const int w = threadIdx.x >> 6;
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = zero4();
+  for (int k0 = 0; k0 < K; k0 += BK) {
+#pragma unroll
+    for (int q = threadIdx.x; q < SK_TN * BK / 8; q += 256) {  // A tile: 64 rows x BK
+      const int r = q / (BK / 8), c = (q % (BK / 8)) * 8;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (n0 + r < N && k0 + c < K) v = *reinterpret_cast<const uint4*>(A + (int64_t)(n0 + r) * lda + k0 + c);
+      *reinterpret_cast<uint4*>(As + r * LDA_ + c) = v;
+    }
+#pragma unroll
+    for (int q = threadIdx.x; q < BK * TM / 8; q += 256) {  // B tile: BK k-rows x TM tokens
+      const int kk = q / (TM / 8), c = (q % (TM / 8)) * 8;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (k0 + kk < K && m0 + c < M) v = *reinterpret_cast<const uint4*>(B + (int64_t)(k0 + kk) * ldb + m0 + c);
+      *reinterpret_cast<uint4*>(Bs + kk * LDB_ + c) = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8 bfr[NJ];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) bfr[j] = frag_tr(Bs, LDB_, 32 * ks, w * WM + 16 * j);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const bf16x8 af = frag_kc(As, LDA_, 16 * i, 32 * ks);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma16(af, bfr[j], acc[i][j]);
+      }
+    }
+    __syncthreads();
+  }
+  // epilogue through LDS: lane holds rows n = 16i + 4g + r of column m = w WM + 16 j + (l & 15)
+  bf16_t* Cs = reinterpret_cast<bf16_t*>(smem);
+  const int l = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Cs[(16 * i + 4 * (l >> 4) + r) * LDC_ + w * WM + 16 * j + (l & 15)] = f2bf(acc[i][j][r]);
+  __syncthreads();
+  for (int q = threadIdx.x; q < SK_TN * TM / 8; q += 256) {
+    const int r = q / (TM / 8), c = (q % (TM / 8)) * 8;
+    if (n0 + r < N && m0 + c < M) {
+      bf16_t* dst = C + (int64_t)(n0 + r) * ldc + m0 + c;
+      uint4 v = *reinterpret_cast<const uint4*>(Cs + r * LDC_ + c);
+      if (ACC) {
+        float f[8], o[8];
+        ld8bf(reinterpret_cast<const bf16_t*>(&v), f);
+        ld8bf(dst, o);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] += o[e];
+        st8bf(reinterpret_cast<bf16_t*>(&v), f);
+      }
+      *reinterpret_cast<uint4*>(dst) = v;
+    }
+  }
+}
+
+bool gemm_skinny_supported(int N, int K, int M, int64_t lda, int64_t ldb, int64_t ldc) {
+  return N > 0 && K > 0 && M > 0 && K % 8 == 0 && M % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0;
+}
+
+hipError_t launch_gemm_skinny(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int N,
+                              int K, int M, bool accumulate, hipStream_t st) {
+  if (!gemm_skinny_supported(N, K, M, lda, ldb, ldc)) return hipErrorInvalidValue;
+  const int ntiles = (N + SK_TN - 1) / SK_TN;
+  // wide outputs (N >= 256, small K) take 256-token tiles and one-MFMA-deep stages; narrow ones
+  // (N < 256, long K) 128-token tiles (the grid still covers the CUs) and 128-deep stages
+  const bool wide = ntiles >= 4;
+  const dim3 block(256);
+#define SK_LAUNCH(TMV, BKV)                                                                                   \
+  {                                                                                                           \
+    const dim3 grid((unsigned)((M + (TMV) - 1) / (TMV)), (unsigned)ntiles);                                   \
+    if (accumulate)                                                                                           \
+      hipLaunchKernelGGL((gemm_skinny_k<TMV, BKV, true>), grid, block, 0, st, (const bf16_t*)A, lda,             \
+                         (const bf16_t*)B, ldb, (bf16_t*)C, ldc, N, K, M);                                    \
+    else                                                                                                      \
+      hipLaunchKernelGGL((gemm_skinny_k<TMV, BKV, false>), grid, block, 0, st, (const bf16_t*)A, lda,            \
+                         (const bf16_t*)B, ldb, (bf16_t*)C, ldc, N, K, M);                                    \
+  }
+  if (wide) SK_LAUNCH(256, 32) else SK_LAUNCH(128, 128)
+#undef SK_LAUNCH
+  return hipGetLastError();
+}
+
 bool gemm_tn_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc) {
   return M > 0 && N > 0 && K > 0 && K % GBK == 0 && N % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0;
 }

@@ -55,6 +55,10 @@ hipError_t launch_conv_update(const void* x, int dt, int64_t sxb, void* state, i
 // ---- gemm.hip ---------------------------------------------------------------------------------
 // C[M, N] = A[M, K] . B[N, K]^T, bf16 in/out, fp32 accumulate (K % 64 == 0, N % 8 == 0)
 bool gemm_tn_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc);
+// C[N, M] (+)= A[N, K] . B[K, M], bf16, rows of B / C contiguous along M (channel-major activations)
+bool gemm_skinny_supported(int N, int K, int M, int64_t lda, int64_t ldb, int64_t ldc);
+hipError_t launch_gemm_skinny(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int N,
+                              int K, int M, bool accumulate, hipStream_t st);
 hipError_t launch_gemm_tn_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M,
                                int N, int K, hipStream_t st);
 // fp32 C[P, Q] (+)= dY[M, P]^T . X[M, Q] (bf16 token-major operands), split over M into

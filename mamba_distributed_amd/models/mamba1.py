@@ -17,6 +17,7 @@ materialisation), like upstream's MambaInnerFn.
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
@@ -39,6 +40,27 @@ def _flat(t: torch.Tensor) -> torch.Tensor:
     return t.permute(1, 0, 2).reshape(t.shape[1], -1)
 
 
+_SKINNY = os.environ.get("MAMBA_AMD_SKINNY", "1") != "0"  # A/B switch: 0 = hipBLASLt for the skinny GEMMs
+
+
+def _mm_cm(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None, accumulate: bool = False):
+    """``out (+)= A @ B`` for a small weight ``A`` (N, K) and a channel-major activation ``B`` (K, M):
+    the native streaming kernel (csrc/kernels/gemm.hip::gemm_skinny_k) for wide short-K products when
+    the layout allows it, torch.mm otherwise.  Used for x_proj / dt_proj and their input gradients."""
+    M = B.shape[1]
+    # native only for the wide, short-K products (delta = W_dt x_dbl[:R], dconv += W_x^T dx_dbl):
+    # for the long-K ones (x_dbl, dx_dbl[:R]) hipBLASLt measured faster (scripts/m1_gemms.py)
+    ok = (_SKINNY and A.shape[0] >= 256 and A.shape[1] <= 128 and A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16 and A.is_cuda and B.stride(1) == 1
+          and A.shape[1] % 8 == 0 and M % 8 == 0 and B.stride(0) % 8 == 0 and B.data_ptr() % 16 == 0
+          and (out is None or (out.stride(1) == 1 and out.stride(0) % 8 == 0 and out.data_ptr() % 16 == 0)))
+    if ok:
+        A = A.contiguous()
+        return _ext.ops().gemm_skinny(A, B, out, accumulate)
+    if accumulate:
+        return out.addmm_(A, B)
+    return torch.mm(A, B, out=out) if out is not None else torch.mm(A, B)
+
+
 class _Mamba1InnerFn(torch.autograd.Function):
     """conv1d+SiLU -> x_proj -> dt_proj -> selective scan(+D, *silu(z)) ; returns y as (di, b*l)."""
 
@@ -55,8 +77,8 @@ class _Mamba1InnerFn(torch.autograd.Function):
         conv_out = ops.conv1d_cf_fwd(x, w2, conv_b, True)                  # (b,di,l) in (di,b,l) memory
         co2 = _flat(conv_out)
         Wx, Wdt = W_x.to(cd), W_dt.to(cd)
-        x_dbl = torch.mm(Wx, co2)                                           # (R+2N, b*l)
-        delta = torch.mm(Wdt, x_dbl[:R])                                    # (di, b*l)
+        x_dbl = _mm_cm(Wx, co2)                                             # (R+2N, b*l)
+        delta = _mm_cm(Wdt, x_dbl[:R])                                      # (di, b*l)
         Bm = _cm(x_dbl[R:R + N], b, l).unsqueeze(1)                         # (b,1,N,l)
         Cm = _cm(x_dbl[R + N:], b, l).unsqueeze(1)
         y, carries, _ = ops.selscan_fwd(conv_out, _cm(delta, b, l), A, Bm, Cm, D, z, dt_bias, True)
@@ -85,10 +107,10 @@ class _Mamba1InnerFn(torch.autograd.Function):
             dxz3[:, di:], _cm(dx_dbl[R:R + N], b, l).unsqueeze(1), _cm(dx_dbl[R + N:], b, l).unsqueeze(1))
         dd2 = _flat(ddelta)
         dWdt = torch.mm(dd2, x_dbl[:R].t())                                  # (di, R)
-        torch.mm(Wdt.t(), dd2, out=dx_dbl[:R])                              # d x_dbl[:R]
+        _mm_cm(Wdt.t(), dd2, out=dx_dbl[:R])                                # d x_dbl[:R]
         dWx = torch.mm(dx_dbl, _flat(conv_out).t())                         # (R+2N, di)
         dco2 = _flat(du)
-        dco2.addmm_(Wx.t(), dx_dbl)                                         # du + W_x^T dx_dbl
+        _mm_cm(Wx.t(), dx_dbl, out=dco2, accumulate=True)                   # du + W_x^T dx_dbl
         _, dw, db = ops.conv1d_cf_bwd(x, w2, conv_b, _cm(dco2, b, l), True, dxz3[:, :di])
         return (dxz, dw.reshape(wshape).to(w2.dtype), db.to(conv_b.dtype) if conv_b is not None else None,
                 dWx.to(wx_dtype), dWdt.to(wdt_dtype), ddt_bias, dA, dD, None, None, None)

@@ -647,3 +647,22 @@ def test_activation_checkpointing_bitwise_on_gpu(cuda, layer):
     assert torch.equal(l0, l1), (l0, l1)
     for (k, p), q in zip(m1.named_parameters(), m0.parameters()):
         assert torch.equal(p.grad, q.grad), k
+
+
+@pytest.mark.parametrize("N,K,M", [(80, 1536, 32768), (1536, 48, 32768), (48, 1536, 4096), (1536, 80, 4096),
+                                   (72, 40, 1000), (130, 24, 264)])
+@pytest.mark.parametrize("acc", [False, True])
+def test_gemm_skinny(cuda, N, K, M, acc):
+    """gemm_skinny_k (channel-major Mamba-1 x_proj / dt_proj family) vs an fp32 matmul, including
+    row-strided B / out views, N / K / M not multiples of the tiles, and accumulation into out."""
+    from mamba_distributed_amd.ops import _ext
+    g = torch.Generator(device=cuda).manual_seed(0)
+    A = torch.randn(N, K, device=cuda, generator=g).to(torch.bfloat16)
+    Bbig = torch.randn(K + 16, M, device=cuda, generator=g).to(torch.bfloat16)
+    B = Bbig[:K]  # row-strided view like x_dbl[:R]
+    C0 = torch.randn(N, M, device=cuda, generator=g).to(torch.bfloat16)
+    out = C0.clone()
+    r = _ext.ops().gemm_skinny(A, B, out, acc)
+    ref = A.float() @ B.float() + (C0.float() if acc else 0)
+    assert r.data_ptr() == out.data_ptr()
+    assert rel(out, ref) < 8e-3, rel(out, ref)
