@@ -621,6 +621,28 @@ Tensor gemm_wgrad(Tensor dY, Tensor X, optional<Tensor> out, bool accumulate) {
   return C;
 }
 
+// dW (fp32, (P, Q)) (+)= dY X for a CHANNEL-major bf16 dY (P, M) and token-major X (M, Q)
+Tensor gemm_wgrad_cm(Tensor dY, Tensor X, optional<Tensor> out, bool accumulate) {
+  check_cuda(dY, "dY");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(dY.device());
+  TORCH_CHECK(dY.dim() == 2 && X.dim() == 2 && dY.size(1) == X.size(0), "gemm_wgrad_cm: dY (P,M), X (M,Q)");
+  TORCH_CHECK(dY.scalar_type() == at::kBFloat16 && X.scalar_type() == at::kBFloat16, "gemm_wgrad_cm: bf16 operands");
+  TORCH_CHECK(dY.stride(1) == 1 && X.stride(1) == 1, "gemm_wgrad_cm: unit inner strides");
+  TORCH_CHECK((uintptr_t)dY.data_ptr() % 16 == 0 && (uintptr_t)X.data_ptr() % 16 == 0, "gemm_wgrad_cm: 16-B aligned");
+  const int64_t P = dY.size(0), M = dY.size(1), Q = X.size(1);
+  TORCH_CHECK(mamba_amd::gemm_wgrad_cm_supported((int)M, (int)P, (int)Q, dY.stride(0), X.stride(0)),
+              "gemm_wgrad_cm: needs M % 64 == 0, P, Q, strides % 8 == 0");
+  Tensor C = out.has_value() && out->defined() ? *out : at::empty({P, Q}, dY.options().dtype(at::kFloat));
+  TORCH_CHECK(C.scalar_type() == at::kFloat && C.is_contiguous() && C.size(0) == P && C.size(1) == Q,
+              "gemm_wgrad_cm: out must be contiguous fp32 (P,Q)");
+  TORCH_CHECK(!accumulate || (out.has_value() && out->defined()), "gemm_wgrad_cm: accumulate needs out");
+  const int S = mamba_amd::gemm_wgrad_splits((int)M, (int)P, (int)Q);
+  auto part = at::empty({S, P, Q}, dY.options().dtype(at::kFloat));
+  HIPCHK(mamba_amd::launch_gemm_wgrad_cm(dY.data_ptr(), dY.stride(0), X.data_ptr(), X.stride(0), part.data_ptr<float>(),
+                                         C.data_ptr<float>(), (int)M, (int)P, (int)Q, accumulate, cur_stream()));
+  return C;
+}
+
 // ---------------------------------------------------------------------------------------------
 // fused Mamba-2 decode step (kernels/decode.hip).  Every operand is preallocated by the caller
 // (inference.FusedMamba2Decoder) so the three launches per layer can be captured in one HIP graph.
@@ -727,6 +749,7 @@ TORCH_LIBRARY(mamba_amd, m) {
         "-> Tensor[]");
   m.def("gemm_tn(Tensor A, Tensor B, Tensor(a!)? out=None) -> Tensor");
   m.def("gemm_wgrad(Tensor dY, Tensor X, Tensor(a!)? out=None, bool accumulate=False) -> Tensor");
+  m.def("gemm_wgrad_cm(Tensor dY, Tensor X, Tensor(a!)? out=None, bool accumulate=False) -> Tensor");
   m.def("gemm_skinny(Tensor A, Tensor B, Tensor(a!)? out=None, bool accumulate=False) -> Tensor");
   m.def("ssm_state_update(Tensor(a!) state, Tensor x, Tensor dt, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? z, "
         "Tensor? dt_bias, bool softplus) -> Tensor");
@@ -742,6 +765,7 @@ TORCH_LIBRARY_IMPL(mamba_amd, CUDA, m) {
   m.impl("gemm_tn", &gemm_tn);
   m.impl("gemm_wgrad", &gemm_wgrad);
   m.impl("gemm_skinny", &gemm_skinny);
+  m.impl("gemm_wgrad_cm", &gemm_wgrad_cm);
   m.impl("add_rmsnorm_bwd", &add_rmsnorm_bwd);
   m.impl("gated_rmsnorm_fwd", &gated_rmsnorm_fwd);
   m.impl("gated_rmsnorm_bwd", &gated_rmsnorm_bwd);

@@ -235,7 +235,10 @@ __device__ __forceinline__ bf16x8 wfrag(const char* lds, int k0, int c0) {
 // bandwidth (the per-CU L2 share); 256^2 halves that.  Operand tiles are [64 tokens][256 cols] stored
 // as two swizzled [64][128] halves; LDS 2 buffers x (32 + 32) KB = 128 KB -> one workgroup per CU,
 // so the split count targets one full round of workgroups.
-template <int TP, int TQ>
+// CM = true: dY is CHANNEL-major (P rows of M contiguous tokens, the Mamba-1 in_proj gradient d(xz)).
+// Its [TP][64-token] tile is then k-contiguous: two [128][64] halves DMA'd with the gemm_tn XOR
+// swizzle and read with the plain k-contiguous fragment (no transpose needed on that side).
+template <int TP, int TQ, bool CM>
 __global__ __launch_bounds__(512) void gemm_wgrad_big_k(const bf16_t* __restrict__ dY, int64_t ldy,
                                                         const bf16_t* __restrict__ X, int64_t ldx,
                                                         float* __restrict__ part, int M, int P, int Q, int mslice) {
@@ -267,10 +270,17 @@ __global__ __launch_bounds__(512) void gemm_wgrad_big_k(const bf16_t* __restrict
         const int tid = threadIdx.x & 255, w4 = tid >> 6;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int q = i * 256 + tid, r = q >> 4, s2 = q & 15;
-          const int col = min(p0 + h * WB + 8 * (s2 ^ (2 * wswz(r))), P - 8);
-          __builtin_amdgcn_global_load_lds((const void*)(dY + (int64_t)(m0 + r) * ldy + col),
-                                           (lds_void*)(buf + h * HB + (i * 256 + w4 * 64) * 16), 16, 0, 0);
+          if constexpr (CM) {  // [128 channels][64 tokens] half: slot (r, cs) <- source chunk cs ^ (r & 7)
+            const int q = i * 256 + tid, r = q >> 3, cs = q & 7;
+            const int row = min(p0 + h * WB + r, P - 1);  // rows past P are never stored
+            __builtin_amdgcn_global_load_lds((const void*)(dY + (int64_t)row * ldy + m0 + 8 * (cs ^ (r & 7))),
+                                             (lds_void*)(buf + h * HB + (i * 256 + w4 * 64) * 16), 16, 0, 0);
+          } else {
+            const int q = i * 256 + tid, r = q >> 4, s2 = q & 15;
+            const int col = min(p0 + h * WB + 8 * (s2 ^ (2 * wswz(r))), P - 8);
+            __builtin_amdgcn_global_load_lds((const void*)(dY + (int64_t)(m0 + r) * ldy + col),
+                                             (lds_void*)(buf + h * HB + (i * 256 + w4 * 64) * 16), 16, 0, 0);
+          }
         }
       }
     }
@@ -307,7 +317,7 @@ __global__ __launch_bounds__(512) void gemm_wgrad_big_k(const bf16_t* __restrict
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         const int c = wp * (TP / WPN) + 16 * i;
-        const bf16x8 af = wfrag(cur + (c / WB) * HB, 32 * ks, c % WB);
+        const bf16x8 af = CM ? frag(cur + (c / WB) * HB, c % WB, ks) : wfrag(cur + (c / WB) * HB, 32 * ks, c % WB);
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = mfma16(af, bfr[j], acc[i][j]);
       }
@@ -376,7 +386,7 @@ hipError_t launch_gemm_wgrad(const void* dY, int64_t ldy, const void* X, int64_t
   const int mslice = ((M + S - 1) / S + WK - 1) / WK * WK;
   if (big) {
     const int tiles = ((P + BT - 1) / BT) * ((Q + BT - 1) / BT);
-    hipLaunchKernelGGL((gemm_wgrad_big_k<BT, BT>), dim3(tiles * S), dim3(512), 0, st, (const bf16_t*)dY, ldy,
+    hipLaunchKernelGGL((gemm_wgrad_big_k<BT, BT, false>), dim3(tiles * S), dim3(512), 0, st, (const bf16_t*)dY, ldy,
                        (const bf16_t*)X, ldx, part, M, P, Q, mslice);
   } else {
     const int tiles = ((P + WB - 1) / WB) * ((Q + WB - 1) / WB);
@@ -507,6 +517,26 @@ hipError_t launch_gemm_skinny(const void* A, int64_t lda, const void* B, int64_t
   }
   if (wide) SK_LAUNCH(256, 32) else SK_LAUNCH(128, 128)
 #undef SK_LAUNCH
+  return hipGetLastError();
+}
+
+// dW (P, Q) (+)= dY X with a channel-major dY (P, M) (Mamba-1 d(xz)) and token-major X (M, Q)
+bool gemm_wgrad_cm_supported(int M, int P, int Q, int64_t ldy, int64_t ldx) {
+  return M % WK == 0 && P % 8 == 0 && Q % 8 == 0 && ldy % 8 == 0 && ldx % 8 == 0 && P >= 8 && Q >= 8;
+}
+
+hipError_t launch_gemm_wgrad_cm(const void* dY, int64_t ldy, const void* X, int64_t ldx, float* part, float* out,
+                                int M, int P, int Q, bool accumulate, hipStream_t st) {
+  if (!gemm_wgrad_cm_supported(M, P, Q, ldy, ldx)) return hipErrorInvalidValue;
+  const int S = wgrad_splits(M, P, Q, true);
+  const int mslice = ((M + S - 1) / S + WK - 1) / WK * WK;
+  const int tiles = ((P + BT - 1) / BT) * ((Q + BT - 1) / BT);
+  hipLaunchKernelGGL((gemm_wgrad_big_k<BT, BT, true>), dim3(tiles * S), dim3(512), 0, st, (const bf16_t*)dY, ldy,
+                     (const bf16_t*)X, ldx, part, M, P, Q, mslice);
+  MAMBA_HIP_CHECK(hipGetLastError());
+  const int64_t n = (int64_t)P * Q;
+  hipLaunchKernelGGL(wgrad_reduce_k, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, st, part, S, n, out,
+                     accumulate);
   return hipGetLastError();
 }
 

@@ -64,6 +64,9 @@ hipError_t launch_gemm_tn_bf16(const void* A, int64_t lda, const void* B, int64_
 // fp32 C[P, Q] (+)= dY[M, P]^T . X[M, Q] (bf16 token-major operands), split over M into
 // gemm_wgrad_splits() fp32 partials (part: splits * P * Q floats) summed in fixed order
 int gemm_wgrad_splits(int M, int P, int Q);
+bool gemm_wgrad_cm_supported(int M, int P, int Q, int64_t ldy, int64_t ldx);
+hipError_t launch_gemm_wgrad_cm(const void* dY, int64_t ldy, const void* X, int64_t ldx, float* part, float* out,
+                                int M, int P, int Q, bool accumulate, hipStream_t st);
 hipError_t launch_gemm_wgrad(const void* dY, int64_t ldy, const void* X, int64_t ldx, float* part, float* out,
                              int M, int P, int Q, bool accumulate, hipStream_t st);
 

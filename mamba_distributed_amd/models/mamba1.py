@@ -24,7 +24,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops import _ext
+from ..ops import _ext, grad_accum
 from ..ops.conv1d import causal_conv1d_fn, causal_conv1d_update
 from ..ops.reference import causal_conv1d_ref, selective_scan_ref, softplus_inverse
 from ..ops.selective_scan import selective_scan_fn, selective_state_update
@@ -40,6 +40,7 @@ def _flat(t: torch.Tensor) -> torch.Tensor:
     return t.permute(1, 0, 2).reshape(t.shape[1], -1)
 
 
+_NATIVE_INPROJ = os.environ.get("MAMBA_AMD_M1_NATIVE_INPROJ", "1") != "0"  # A/B switch
 _SKINNY = os.environ.get("MAMBA_AMD_SKINNY", "1") != "0"  # A/B switch: 0 = hipBLASLt for the skinny GEMMs
 
 
@@ -59,6 +60,49 @@ def _mm_cm(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,
     if accumulate:
         return out.addmm_(A, B)
     return torch.mm(A, B, out=out) if out is not None else torch.mm(A, B)
+
+
+class _InProjCMFn(torch.autograd.Function):
+    """xz (2di, b*l) = W_in h^T, channel-major (the Mamba-1 in_proj).  The bf16 weight cast is cached
+    for the optimizer step (ops/grad_accum.py) and the weight gradient dW = d(xz) h runs on the native
+    channel-major wgrad GEMM (csrc/kernels/gemm.hip, CM variant): fp32 out, added in place into
+    ``.grad`` on the no-sync micro-steps (side stream), no bf16 -> fp32 cast."""
+
+    @staticmethod
+    def forward(ctx, h2, weight, cd):
+        w = grad_accum.cached_cast(weight, cd)
+        ctx.save_for_backward(h2, w)
+        ctx.param = weight
+        return torch.mm(w, h2.t())
+
+    @staticmethod
+    def backward(ctx, dxz):
+        h2, w = ctx.saved_tensors
+        if dxz.stride(1) != 1:
+            dxz = dxz.contiguous()
+        dh = torch.mm(dxz.t(), w) if ctx.needs_input_grad[0] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            p = ctx.param
+            native = (dxz.dtype == torch.bfloat16 and h2.dtype == torch.bfloat16 and h2.stride(1) == 1
+                      and dxz.shape[1] % 64 == 0 and dxz.shape[0] % 8 == 0 and h2.shape[1] % 8 == 0
+                      and dxz.stride(0) % 8 == 0 and h2.stride(0) % 8 == 0
+                      and dxz.data_ptr() % 16 == 0 and h2.data_ptr() % 16 == 0)
+            if (native and grad_accum.accumulable(p) and p.grad.dtype == torch.float32 and p.grad.is_contiguous()
+                    and p.grad.shape == w.shape):
+                side = grad_accum.side_stream(dxz.device)
+                if side is None:
+                    _ext.ops().gemm_wgrad_cm(dxz, h2, p.grad, True)
+                else:
+                    side.wait_stream(torch.cuda.current_stream(dxz.device))
+                    with torch.cuda.stream(side):
+                        _ext.ops().gemm_wgrad_cm(dxz, h2, p.grad, True)
+                    dxz.record_stream(side)
+                    h2.record_stream(side)
+            else:
+                dw = _ext.ops().gemm_wgrad_cm(dxz, h2, None, False) if native else torch.mm(dxz, h2).float()
+                dw = grad_accum.defer(p, dw.to(p.dtype))
+        return dh, dw, None
 
 
 class _Mamba1InnerFn(torch.autograd.Function):
@@ -186,7 +230,10 @@ class Mamba(nn.Module):
         cd = torch.get_autocast_dtype("cuda") if (hidden_states.is_cuda and torch.is_autocast_enabled("cuda")) else hidden_states.dtype
         A = -torch.exp(self.A_log.float())
         h2 = hidden_states.reshape(b * l, -1).to(cd)
-        xz = torch.mm(self.in_proj.weight.to(cd), h2.t())                  # (2di, b*l)
+        if _NATIVE_INPROJ and _ext.use_native(h2) and self.in_proj.weight.requires_grad:
+            xz = _InProjCMFn.apply(h2, self.in_proj.weight, cd)            # (2di, b*l)
+        else:
+            xz = torch.mm(self.in_proj.weight.to(cd), h2.t())              # (2di, b*l)
         if self.in_proj.bias is not None:
             xz = xz + self.in_proj.bias.to(cd)[:, None]
         if conv_state is None and self.use_fast_path and _ext.use_native(xz):

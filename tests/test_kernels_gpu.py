@@ -666,3 +666,20 @@ def test_gemm_skinny(cuda, N, K, M, acc):
     ref = A.float() @ B.float() + (C0.float() if acc else 0)
     assert r.data_ptr() == out.data_ptr()
     assert rel(out, ref) < 8e-3, rel(out, ref)
+
+
+@pytest.mark.parametrize("P,M,Q", [(3072, 32768, 768), (2048, 4096, 1024), (200, 1024, 136), (8, 64, 8)])
+@pytest.mark.parametrize("acc", [False, True])
+def test_gemm_wgrad_channel_major(cuda, P, M, Q, acc):
+    """gemm_wgrad_cm (Mamba-1 in_proj dW = d(xz) h with a channel-major d(xz)) vs an fp32 matmul,
+    fp32 output, accumulation into an existing gradient; P / Q not multiples of the 256 tiles."""
+    from mamba_distributed_amd.ops import _ext
+    g = torch.Generator(device=cuda).manual_seed(0)
+    dY = torch.randn(P, M, device=cuda, generator=g).to(torch.bfloat16)
+    X = torch.randn(M, Q, device=cuda, generator=g).to(torch.bfloat16)
+    out = torch.randn(P, Q, device=cuda, generator=g)
+    base = out.clone()
+    r = _ext.ops().gemm_wgrad_cm(dY, X, out if acc else None, acc)
+    ref = dY.float() @ X.float() + (base if acc else 0)
+    assert r.dtype == torch.float32
+    assert rel(r, ref) < 2e-3, rel(r, ref)
