@@ -621,15 +621,19 @@ Tensor gemm_wgrad(Tensor dY, Tensor X, optional<Tensor> out, bool accumulate) {
   return C;
 }
 
-// dW (fp32, (P, Q)) (+)= dY X for a CHANNEL-major bf16 dY (P, M) and token-major X (M, Q)
-Tensor gemm_wgrad_cm(Tensor dY, Tensor X, optional<Tensor> out, bool accumulate) {
+// dW (fp32, (P, Q)) (+)= dY^T X over M tokens where either operand may be CHANNEL-major:
+//   dy_cm: dY given as (P, M) (else (M, P));  x_cm: X given as (Q, M) (else (M, Q)).  At least one is.
+Tensor gemm_wgrad_cm(Tensor dY, Tensor X, optional<Tensor> out, bool accumulate, bool dy_cm, bool x_cm) {
   check_cuda(dY, "dY");
   at::hip::HIPGuardMasqueradingAsCUDA guard(dY.device());
-  TORCH_CHECK(dY.dim() == 2 && X.dim() == 2 && dY.size(1) == X.size(0), "gemm_wgrad_cm: dY (P,M), X (M,Q)");
+  TORCH_CHECK(dy_cm || x_cm, "gemm_wgrad_cm: use gemm_wgrad for two token-major operands");
+  TORCH_CHECK(dY.dim() == 2 && X.dim() == 2, "gemm_wgrad_cm: 2-D operands");
   TORCH_CHECK(dY.scalar_type() == at::kBFloat16 && X.scalar_type() == at::kBFloat16, "gemm_wgrad_cm: bf16 operands");
   TORCH_CHECK(dY.stride(1) == 1 && X.stride(1) == 1, "gemm_wgrad_cm: unit inner strides");
   TORCH_CHECK((uintptr_t)dY.data_ptr() % 16 == 0 && (uintptr_t)X.data_ptr() % 16 == 0, "gemm_wgrad_cm: 16-B aligned");
-  const int64_t P = dY.size(0), M = dY.size(1), Q = X.size(1);
+  const int64_t P = dy_cm ? dY.size(0) : dY.size(1), M = dy_cm ? dY.size(1) : dY.size(0);
+  const int64_t Q = x_cm ? X.size(0) : X.size(1), MX = x_cm ? X.size(1) : X.size(0);
+  TORCH_CHECK(M == MX, "gemm_wgrad_cm: token counts differ");
   TORCH_CHECK(mamba_amd::gemm_wgrad_cm_supported((int)M, (int)P, (int)Q, dY.stride(0), X.stride(0)),
               "gemm_wgrad_cm: needs M % 64 == 0, P, Q, strides % 8 == 0");
   Tensor C = out.has_value() && out->defined() ? *out : at::empty({P, Q}, dY.options().dtype(at::kFloat));
@@ -639,7 +643,8 @@ Tensor gemm_wgrad_cm(Tensor dY, Tensor X, optional<Tensor> out, bool accumulate)
   const int S = mamba_amd::gemm_wgrad_splits((int)M, (int)P, (int)Q);
   auto part = at::empty({S, P, Q}, dY.options().dtype(at::kFloat));
   HIPCHK(mamba_amd::launch_gemm_wgrad_cm(dY.data_ptr(), dY.stride(0), X.data_ptr(), X.stride(0), part.data_ptr<float>(),
-                                         C.data_ptr<float>(), (int)M, (int)P, (int)Q, accumulate, cur_stream()));
+                                         C.data_ptr<float>(), (int)M, (int)P, (int)Q, accumulate, dy_cm, x_cm,
+                                         cur_stream()));
   return C;
 }
 
@@ -749,7 +754,8 @@ TORCH_LIBRARY(mamba_amd, m) {
         "-> Tensor[]");
   m.def("gemm_tn(Tensor A, Tensor B, Tensor(a!)? out=None) -> Tensor");
   m.def("gemm_wgrad(Tensor dY, Tensor X, Tensor(a!)? out=None, bool accumulate=False) -> Tensor");
-  m.def("gemm_wgrad_cm(Tensor dY, Tensor X, Tensor(a!)? out=None, bool accumulate=False) -> Tensor");
+  m.def("gemm_wgrad_cm(Tensor dY, Tensor X, Tensor(a!)? out=None, bool accumulate=False, bool dy_cm=True, "
+        "bool x_cm=False) -> Tensor");
   m.def("gemm_skinny(Tensor A, Tensor B, Tensor(a!)? out=None, bool accumulate=False) -> Tensor");
   m.def("ssm_state_update(Tensor(a!) state, Tensor x, Tensor dt, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? z, "
         "Tensor? dt_bias, bool softplus) -> Tensor");

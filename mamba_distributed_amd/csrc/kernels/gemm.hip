@@ -238,7 +238,9 @@ __device__ __forceinline__ bf16x8 wfrag(const char* lds, int k0, int c0) {
 // CM = true: dY is CHANNEL-major (P rows of M contiguous tokens, the Mamba-1 in_proj gradient d(xz)).
 // Its [TP][64-token] tile is then k-contiguous: two [128][64] halves DMA'd with the gemm_tn XOR
 // swizzle and read with the plain k-contiguous fragment (no transpose needed on that side).
-template <int TP, int TQ, bool CM>
+// CMB = true: X is channel-major as well (Q rows of M contiguous tokens, e.g. the Mamba-1 scan output
+// y for the out_proj gradient): staged and read exactly like a CM dY tile.
+template <int TP, int TQ, bool CM, bool CMB = false>
 __global__ __launch_bounds__(512) void gemm_wgrad_big_k(const bf16_t* __restrict__ dY, int64_t ldy,
                                                         const bf16_t* __restrict__ X, int64_t ldx,
                                                         float* __restrict__ part, int M, int P, int Q, int mslice) {
@@ -291,10 +293,17 @@ __global__ __launch_bounds__(512) void gemm_wgrad_big_k(const bf16_t* __restrict
         const int tid = threadIdx.x & 255, w4 = tid >> 6;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int q = i * 256 + tid, r = q >> 4, s2 = q & 15;
-          const int col = min(q0 + h * WB + 8 * (s2 ^ (2 * wswz(r))), Q - 8);
-          __builtin_amdgcn_global_load_lds((const void*)(X + (int64_t)(m0 + r) * ldx + col),
-                                           (lds_void*)(buf + AB + h * HB + (i * 256 + w4 * 64) * 16), 16, 0, 0);
+          if constexpr (CMB) {
+            const int q = i * 256 + tid, r = q >> 3, cs = q & 7;
+            const int row = min(q0 + h * WB + r, Q - 1);  // rows past Q are never stored
+            __builtin_amdgcn_global_load_lds((const void*)(X + (int64_t)row * ldx + m0 + 8 * (cs ^ (r & 7))),
+                                             (lds_void*)(buf + AB + h * HB + (i * 256 + w4 * 64) * 16), 16, 0, 0);
+          } else {
+            const int q = i * 256 + tid, r = q >> 4, s2 = q & 15;
+            const int col = min(q0 + h * WB + 8 * (s2 ^ (2 * wswz(r))), Q - 8);
+            __builtin_amdgcn_global_load_lds((const void*)(X + (int64_t)(m0 + r) * ldx + col),
+                                             (lds_void*)(buf + AB + h * HB + (i * 256 + w4 * 64) * 16), 16, 0, 0);
+          }
         }
       }
     }
@@ -312,7 +321,7 @@ __global__ __launch_bounds__(512) void gemm_wgrad_big_k(const bf16_t* __restrict
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int c = wq * (TQ / WQN) + 16 * j;
-        bfr[j] = wfrag(cur + AB + (c / WB) * HB, 32 * ks, c % WB);
+        bfr[j] = CMB ? frag(cur + AB + (c / WB) * HB, c % WB, ks) : wfrag(cur + AB + (c / WB) * HB, 32 * ks, c % WB);
       }
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
@@ -526,13 +535,20 @@ bool gemm_wgrad_cm_supported(int M, int P, int Q, int64_t ldy, int64_t ldx) {
 }
 
 hipError_t launch_gemm_wgrad_cm(const void* dY, int64_t ldy, const void* X, int64_t ldx, float* part, float* out,
-                                int M, int P, int Q, bool accumulate, hipStream_t st) {
-  if (!gemm_wgrad_cm_supported(M, P, Q, ldy, ldx)) return hipErrorInvalidValue;
+                                int M, int P, int Q, bool accumulate, bool dy_cm, bool x_cm, hipStream_t st) {
+  if (!gemm_wgrad_cm_supported(M, P, Q, ldy, ldx) || (!dy_cm && !x_cm)) return hipErrorInvalidValue;
   const int S = wgrad_splits(M, P, Q, true);
   const int mslice = ((M + S - 1) / S + WK - 1) / WK * WK;
   const int tiles = ((P + BT - 1) / BT) * ((Q + BT - 1) / BT);
-  hipLaunchKernelGGL((gemm_wgrad_big_k<BT, BT, true>), dim3(tiles * S), dim3(512), 0, st, (const bf16_t*)dY, ldy,
-                     (const bf16_t*)X, ldx, part, M, P, Q, mslice);
+  if (dy_cm && x_cm)
+    hipLaunchKernelGGL((gemm_wgrad_big_k<BT, BT, true, true>), dim3(tiles * S), dim3(512), 0, st, (const bf16_t*)dY,
+                       ldy, (const bf16_t*)X, ldx, part, M, P, Q, mslice);
+  else if (dy_cm)
+    hipLaunchKernelGGL((gemm_wgrad_big_k<BT, BT, true, false>), dim3(tiles * S), dim3(512), 0, st, (const bf16_t*)dY,
+                       ldy, (const bf16_t*)X, ldx, part, M, P, Q, mslice);
+  else
+    hipLaunchKernelGGL((gemm_wgrad_big_k<BT, BT, false, true>), dim3(tiles * S), dim3(512), 0, st, (const bf16_t*)dY,
+                       ldy, (const bf16_t*)X, ldx, part, M, P, Q, mslice);
   MAMBA_HIP_CHECK(hipGetLastError());
   const int64_t n = (int64_t)P * Q;
   hipLaunchKernelGGL(wgrad_reduce_k, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, st, part, S, n, out,

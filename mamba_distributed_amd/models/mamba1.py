@@ -84,25 +84,36 @@ class _InProjCMFn(torch.autograd.Function):
         dw = None
         if ctx.needs_input_grad[1]:
             p = ctx.param
-            native = (dxz.dtype == torch.bfloat16 and h2.dtype == torch.bfloat16 and h2.stride(1) == 1
-                      and dxz.shape[1] % 64 == 0 and dxz.shape[0] % 8 == 0 and h2.shape[1] % 8 == 0
-                      and dxz.stride(0) % 8 == 0 and h2.stride(0) % 8 == 0
-                      and dxz.data_ptr() % 16 == 0 and h2.data_ptr() % 16 == 0)
-            if (native and grad_accum.accumulable(p) and p.grad.dtype == torch.float32 and p.grad.is_contiguous()
-                    and p.grad.shape == w.shape):
-                side = grad_accum.side_stream(dxz.device)
-                if side is None:
-                    _ext.ops().gemm_wgrad_cm(dxz, h2, p.grad, True)
-                else:
-                    side.wait_stream(torch.cuda.current_stream(dxz.device))
-                    with torch.cuda.stream(side):
-                        _ext.ops().gemm_wgrad_cm(dxz, h2, p.grad, True)
-                    dxz.record_stream(side)
-                    h2.record_stream(side)
-            else:
-                dw = _ext.ops().gemm_wgrad_cm(dxz, h2, None, False) if native else torch.mm(dxz, h2).float()
-                dw = grad_accum.defer(p, dw.to(p.dtype))
+            handled, dw = _wgrad_native(p, dxz, h2, True, False)
+            if not handled:
+                dw = grad_accum.defer(p, torch.mm(dxz, h2).to(p.dtype))
         return dh, dw, None
+
+
+def _wgrad_native(p, dY, X, dy_cm, x_cm):
+    """Weight gradient of a channel-major projection on the native wgrad GEMM (csrc/kernels/gemm.hip,
+    CM / CMB variants): fp32, added in place into ``p.grad`` on the no-sync micro-steps (side stream,
+    ops/grad_accum.py), otherwise returned through grad_accum.defer.  Returns (handled, dw);
+    handled is False when the layout is not supported and the caller must fall back."""
+    M = dY.shape[1] if dy_cm else dY.shape[0]
+    ok = (dY.dtype == torch.bfloat16 and X.dtype == torch.bfloat16 and dY.stride(1) == 1 and X.stride(1) == 1
+          and M % 64 == 0 and dY.stride(0) % 8 == 0 and X.stride(0) % 8 == 0 and dY.shape[0] % 8 == 0
+          and X.shape[0] % 8 == 0 and dY.shape[1] % 8 == 0 and X.shape[1] % 8 == 0
+          and dY.data_ptr() % 16 == 0 and X.data_ptr() % 16 == 0)
+    if not ok:
+        return False, None
+    if grad_accum.accumulable(p) and p.grad.dtype == torch.float32 and p.grad.is_contiguous():
+        side = grad_accum.side_stream(dY.device)
+        if side is None:
+            _ext.ops().gemm_wgrad_cm(dY, X, p.grad, True, dy_cm, x_cm)
+        else:
+            side.wait_stream(torch.cuda.current_stream(dY.device))
+            with torch.cuda.stream(side):
+                _ext.ops().gemm_wgrad_cm(dY, X, p.grad, True, dy_cm, x_cm)
+            dY.record_stream(side)
+            X.record_stream(side)
+        return True, None
+    return True, grad_accum.defer(p, _ext.ops().gemm_wgrad_cm(dY, X, None, False, dy_cm, x_cm).to(p.dtype))
 
 
 class _Mamba1InnerFn(torch.autograd.Function):
@@ -240,6 +251,8 @@ class Mamba(nn.Module):
             y2 = _Mamba1InnerFn.apply(xz, self.conv1d.weight, self.conv1d.bias, self.x_proj.weight,
                                       self.dt_proj.weight, self.dt_proj.bias.float(), A, self.D.float(),
                                       b, l, cd)
+            # out_proj stays on hipBLASLt end to end: a native dW with a channel-major y operand
+            # (gemm_wgrad_cm, x_cm=True) measured -4.5% in an interleaved A/B
             out = F.linear(y2.t().to(cd), self.out_proj.weight.to(cd),
                            None if self.out_proj.bias is None else self.out_proj.bias.to(cd))
             return out.view(b, l, -1)

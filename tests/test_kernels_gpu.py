@@ -683,3 +683,21 @@ def test_gemm_wgrad_channel_major(cuda, P, M, Q, acc):
     ref = dY.float() @ X.float() + (base if acc else 0)
     assert r.dtype == torch.float32
     assert rel(r, ref) < 2e-3, rel(r, ref)
+
+
+@pytest.mark.parametrize("dy_cm,x_cm", [(False, True), (True, True)])
+@pytest.mark.parametrize("P,M,Q", [(768, 32768, 1536), (200, 1024, 136)])
+def test_gemm_wgrad_channel_major_x(cuda, dy_cm, x_cm, P, M, Q):
+    """gemm_wgrad_cm with a channel-major X (Mamba-1 out_proj dW = dout^T y^T from the (di, b*l) scan
+    output) and with both operands channel-major, accumulating into fp32."""
+    from mamba_distributed_amd.ops import _ext
+    g = torch.Generator(device=cuda).manual_seed(1)
+    dY = torch.randn(P, M, device=cuda, generator=g).to(torch.bfloat16)   # logical (P, M)
+    X = torch.randn(Q, M, device=cuda, generator=g).to(torch.bfloat16)    # logical (Q, M)
+    out = torch.randn(P, Q, device=cuda, generator=g)
+    base = out.clone()
+    dY_arg = dY if dy_cm else dY.t().contiguous()
+    X_arg = X if x_cm else X.t().contiguous()
+    _ext.ops().gemm_wgrad_cm(dY_arg, X_arg, out, True, dy_cm, x_cm)
+    ref = dY.float() @ X.float().t() + base
+    assert rel(out, ref) < 2e-3, rel(out, ref)
