@@ -40,6 +40,7 @@ def _flat(t: torch.Tensor) -> torch.Tensor:
     return t.permute(1, 0, 2).reshape(t.shape[1], -1)
 
 
+_NATIVE_XDT = os.environ.get("MAMBA_AMD_M1_NATIVE_XDT", "1") != "0"  # A/B switch: x_proj / dt_proj dW
 _NATIVE_INPROJ = os.environ.get("MAMBA_AMD_M1_NATIVE_INPROJ", "1") != "0"  # A/B switch
 _SKINNY = os.environ.get("MAMBA_AMD_SKINNY", "1") != "0"  # A/B switch: 0 = hipBLASLt for the skinny GEMMs
 
@@ -139,6 +140,7 @@ class _Mamba1InnerFn(torch.autograd.Function):
         y, carries, _ = ops.selscan_fwd(conv_out, _cm(delta, b, l), A, Bm, Cm, D, z, dt_bias, True)
         ctx.save_for_backward(xz, w2, conv_b, Wx, Wdt, dt_bias, A, D, conv_out, x_dbl, delta, carries)
         ctx.meta = (b, l, conv_w.shape, W_x.dtype, W_dt.dtype)
+        ctx.wparams = (W_x, W_dt)  # the parameters themselves (native weight gradients accumulate into .grad)
         return _flat(y)
 
     @staticmethod
@@ -161,14 +163,25 @@ class _Mamba1InnerFn(torch.autograd.Function):
             Bm, Cm, D, z, dt_bias, carries, True,
             dxz3[:, di:], _cm(dx_dbl[R:R + N], b, l).unsqueeze(1), _cm(dx_dbl[R + N:], b, l).unsqueeze(1))
         dd2 = _flat(ddelta)
-        dWdt = torch.mm(dd2, x_dbl[:R].t())                                  # (di, R)
+        pWx, pWdt = ctx.wparams
+        if _NATIVE_XDT:  # both operands channel-major: (di, M) . (R, M)^T on the native wgrad GEMM
+            ok_dt, dWdt = _wgrad_native(pWdt, dd2, x_dbl[:R], True, True)
+        else:
+            ok_dt = False
+        if not ok_dt:
+            dWdt = torch.mm(dd2, x_dbl[:R].t()).to(wdt_dtype)                # (di, R)
         _mm_cm(Wdt.t(), dd2, out=dx_dbl[:R])                                # d x_dbl[:R]
-        dWx = torch.mm(dx_dbl, _flat(conv_out).t())                         # (R+2N, di)
+        if _NATIVE_XDT:
+            ok_x, dWx = _wgrad_native(pWx, dx_dbl, _flat(conv_out), True, True)
+        else:
+            ok_x = False
+        if not ok_x:
+            dWx = torch.mm(dx_dbl, _flat(conv_out).t()).to(wx_dtype)         # (R+2N, di)
         dco2 = _flat(du)
         _mm_cm(Wx.t(), dx_dbl, out=dco2, accumulate=True)                   # du + W_x^T dx_dbl
         _, dw, db = ops.conv1d_cf_bwd(x, w2, conv_b, _cm(dco2, b, l), True, dxz3[:, :di])
         return (dxz, dw.reshape(wshape).to(w2.dtype), db.to(conv_b.dtype) if conv_b is not None else None,
-                dWx.to(wx_dtype), dWdt.to(wdt_dtype), ddt_bias, dA, dD, None, None, None)
+                dWx, dWdt, ddt_bias, dA, dD, None, None, None)
 
 
 def mamba1_inner_ref(xz3, conv_w, conv_b, W_x, W_dt, dt_bias, A, D):
