@@ -120,6 +120,33 @@ __device__ __forceinline__ void scan_suffix(float& a, float& b) {
   b = fmaf(a, cb, b);
   a *= ca;
 }
+// The forward replay's prefix scan (a, b) and the adjoint's suffix scan (c, d) are independent: one
+// asm block interleaves their row steps so each DPP read is >= 3 instructions after the write it
+// depends on -- no s_nop inside the 4 row steps (vs. one per op when each scan runs alone).  The
+// prefix's two cross-row broadcasts follow; the suffix's cross-row part is the readlane composition.
+__device__ __forceinline__ void scan_prefix_suffix(float& a, float& b, float& c, float& d) {
+#define SS_PAIR(K)                                                                         \
+  "v_fmac_f32_dpp %1, %1, %0 row_shr:" K " row_mask:0xf bank_mask:0xf\n\t"                  \
+  "v_fmac_f32_dpp %3, %3, %2 row_shl:" K " row_mask:0xf bank_mask:0xf\n\t"                  \
+  "v_mul_f32_dpp %0, %0, %0 row_shr:" K " row_mask:0xf bank_mask:0xf\n\t"                   \
+  "v_mul_f32_dpp %2, %2, %2 row_shl:" K " row_mask:0xf bank_mask:0xf\n\t"
+  asm volatile("s_nop 1\n\t" SS_PAIR("1") SS_PAIR("2") SS_PAIR("4") SS_PAIR("8")
+               SS_DPP2("row_bcast:15 row_mask:0xa bank_mask:0xf") SS_DPP2("row_bcast:31 row_mask:0xc bank_mask:0xf")
+               "s_nop 1"
+               : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+#undef SS_PAIR
+  // suffix: compose the four row totals (lanes 0/16/32/48) through readlane, as scan_suffix
+  const float a1 = readlanef(c, 16), b1 = readlanef(d, 16);
+  const float a2 = readlanef(c, 32), b2 = readlanef(d, 32);
+  const float a3 = readlanef(c, 48), b3 = readlanef(d, 48);
+  const float c1a = a2 * a3, c1b = fmaf(a2, b3, b2);
+  const float c0a = a1 * c1a, c0b = fmaf(a1, c1b, b1);
+  const int row = (threadIdx.x & 63) >> 4;
+  const float ca = row == 0 ? c0a : row == 1 ? c1a : row == 2 ? a3 : 1.f;
+  const float cb = row == 0 ? c0b : row == 1 ? c1b : row == 2 ? b3 : 0.f;
+  d = fmaf(c, cb, d);
+  c *= ca;
+}
 #undef SS_DPP2
 __device__ __forceinline__ float wave_sum_dpp(float v) {
   v += dppf<0x111>(0.f, v);
@@ -736,8 +763,12 @@ __global__ __launch_bounds__(256) void selscan_bwd_fast_k(SelScanArgs a) {
           cb = fmaf(av[i], cb, xb[i]);
           ca *= av[i];
         }
-        const float prod = ca;
-        scan_prefix(ca, cb);
+        // adjoint x_t = a_t (dy_t C_t + x_{t+1}): this lane's map, composed before the scans so the
+        // prefix (forward replay) and suffix (adjoint) scans run interleaved
+        float ma = ca, mb = 0.f;
+#pragma unroll
+        for (int i = IT - 1; i >= 0; --i) mb = av[i] * fmaf(dy[i], Cv[i], mb);
+        scan_prefix_suffix(ca, cb, ma, mb);
         const float hend = fmaf(ca, hcn, cb);
         float h = dppf<0x138>(hcn, hend);  // wave_shr:1 -> state before this lane's first step
 #pragma unroll
@@ -746,11 +777,6 @@ __global__ __launch_bounds__(256) void selscan_bwd_fast_k(SelScanArgs a) {
           hs[i] = h;
           yv[i] = fmaf(Cv[i], h, yv[i]);
         }
-        // adjoint x_t = a_t (dy_t C_t + x_{t+1}) as a suffix scan of affine maps
-        float ma = prod, mb = 0.f;
-#pragma unroll
-        for (int i = IT - 1; i >= 0; --i) mb = av[i] * fmaf(dy[i], Cv[i], mb);
-        scan_suffix(ma, mb);
         const float xc = lamc[k][n];
         const float xfirst = fmaf(ma, xc, mb);
         float x = dppf<0x130>(xc, xfirst);  // wave_shl:1 -> adjoint after this lane's last step
