@@ -110,6 +110,14 @@ def run_micro_batches(model, next_batch: Callable, accum: int, compute_loss: Cal
     # on the other stream (even ``accum``): without this wait, blocks freed by zero_grad are handed
     # to forward 0's activations while AdamW may still be reading them as gradients
     other.wait_stream(main)
+    # A leaf's AccumulateGrad node lives as long as any in-flight graph holds it, so with two
+    # micro-batch graphs alive at once it was usually created on the other stream; autograd then
+    # accumulates on that stream behind an event wait on the producer.  That is ordered (see the
+    # module docstring's bitwise test) and adds no wait beyond "backward k after backward k-1": silence the
+    # per-backward warning torch emits about it.
+    _quiet = getattr(torch.autograd.graph, "set_warn_on_accumulate_grad_stream_mismatch", None)
+    if _quiet is not None:
+        _quiet(False)
     losses = [None] * accum
 
     def forward(k):
