@@ -26,6 +26,22 @@ BASELINE_TOK_S = 238000.0  # BASELINE.md derived 8xA100 node throughput (no publ
 METRIC = "tokens/sec (whole node) Mamba-2 280M DDP at 1/2/4/8 MI355X; HellaSwag acc"
 
 
+def _relaunch_under_torchrun(argv, n):
+    """``python bench.py --gpus N`` outside torchrun: start N ranks with torch.distributed.run as a
+    CHILD process (before this process touches the GPU: no exec from a GPU-initialised process)
+    and exit with its return code, so a multi-GPU request can never silently measure one GPU."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -52,6 +68,8 @@ def main():
     p.add_argument("--dp-impl", default="native", choices=["native", "ddp"],
                    help="gradient all-reduce: native bucketed reducer (parallel/reducer.py) or torch DDP")
     a = p.parse_args()
+    if a.gpus > 1 and "RANK" not in os.environ:
+        sys.exit(_relaunch_under_torchrun(sys.argv[1:], a.gpus))
     if a.reference_ops:
         os.environ["MAMBA_AMD_FORCE_REFERENCE"] = "1"
 
@@ -65,6 +83,10 @@ def main():
     info = init_distributed("auto")
     world = info.world_size
     dev = info.device
+    if world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but the job has {world} rank(s); refusing to report", file=sys.stderr)
+        destroy()
+        sys.exit(2)
     assert a.global_batch_tokens % (a.B * a.T * world) == 0
     accum = a.global_batch_tokens // (a.B * a.T * world)
     from mamba_distributed_amd.utils.gemm_tuning import enable_tuned_gemms
@@ -105,8 +127,12 @@ def main():
             print(f"step loss {loss_acc.item():.5f} grad_norm {norm.item():.4f}", flush=True)
         return loss_acc
 
+    red = ddp_mod._reducer(dmodel)
     for _ in range(a.warmup):
         step()
+    if red is not None:
+        red.timing = True
+        red.exposed_ms()
     barrier()
     sync()
     t0 = time.perf_counter()
@@ -117,6 +143,16 @@ def main():
     elapsed = torch.tensor(time.perf_counter() - t0, device=dev, dtype=torch.float64)
     all_reduce_max(elapsed)
     elapsed = float(elapsed.item())
+    comm = {"backend": info.backend, "world_size": world}
+    if red is not None:
+        exp = red.exposed_ms()
+        red.timing = False
+        ex = torch.tensor([sorted(exp)[len(exp) // 2] if exp else 0.0], device=dev, dtype=torch.float64)
+        all_reduce_max(ex)
+        bb = red.bucket_bytes()
+        comm.update({"exposed_allreduce_ms_per_step": round(float(ex.item()), 3), "n_buckets": len(bb),
+                     "bucket_mb": [round(b / 2**20, 1) for b in bb],
+                     "grad_bytes": int(sum(bb)), "grad_comm_dtype": a.grad_comm_dtype})
     peak_gb = torch.cuda.max_memory_allocated() / 2**30 if dev.startswith("cuda") else 0.0
     loss_v = float(last.item())
     if a.profile_steps and info.master:
@@ -160,6 +196,8 @@ def main():
                 "activation_checkpointing": a.activation_checkpointing,
                 "final_loss": round(loss_v, 4),
                 "peak_mem_gb": round(peak_gb, 1),
+                "comm": comm,
+                "per_gpu_tok_s": round(value / world, 1),
             },
         }
         print(json.dumps(out), flush=True)

@@ -115,9 +115,15 @@ def score_example(model, tokens, mask, autocast_dtype: Optional[torch.dtype] = N
 @torch.no_grad()
 def evaluate(model_type, hf_model_name: str, device: str = "cuda", checkpoint_path: str = CHECKPOINT_PATH,
              data_dir: str = "hellaswag", num_examples: int = 2000, out_file: str = "log/hellaswag_eval.txt",
-             dtype: str = "fp32", model: Optional[LMHeadModel] = None, verbose: bool = True) -> float:
+             dtype: str = "fp32", model: Optional[LMHeadModel] = None, verbose: bool = True,
+             allow_byte_tokenizer: bool = False, enc=None) -> float:
     torch.set_float32_matmul_precision("high")
-    enc = get_encoding("gpt2")
+    enc = enc if enc is not None else get_encoding("gpt2")
+    tok_name = getattr(enc, "name", type(enc).__name__)
+    if tok_name == "bytes" and not allow_byte_tokenizer:
+        # a GPT-2-BPE-trained model scored on byte ids prints a plausible-looking, meaningless accuracy
+        raise RuntimeError("HellaSwag needs the GPT-2 BPE (tiktoken or MAMBA_AMD_TOKENIZER_DIR); only the byte "
+                           "fallback tokenizer is available.  Pass --allow-byte-tokenizer to score anyway.")
     if model is None:
         if ModelType(model_type) == ModelType.CUSTOM:
             model = load_model_from_checkpoint(checkpoint_path, device, enc=enc)
@@ -151,7 +157,10 @@ def evaluate(model_type, hf_model_name: str, device: str = "cuda", checkpoint_pa
     if out_file:
         os.makedirs(os.path.dirname(out_file) or ".", exist_ok=True)
         with open(out_file, "a") as f:
-            f.write(f"{num_total} {num_correct_norm}/{num_total} {acc:.4f}")
+            f.write(f"{num_total} {num_correct_norm}/{num_total} {acc:.4f}" +
+                    ("" if tok_name != "bytes" else f" tokenizer={tok_name}"))
+    if verbose:
+        print(f"hellaswag acc_norm {acc:.4f} over {num_total} examples (tokenizer={tok_name})")
     return acc
 
 
@@ -167,6 +176,8 @@ def main(argv=None):
     p.add_argument("--num-examples", type=int, default=2000)
     p.add_argument("--out-file", type=str, default="log/hellaswag_eval.txt")
     p.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32")
+    p.add_argument("--allow-byte-tokenizer", action="store_true",
+                   help="score with the byte fallback tokenizer when no GPT-2 BPE is available (result tagged)")
     a = p.parse_args(argv)
     return evaluate(a.model_type, a.hf_model_name, a.device, a.checkpoint, a.data_dir, a.num_examples, a.out_file,
-                    a.dtype)
+                    a.dtype, allow_byte_tokenizer=a.allow_byte_tokenizer)

@@ -62,6 +62,10 @@ class GradReducer:
             self._attach(p)
         self._hooks = [p.register_post_accumulate_grad_hook(self._hook) for p in params]
         self._armed = False
+        # exposed all-reduce time per sync step: stream time from the end of the last backward
+        # (finish() entry, in stream order) to the averaged gradients being ready (finish() exit)
+        self.timing = False
+        self._exposed: List[tuple] = []
         self._left: List[int] = []
         self._next = 0
         self._works = []
@@ -114,6 +118,7 @@ class GradReducer:
         """After the sync backward: launch any bucket not launched yet, wait for all, average."""
         if not self._armed:
             return
+        t0 = self._stamp()
         while self._next < len(self.buckets):  # parameters that got no gradient this step
             s, e, _ = self.buckets[self._next]
             self._works.append(self._all_reduce(self.flat[s:e]))
@@ -125,8 +130,36 @@ class GradReducer:
                     w[1].copy_(w[2])
         if self.world > 1 and self.comm_dtype is None:
             self.flat.mul_(1.0 / self.world)
+        if t0 is not None:
+            self._exposed.append((t0, self._stamp()))
         self._armed = False
         self._works = []
+
+    def _stamp(self):
+        if not self.timing:
+            return None
+        if self.flat.is_cuda:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            return e
+        import time
+        return time.perf_counter()
+
+    def exposed_ms(self, clear: bool = True) -> List[float]:
+        """Exposed all-reduce time (ms) of every timed sync step since the last call (syncs)."""
+        out = []
+        for a, b in self._exposed:
+            if isinstance(a, float):
+                out.append(1000.0 * (b - a))
+            else:
+                b.synchronize()
+                out.append(a.elapsed_time(b))
+        if clear:
+            self._exposed = []
+        return out
+
+    def bucket_bytes(self) -> List[int]:
+        return [4 * (e - s) for s, e, _ in self.buckets]
 
     def remove(self) -> None:
         for h in self._hooks:

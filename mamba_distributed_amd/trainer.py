@@ -37,10 +37,10 @@ from .lm import LMHeadModel
 from .parallel import ddp as ddp_mod
 from .parallel.api import clip_grad_norm_ as par_clip_grad_norm_
 from .parallel.api import full_state_dict, parallelize, sync_tp_grads
-from .parallel.dist import all_gather_object, all_reduce_avg, destroy, init_distributed
+from .parallel.dist import all_gather_object, all_reduce_avg, barrier, destroy, init_distributed
 from .parallel.groups import init_parallel_groups
 from .parallel.microbatch import resolve_overlap, run_micro_batches
-from .utils.checkpoint import latest_checkpoint, load_checkpoint, save_checkpoint, set_rng_state
+from .utils.checkpoint import latest_checkpoint, load_checkpoint, rng_state, save_checkpoint, set_rng_state
 from .utils.lr import get_lr
 
 
@@ -75,6 +75,7 @@ class TrainArgs:
     resume: bool = False
     fused_ce: bool = True
     save_optimizer: bool = True
+    allow_optimizer_reset: bool = False  # resume even when the checkpoint holds no (matching) optimizer state
     metrics_jsonl: Optional[str] = None
     sample_prompt: str = "Hello, I'm a language model,"
     device_type: str = "auto"
@@ -189,8 +190,16 @@ class Trainer:
         path = ck["_path"]
         if "optimizer" in ck and self.a.tp == 1:
             self.optimizer.load_state_dict(ck["optimizer"])
-        elif "optimizer" in ck and self.master:
-            print("note: tensor-parallel resume restarts the AdamW moments (checkpoints hold the full layout)")
+        elif ck.get("optimizer_sharded"):
+            shard = f"{path}.optim_rank{self.info.rank}.pt"
+            if os.path.exists(shard) and int(ck.get("tp", 0)) == self.a.tp:
+                self.optimizer.load_state_dict(load_checkpoint(shard, map_location=self.device)["optimizer"])
+            elif not self.a.allow_optimizer_reset:
+                raise RuntimeError(f"{shard} missing or saved at another TP degree: resuming would restart the "
+                                   "AdamW moments (pass --allow-optimizer-reset to accept that)")
+        elif self.a.save_optimizer and not self.a.allow_optimizer_reset:
+            raise RuntimeError(f"{path} holds no optimizer state: resuming would restart the AdamW moments "
+                               "(pass --allow-optimizer-reset to accept that)")
         if "loader" in ck and hasattr(self.train_loader, "load_state_dict"):
             loaders = ck["loader"]
             if isinstance(loaders, list) and len(loaders) != self.info.world_size and self.master:
@@ -199,8 +208,11 @@ class Trainer:
             st = loaders[r] if isinstance(loaders, list) and r < len(loaders) else None
             if st is not None:
                 self.train_loader.load_state_dict(st)
-        if "rng" in ck:
-            set_rng_state(ck["rng"])
+        if "rng" in ck:  # per-rank list (older checkpoints: one dict, rank 0's)
+            rngs = ck["rng"]
+            r = self.info.rank
+            set_rng_state(rngs[r] if isinstance(rngs, list) and r < len(rngs) else
+                          (rngs[0] if isinstance(rngs, list) else rngs))
         # the checkpoint was taken at the start of ck["step"], before that step's update
         self.start_step = int(ck["step"])
         self.resumed_at = self.start_step
@@ -268,17 +280,29 @@ class Trainer:
         return loss_accum, norm, lr
 
     def save(self, step, val_loss):
-        """Collective (every rank calls it): gathers all ranks' loader positions, rank 0 writes."""
+        """Collective (every rank calls it): gathers all ranks' loader positions and RNG states,
+        rank 0 writes the model checkpoint.  Under tensor parallelism every rank also writes its own
+        optimizer shard next to it (``<ckpt>.optim_rank{r}.pt``): the AdamW moments live in the
+        sharded layout, so resume restores them rank by rank."""
         st = self.train_loader.state_dict() if hasattr(self.train_loader, "state_dict") else None
         loader_states = all_gather_object(st)
+        rngs = all_gather_object(rng_state())
         full_sd = full_state_dict(self.raw_model) if self.a.tp > 1 else None   # collective over TP
+        path = os.path.join(self.a.log_dir, f"model_{step:05d}.pt")
+        if self.a.tp > 1 and self.a.save_optimizer:
+            os.makedirs(self.a.log_dir, exist_ok=True)
+            shard = f"{path}.optim_rank{self.info.rank}.pt"
+            torch.save({"optimizer": self.optimizer.state_dict(), "rank": self.info.rank,
+                        "world_size": self.info.world_size, "tp": self.a.tp}, shard + ".tmp")
+            os.replace(shard + ".tmp", shard)
+        barrier()  # every shard is on disk before the model file that points at them
         if not self.master:
             return None
-        path = os.path.join(self.a.log_dir, f"model_{step:05d}.pt")
         opt = self.optimizer if (self.a.save_optimizer and self.a.tp == 1) else None
         save_checkpoint(path, self.raw_model, step, val_loss, optimizer=opt,
-                        loader_state=loader_states if st is not None else None, include_rng=True,
-                        model_state=full_sd)
+                        loader_state=loader_states if st is not None else None,
+                        model_state=full_sd, extra={"rng": rngs, "tp": self.a.tp,
+                                                    "optimizer_sharded": self.a.tp > 1 and self.a.save_optimizer})
         return path
 
     def _maybe_inject_fault(self, step):

@@ -22,17 +22,35 @@ from ..config import MambaConfig
 
 
 def rng_state():
-    st = {"torch": torch.get_rng_state(), "numpy": np.random.get_state()[1].tolist(),
-          "python": list(random.getstate()[1])}
+    """Every RNG this process draws from, as plain tensors / lists (weights_only-loadable)."""
+    name, keys, pos, has_gauss, cached = np.random.get_state()
+    ver, pstate, gauss_next = random.getstate()
+    st = {"torch": torch.get_rng_state(),
+          "numpy": {"name": name, "keys": keys.tolist(), "pos": int(pos), "has_gauss": int(has_gauss),
+                    "cached": float(cached)},
+          "python": {"version": int(ver), "state": list(pstate), "gauss_next": gauss_next}}
     if torch.cuda.is_available():
         st["cuda"] = torch.cuda.get_rng_state()
     return st
 
 
 def set_rng_state(st):
+    """Inverse of ``rng_state`` (torch, CUDA, numpy and python).  Older checkpoints stored only the
+    numpy / python key arrays: those are restored with default positions."""
     torch.set_rng_state(st["torch"])
     if "cuda" in st and torch.cuda.is_available():
         torch.cuda.set_rng_state(st["cuda"])
+    npst = st.get("numpy")
+    if isinstance(npst, dict):
+        np.random.set_state((npst["name"], np.asarray(npst["keys"], dtype=np.uint32), npst["pos"],
+                             npst["has_gauss"], npst["cached"]))
+    elif npst is not None:
+        np.random.set_state(("MT19937", np.asarray(npst, dtype=np.uint32), 624, 0, 0.0))
+    pyst = st.get("python")
+    if isinstance(pyst, dict):
+        random.setstate((pyst["version"], tuple(pyst["state"]), pyst["gauss_next"]))
+    elif pyst is not None:
+        random.setstate((3, tuple(pyst), None))
 
 
 def save_checkpoint(path: str, model, step: int, val_loss: Optional[float] = None, optimizer=None,
@@ -57,9 +75,29 @@ def save_checkpoint(path: str, model, step: int, val_loss: Optional[float] = Non
     return path
 
 
+class _RefMambaConfig:
+    """Stand-in for ``mamba_ssm.models.config_mamba.MambaConfig``, the dataclass the reference pickles
+    into its checkpoints (train.py:152-163).  Registered as a weights_only safe global under that
+    module path: the unpickler builds this inert object (attribute dict only, no code from the file
+    runs) and ``config_from_checkpoint`` turns it into our MambaConfig."""
+
+    def __setstate__(self, state):
+        self.__dict__.update(state if isinstance(state, dict) else {})
+
+    def to_dict(self):
+        return dict(self.__dict__)
+
+
+_RefMambaConfig.__module__ = "mamba_ssm.models.config_mamba"
+_RefMambaConfig.__qualname__ = "MambaConfig"
+_RefMambaConfig.__name__ = "MambaConfig"
+
+
 def load_checkpoint(path: str, map_location="cpu"):
-    """Safe load (weights_only=True: nothing in the file is executed)."""
-    return torch.load(path, map_location=map_location, weights_only=True)
+    """Safe load (weights_only=True: nothing in the file is executed).  Reference-format checkpoints
+    (a pickled mamba_ssm MambaConfig under "config") load through the inert ``_RefMambaConfig``."""
+    with torch.serialization.safe_globals([_RefMambaConfig]):
+        return torch.load(path, map_location=map_location, weights_only=True)
 
 
 def config_from_checkpoint(ckpt) -> MambaConfig:
@@ -68,6 +106,8 @@ def config_from_checkpoint(ckpt) -> MambaConfig:
         return cfg
     if isinstance(cfg, dict):
         return MambaConfig.from_dict(cfg)
+    if isinstance(cfg, _RefMambaConfig):
+        return MambaConfig.from_dict(cfg.to_dict())
     # reference-era checkpoint without a readable config: the hard-coded eval.py:34 config
     return MambaConfig(d_model=768, vocab_size=50304)
 

@@ -111,3 +111,77 @@ def test_plot_loss_parses_reference_format(tmp_path):
     assert d["val"] == ([0, 250], [10.9911, 6.1]) and d["train"][0] == [0, 1]
     out = plot(str(log), str(tmp_path / "v.png"))
     assert (tmp_path / "v.png").exists() and out.endswith("v.png")
+
+
+def test_reference_format_checkpoint_loads_weights_only(tmp_path):
+    """The reference pickles a mamba_ssm MambaConfig dataclass into its checkpoints
+    (train.py:152-163).  That must load under weights_only=True (nothing executed) through the inert
+    stand-in class, and eval's loader must rebuild the model from it."""
+    import dataclasses
+    import sys
+    import types
+    from mamba_distributed_amd.evaluation.hellaswag import load_model_from_checkpoint
+
+    mods = ["mamba_ssm", "mamba_ssm.models", "mamba_ssm.models.config_mamba"]
+    saved = {m: sys.modules.get(m) for m in mods}
+    fake = types.ModuleType("mamba_ssm.models.config_mamba")
+
+    @dataclasses.dataclass
+    class MambaConfig:  # the upstream field set the reference's checkpoints carry
+        d_model: int = 2560
+        d_intermediate: int = 0
+        n_layer: int = 64
+        vocab_size: int = 50277
+        ssm_cfg: dict = dataclasses.field(default_factory=dict)
+        attn_layer_idx: list = dataclasses.field(default_factory=list)
+        attn_cfg: dict = dataclasses.field(default_factory=dict)
+        rms_norm: bool = True
+        residual_in_fp32: bool = True
+        fused_add_norm: bool = True
+        pad_vocab_size_multiple: int = 8
+        tie_embeddings: bool = True
+
+    MambaConfig.__module__ = fake.__name__
+    MambaConfig.__qualname__ = "MambaConfig"
+    fake.MambaConfig = MambaConfig
+    for m in mods:
+        sys.modules[m] = types.ModuleType(m) if m != fake.__name__ else fake
+    try:
+        cfg = MambaConfig(d_model=64, n_layer=2, vocab_size=512, ssm_cfg={"layer": "Mamba2", "headdim": 32})
+        model = LMHeadModel(MambaConfig_ours(cfg))
+        path = str(tmp_path / "model_03000.pt")
+        torch.save({"model": model.state_dict(), "config": cfg, "step": 3000, "val_loss": 3.28}, path)
+    finally:
+        for m, v in saved.items():
+            if v is None:
+                sys.modules.pop(m, None)
+            else:
+                sys.modules[m] = v
+    assert "mamba_ssm.models.config_mamba" not in sys.modules
+    ck = load_checkpoint(path)
+    got = config_from_checkpoint(ck)
+    assert (got.d_model, got.n_layer, got.vocab_size, got.layer_type) == (64, 2, 512, "Mamba2")
+    m2 = load_model_from_checkpoint(path, device="cpu")
+    for (k, a), (_, b) in zip(model.state_dict().items(), m2.state_dict().items()):
+        assert torch.equal(a, b), k
+
+
+def MambaConfig_ours(ref_cfg):
+    import dataclasses
+    return MambaConfig.from_dict(dataclasses.asdict(ref_cfg))
+
+
+def test_rng_state_roundtrip_all_generators():
+    import random
+    from mamba_distributed_amd.utils.checkpoint import rng_state, set_rng_state
+    torch.manual_seed(3)
+    np.random.seed(4)
+    random.seed(5)
+    st = rng_state()
+    a = (torch.rand(3), np.random.rand(3), random.random())
+    torch.manual_seed(99)
+    np.random.seed(98)
+    random.seed(97)
+    set_rng_state(st)
+    b = (torch.rand(3), np.random.rand(3), random.random())
+    assert torch.equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2]

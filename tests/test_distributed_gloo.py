@@ -156,3 +156,32 @@ def test_bench_multi_rank_flow_on_cpu(dp_impl):
     assert d["config"]["parallelism"] == "dp2" and d["config"]["dp_impl"] == dp_impl
     assert d["config"]["grad_accum"] == 2 and d["value"] > 0
     assert math.isfinite(d["config"]["final_loss"]), d
+
+
+def test_bench_gpus2_relaunches_under_torchrun():
+    """``python bench.py --gpus 2`` outside torchrun must start 2 ranks itself (a child
+    torch.distributed.run) and report n_gpus 2 from the real world size, never one rank."""
+    import json
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "1",
+           "--model", "mamba2-tiny", "--B", "2", "--T", "32", "--global-batch-tokens", "256"]
+    env = dict(_env())
+    env.pop("RANK", None)
+    p = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
+    assert out["config"]["comm"]["world_size"] == 2 and out["config"]["comm"]["n_buckets"] >= 1
+    assert out["config"]["grad_accum"] == 2
+
+
+def test_bench_refuses_world_mismatch():
+    """Under torchrun, a --gpus that disagrees with WORLD_SIZE exits non-zero without a JSON line."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "1", "--warmup", "0", "--model", "mamba2-tiny", "--B", "2", "--T", "32",
+           "--global-batch-tokens", "128"]
+    p = subprocess.run(cmd, env=_env(), stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=600)
+    assert p.returncode != 0
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]

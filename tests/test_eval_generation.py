@@ -40,10 +40,13 @@ def test_evaluate_checkpoint_end_to_end(tmp_path):
     data = str(tmp_path / "hs")
     _write_jsonl(data, n=6)
     out = str(tmp_path / "log" / "hellaswag_eval.txt")
+    with pytest.raises(RuntimeError, match="byte"):  # no GPT-2 BPE here: refuse unless asked
+        hs.evaluate("custom", "unused", "cpu", checkpoint_path=ck, data_dir=data, num_examples=2000,
+                    out_file=out, verbose=False, enc=ByteTokenizer())
     acc = hs.evaluate("custom", "unused", "cpu", checkpoint_path=ck, data_dir=data, num_examples=2000,
-                      out_file=out, verbose=False)
+                      out_file=out, verbose=False, allow_byte_tokenizer=True, enc=ByteTokenizer())
     line = open(out).read()
-    assert line.startswith("6 ") and line.endswith(f"{acc:.4f}") and "\n" not in line
+    assert line.startswith("6 ") and line.endswith(f"{acc:.4f} tokenizer=bytes") and "\n" not in line
 
 
 def _cached_vs_full(cfg):
