@@ -648,6 +648,58 @@ Tensor gemm_wgrad_cm(Tensor dY, Tensor X, optional<Tensor> out, bool accumulate,
   return C;
 }
 
+// Pipelined MFMA GEMM (kernels/gemm_pipe.hip): C = A . B^T with each operand as stored:
+//   la = 0: A is (M, K) K-contiguous; la = 1: A is (K, M) M-contiguous.  lb likewise for B ((N, K) / (K, N)).
+// mode 0: bf16 C (M, N) (out may be a row-strided view); 1: fp32 C; 2: fp32 C += (out required).
+// splits > 1 (fp32 modes): out is (splits, M, N) -- one fp32 slab per K split (reduce with gp_reduce).
+Tensor gp_mm(Tensor A, Tensor B, optional<Tensor> out, int64_t la, int64_t lb, int64_t mode, int64_t splits,
+             int64_t bm) {
+  check_cuda(A, "A");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(A.device());
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2, "gp_mm: 2-D operands");
+  TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "gp_mm: bf16 operands");
+  TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1, "gp_mm: unit inner strides");
+  TORCH_CHECK((la == 0 || la == 1) && (lb == 0 || lb == 1) && mode >= 0 && mode <= 2 && splits >= 1, "gp_mm: args");
+  TORCH_CHECK(!(la == 1 && lb == 0), "gp_mm: (la, lb) = (1, 0) is not instantiated");
+  const int64_t M = la == 0 ? A.size(0) : A.size(1), K = la == 0 ? A.size(1) : A.size(0);
+  const int64_t N = lb == 0 ? B.size(0) : B.size(1), KB = lb == 0 ? B.size(1) : B.size(0);
+  TORCH_CHECK(K == KB, "gp_mm: contraction sizes differ (", K, " vs ", KB, ")");
+  TORCH_CHECK(mode != 0 || splits == 1, "gp_mm: bf16 output needs splits == 1");
+  TORCH_CHECK(M < (1ll << 31) && N < (1ll << 31) && K < (1ll << 31), "gp_mm: sizes");
+  TORCH_CHECK((uintptr_t)A.data_ptr() % 16 == 0 && (uintptr_t)B.data_ptr() % 16 == 0, "gp_mm: 16-B aligned operands");
+  Tensor C;
+  const auto dt = mode == 0 ? at::kBFloat16 : at::kFloat;
+  if (out.has_value() && out->defined()) {
+    C = *out;
+  } else {
+    TORCH_CHECK(mode != 2, "gp_mm: mode 2 accumulates into out");
+    C = splits > 1 ? at::empty({splits, M, N}, A.options().dtype(dt)) : at::empty({M, N}, A.options().dtype(dt));
+  }
+  TORCH_CHECK(C.scalar_type() == dt && C.stride(-1) == 1 && C.size(-1) == N && C.size(-2) == M, "gp_mm: out shape/dtype");
+  TORCH_CHECK(splits == 1 || (C.dim() == 3 && C.size(0) == splits && C.is_contiguous()), "gp_mm: split out (S, M, N)");
+  TORCH_CHECK((uintptr_t)C.data_ptr() % 16 == 0, "gp_mm: 16-B aligned out");
+  const int64_t ldc = C.stride(-2);
+  TORCH_CHECK(mamba_amd::gemm_pipe_supported((int)la, (int)lb, (int)M, (int)N, (int)K, A.stride(0), B.stride(0), ldc),
+              "gp_mm: unsupported shape/strides (K, row strides % 8; XC operand rows % 8; N % 4)");
+  HIPCHK(mamba_amd::launch_gemm_pipe((int)la, (int)lb, A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0),
+                                     C.data_ptr(), ldc, (int)M, (int)N, (int)K, (int)splits, M * ldc, (int)mode,
+                                     (int)bm, cur_stream()));
+  return C;
+}
+
+int64_t gp_splits(int64_t M, int64_t N, int64_t K) { return mamba_amd::gemm_pipe_splits((int)M, (int)N, (int)K); }
+void gp_set_ablate(int64_t bits) { mamba_amd::gemm_pipe_set_ablate((int)bits); }
+
+// out (+)= sum over the leading dim of part (S, ...) in fixed order; out fp32 contiguous, numel(out) = numel(part[0])
+void gp_reduce(Tensor part, Tensor out, bool accumulate) {
+  check_cuda(part, "part");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(part.device());
+  TORCH_CHECK(part.scalar_type() == at::kFloat && out.scalar_type() == at::kFloat && part.is_contiguous() &&
+              out.is_contiguous() && part.dim() >= 2 && part.numel() == part.size(0) * out.numel(), "gp_reduce: shapes");
+  HIPCHK(mamba_amd::launch_gp_reduce(part.data_ptr<float>(), (int)part.size(0), out.numel(), out.numel(),
+                                     out.data_ptr<float>(), accumulate, cur_stream()));
+}
+
 // ---------------------------------------------------------------------------------------------
 // fused Mamba-2 decode step (kernels/decode.hip).  Every operand is preallocated by the caller
 // (inference.FusedMamba2Decoder) so the three launches per layer can be captured in one HIP graph.
@@ -756,6 +808,10 @@ TORCH_LIBRARY(mamba_amd, m) {
   m.def("gemm_wgrad(Tensor dY, Tensor X, Tensor(a!)? out=None, bool accumulate=False) -> Tensor");
   m.def("gemm_wgrad_cm(Tensor dY, Tensor X, Tensor(a!)? out=None, bool accumulate=False, bool dy_cm=True, "
         "bool x_cm=False) -> Tensor");
+  m.def("gp_mm(Tensor A, Tensor B, Tensor(a!)? out=None, int la=0, int lb=0, int mode=0, int splits=1, int bm=256) -> Tensor");
+  m.def("gp_splits(int M, int N, int K) -> int", &gp_splits);
+  m.def("gp_set_ablate(int bits) -> ()", &gp_set_ablate);
+  m.def("gp_reduce(Tensor part, Tensor(a!) out, bool accumulate=False) -> ()");
   m.def("gemm_skinny(Tensor A, Tensor B, Tensor(a!)? out=None, bool accumulate=False) -> Tensor");
   m.def("ssm_state_update(Tensor(a!) state, Tensor x, Tensor dt, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? z, "
         "Tensor? dt_bias, bool softplus) -> Tensor");
@@ -772,6 +828,8 @@ TORCH_LIBRARY_IMPL(mamba_amd, CUDA, m) {
   m.impl("gemm_wgrad", &gemm_wgrad);
   m.impl("gemm_skinny", &gemm_skinny);
   m.impl("gemm_wgrad_cm", &gemm_wgrad_cm);
+  m.impl("gp_mm", &gp_mm);
+  m.impl("gp_reduce", &gp_reduce);
   m.impl("add_rmsnorm_bwd", &add_rmsnorm_bwd);
   m.impl("gated_rmsnorm_fwd", &gated_rmsnorm_fwd);
   m.impl("gated_rmsnorm_bwd", &gated_rmsnorm_bwd);

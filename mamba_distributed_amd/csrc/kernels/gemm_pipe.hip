@@ -1,0 +1,409 @@
+// Pipelined bf16 MFMA GEMM engine for the Mamba projections (in_proj / out_proj forward,
+// input gradient and weight gradient; reached from model.py:35-41 through the mixers' in_proj/out_proj).
+//
+//   C[M, N] (op)= A[M, K] . B[N, K]^T      fp32 accumulate, bf16 or fp32 output
+//
+// Each operand comes in one of two layouts, so every product of a projection runs without a transpose:
+//   KC : the operand's rows hold K contiguously        (activations x[tokens, K], nn.Linear W[out, in])
+//   XC : the operand is stored [K][rows], rows contiguous (dY^T / X^T for the weight gradient, W for dgrad)
+// forward  y  = x W^T      A = x  (KC), B = W  (KC)
+// dgrad    dx = dy W       A = dy (KC), B = W  (XC: B[n=i][k=o] = W[o][i])
+// wgrad    dW = dy^T x     A = dy (XC), B = x  (XC), K = tokens, split over K into fp32 slabs
+//
+// MI355X design (cdna_hip_programming.md §5 "Pipelining across barriers", "glds vs register staging"):
+//  * 256 x 256 (or 128 x 256) output tile per 512-thread workgroup, 8 waves as 2 (M) x 4 (N); every wave
+//    owns a (BM/2) x 64 sub-tile = MI x 4 accumulators of v_mfma_f32_16x16x32_bf16 (128 acc VGPRs at 256^2).
+//  * K advances in 32-deep stages through a 4-slot LDS ring filled by global_load_lds_dwordx4 (LDS-DMA:
+//    no VGPR staging, no ds_write).  Stage s+4 is issued right after the barrier that retires stage s, so
+//    three stages (~3k MFMA cycles) are in flight; each stage boundary waits with a COUNTED vmcnt (never 0
+//    in steady state) and a raw s_barrier (no __syncthreads: its fence would drain the in-flight DMA).
+//  * inside a stage the MFMAs of the first M-half run while the second half's fragments are read, and the
+//    next stage's fragments are read (into a second B register set) behind the second half's MFMAs, so the
+//    matrix pipe never waits on an LDS round trip.
+//  * LDS images are lane-linear (what the DMA writes) with the bank-conflict swizzle applied to the
+//    per-lane SOURCE address and undone on the read (rule 21):
+//      KC [rows][32 k] (64-B rows): 16-B chunk c of row r at slot c ^ kc_swz(r) — the four 16-lane groups of
+//         ds_read_b128 then hit 16 distinct slots (checked by hand, see kc_swz).
+//      XC [32 k][128] halves (256-B rows): chunk s of k-row r at s ^ 2 xc_swz(r), read with
+//         ds_read_b64_tr_b16 (hardware transpose), conflict-free for the rows one 32-lane half reads.
+//  * MFMA operands are swapped (D = B_tile . A_tile^T) so each lane's 4 accumulator registers are 4
+//    CONSECUTIVE output columns of one row: the epilogue stores 8 B (bf16) / 16 B (fp32) per lane and
+//    needs no LDS round trip; fp32 output may accumulate in place (+=).
+//  * XCD-aware bijective block remap; tiles of one M panel (and one K split) are consecutive, so they
+//    share the A panel / the K slab in one XCD's L2.
+//  * K tails: chunks with k >= K are DMA'd from a 16-B zero page (per-lane source), rows / columns past
+//    M / N are clamped on load and never stored.
+#include "mfma.h"
+#include "launchers.h"
+
+namespace mamba_amd {
+namespace {
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+constexpr int GP_NT = 512;   // threads per workgroup
+constexpr int GP_BK = 64;    // k per K-tile (one LDS buffer)
+
+__device__ __attribute__((aligned(64))) unsigned int g_gp_zero[16];  // zero page for k >= K chunks
+
+// KC image [rows][64 k] (128-B rows): 16-B chunk c of row r at slot c ^ (r & 7).  A ds_read_b128 lane group
+// (rows 0-3 and 12-15 at chunk 4ks+g, rows 4-11 at chunk 4ks+g+1) then covers all 16 slots of a bank row.
+// XC image: [64 k][128] halves (256-B rows); chunk s of k-row r at s ^ 2 xc_swz(r)
+__device__ __forceinline__ int xc_swz(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
+
+// ---- fragment reads (16 operand rows x 32 k of k-step ks, STD k order) --------------------------------------
+// Lane-dependent byte offsets are computed once (lane_kc / lane_xc); the row / column block and the buffer
+// are compile-time or wave-uniform, so every read is `lane VGPR + immediate` (hipcc cannot prove on its own
+// that the swizzle term depends on the lane only, and otherwise keeps one address VGPR per read).
+// KC: row r = r0 + (l & 15) with r0 % 16 == 0  ->  r & 7 == l & 7
+__device__ __forceinline__ int lane_kc(int ks) {
+  const int l = threadIdx.x & 63;
+  return (l & 15) * 128 + (((4 * ks + (l >> 4)) ^ (l & 7)) << 4);
+}
+__device__ __forceinline__ bf16x8 ld_kc(const char* img, int lane_off, int r0) {
+  return *reinterpret_cast<const bf16x8*>(img + lane_off + r0 * 128);
+}
+// XC: column block c0 (multiple of 16) of a [64 k][128]-halved image; k-rows 32 ks + 8 g + (li >> 2) (+4).
+// The XOR mask depends on the lane only (xc_swz of those rows), the 8-B unit on c0: one offset per c0 % 128.
+__device__ __forceinline__ int lane_xc(int c0) {
+  const int l = threadIdx.x & 63, g = l >> 4, li = l & 15;
+  const int r = 8 * g + (li >> 2);
+  const int u = ((c0 & 127) >> 2) + (li & 3);
+  return r * 256 + ((u ^ (xc_swz(r) << 2)) << 3);
+}
+__device__ __forceinline__ bf16x8 ld_xc(const char* img, int lane_off, int c0, int ks) {
+  const char* p = img + (c0 >> 7) * (64 * 256) + ks * (32 * 256) + lane_off;
+  return cat8(tr4(reinterpret_cast<const bf16_t*>(p)), tr4(reinterpret_cast<const bf16_t*>(p + 4 * 256)));
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// pin the preceding block as [NMFMA MFMAs] with NREADS DS reads issued first, two per MFMA, then a
+// scheduling fence (hipcc otherwise hoists MFMAs across the barrier and merges neighbouring K-tiles)
+template <int NREADS, int NMFMA, int NVMEM = 0>
+__device__ __forceinline__ void pin() {
+#pragma unroll
+  for (int k = 0; k < NREADS / 2; ++k) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
+  }
+#pragma unroll
+  for (int k = 0; k < NVMEM; ++k) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read (LDS-DMA)
+  }
+  __builtin_amdgcn_sched_group_barrier(0x008, NMFMA - NREADS / 2 - NVMEM, 0);
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+}  // namespace
+
+struct GemmPipeArgs {
+  const bf16_t* A; int64_t lda;
+  const bf16_t* B; int64_t ldb;
+  void* C; int64_t ldc; int64_t split_stride;  // elements between the fp32 slabs of consecutive K splits
+  int M, N, K, kslice, splits;
+  int ablate;  // diagnostics: bit 0 no vmcnt wait, 1 no DMA, 2 no barrier, 3 no epilogue (results garbage)
+};
+
+// LA / LB: operand layouts (0 = KC, 1 = XC); MI: 16-row tiles per wave along M (BM = 32 MI); EPI: 0 = bf16
+// store, 1 = fp32 store, 2 = fp32 +=
+//
+// Schedule (2 LDS buffers of one 64-deep K-tile each, t = K-tile, X = buffer t % 2, Y = the other):
+//   k-step 0: read ahi | [B-half DMA of t+1 -> Y] MFMA alo x b0 | read alo, b1 (k-step 1) | MFMA ahi x b0
+//   k-step 1: read ahi | MFMA alo x b1 | lgkmcnt(0), vmcnt(0) [t+1 landed in Y], s_barrier [X read by every
+//             wave] | A-half DMA of t+2 -> X, read alo, b0 of t+1 from Y | MFMA ahi x b1
+// so every DMA has ~one K-tile of MFMAs to land, fetches whole 128-B lines, and no block carries more than
+// four LDS-DMAs or an MFMA waiting on a fragment read issued fewer than 16 MFMAs earlier.
+// (A persistent variant that streams the next output tile's K-tiles behind this one's was measured slower:
+// the dynamic buffer parity and tile bookkeeping cost more in the K-loop than the hidden epilogue gained.)
+template <int LA, int LB, int MI, int EPI, int ABL = 0>
+__global__ __launch_bounds__(512) void gemm_pipe_k(GemmPipeArgs a) {
+  constexpr int NJ = 4;                       // 16-col tiles per wave (BN = 256)
+  constexpr int BM = 32 * MI, BN = 64 * NJ;
+  constexpr int SA = BM * 128, SB = BN * 128;  // bytes per K-tile image
+  constexpr int SS = SA + SB;
+  constexpr int GA = BM / 64, GB = BN / 64;    // DMA instructions per thread per K-tile and operand
+  constexpr int G = GA + GB;
+  constexpr int MH = MI / 2;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * SS];
+
+  const int tn = (a.N + BN - 1) / BN, tm = (a.M + BM - 1) / BM;
+  const int nwg = tm * tn * a.splits;
+  const int t = xcd_remap(blockIdx.x, nwg);
+  const int split = t / (tm * tn), tile = t % (tm * tn);
+  const int m0 = (tile / tn) * BM, n0 = (tile % tn) * BN;
+  const int kbeg = split * a.kslice, kend = min(a.K, kbeg + a.kslice);
+  const int KT = (kend - kbeg + GP_BK - 1) / GP_BK;
+  const int KTF = (kend - kbeg) / GP_BK;  // full K-tiles (the rest, if any, takes the zero-page check)
+  const int mvalid = min(BM, a.M - m0), nvalid = min(BN, a.N - n0);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int wr = w >> 2, wc = w & 3;
+  const int am0 = wr * (BM / 2), bn0 = wc * (BN / 4);
+  constexpr int abl = ABL;  // diagnostics only (0 in every real launch)
+
+  // per-thread DMA sources as 32-bit BYTE offsets from the operand base at k = kbeg (host-checked to fit):
+  // global_load_lds then takes the saddr + voffset form with no per-DMA 64-bit pointer registers
+  unsigned off[G];
+  {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      const bool isA = i < GA;
+      const int ii = isA ? i : i - GA;
+      const int L = isA ? LA : LB;
+      const int base = isA ? m0 : n0, valid = isA ? mvalid : nvalid;
+      const int64_t ld = isA ? a.lda : a.ldb;
+      int64_t e;
+      if (L == 0) {
+        const int q = ii * GP_NT + tid, r = q >> 3, c = (q & 7) ^ (r & 7);
+        e = (int64_t)(base + min(r, valid - 1)) * ld + 8 * c;
+      } else {
+        const int h = ii >> 1, q = (ii & 1) * GP_NT + tid, r = q >> 4, sx = q & 15;
+        const int c = min(h * 128 + 8 * (sx ^ (2 * xc_swz(r))), valid - 8);
+        e = (int64_t)r * ld + base + c;
+      }
+      off[i] = (unsigned)(e * 2);
+    }
+  }
+  const int64_t stepA = LA == 0 ? GP_BK : GP_BK * a.lda;  // elements per K-tile
+  const int64_t stepB = LB == 0 ? GP_BK : GP_BK * a.ldb;
+  const char* baseA = reinterpret_cast<const char*>(a.A + (LA == 0 ? kbeg : (int64_t)kbeg * a.lda));
+  const char* baseB = reinterpret_cast<const char*>(a.B + (LB == 0 ? kbeg : (int64_t)kbeg * a.ldb));
+  const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // DMA of K-tile kt into buf; part 0: A's DMAs, 1: B's, 2: both
+  auto dma = [&](int kt_, char* buf, bool checked, int part) {
+    if constexpr ((abl & 2) != 0) return;
+    const int kt = __builtin_amdgcn_readfirstlane(kt_);  // opaque to LLVM's strength reduction
+    const int k0 = kbeg + kt * GP_BK;
+    const char* bA = baseA + kt * stepA * 2;
+    const char* bB = baseB + kt * stepB * 2;
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      const bool isA = i < GA;
+      if ((part == 0 && !isA) || (part == 1 && isA)) continue;
+      const int ii = isA ? i : i - GA;
+      const void* p = (isA ? bA : bB) + off[i];
+      if (checked) {  // k of this lane's chunk
+        const int L = isA ? LA : LB;
+        const int tid = threadIdx.x;
+        int kk;
+        if (L == 0) {
+          const int q = ii * GP_NT + tid, r = q >> 3;
+          kk = k0 + 8 * ((q & 7) ^ (r & 7));
+        } else {
+          kk = k0 + (((ii & 1) * GP_NT + tid) >> 4);
+        }
+        if (kk >= kend) p = (const void*)g_gp_zero;
+      }
+      __builtin_amdgcn_global_load_lds(p, (lds_void*)(buf + (isA ? 0 : SA) + (ii * GP_NT + wu * 64) * 16), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = zero4();
+
+  bf16x8 alo[MH], ahi[MH], b0[NJ], b1[NJ];
+  // lane offsets: KC -> one per k-step; XC -> one per 16-column block (k-step and half are immediates)
+  constexpr int NOA = LA == 0 ? 2 : MI, NOB = LB == 0 ? 2 : NJ;
+  int oa[NOA], ob[NOB];
+#pragma unroll
+  for (int i = 0; i < NOA; ++i) oa[i] = LA == 0 ? lane_kc(i) : lane_xc(am0 + 16 * i);
+#pragma unroll
+  for (int j = 0; j < NOB; ++j) ob[j] = LB == 0 ? lane_kc(j) : lane_xc(bn0 + 16 * j);
+  auto fa = [&](const char* img, int i, int ks) -> bf16x8 {
+    const int r0 = am0 + 16 * i;
+    if constexpr (LA == 0) return ld_kc(img, oa[ks], r0);
+    else return ld_xc(img, oa[i], r0, ks);
+  };
+  auto fb = [&](const char* img, int j, int ks) -> bf16x8 {
+    const int c0 = bn0 + 16 * j;
+    if constexpr (LB == 0) return ld_kc(img + SA, ob[ks], c0);
+    else return ld_xc(img + SA, ob[j], c0, ks);
+  };
+  auto rd_lo = [&](const char* img, int ks, bf16x8 (&bf)[NJ]) {
+#pragma unroll
+    for (int i = 0; i < MH; ++i) alo[i] = fa(img, i, ks);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) bf[j] = fb(img, j, ks);
+  };
+  auto rd_hi = [&](const char* img, int ks) {
+#pragma unroll
+    for (int i = 0; i < MH; ++i) ahi[i] = fa(img, MH + i, ks);
+  };
+  auto mm_lo = [&](bf16x8 (&bf)[NJ]) {
+#pragma unroll
+    for (int i = 0; i < MH; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = mfma16(bf[j], alo[i], acc[i][j]);
+  };
+  auto mm_hi = [&](bf16x8 (&bf)[NJ]) {
+#pragma unroll
+    for (int i = 0; i < MH; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[MH + i][j] = mfma16(bf[j], ahi[i], acc[MH + i][j]);
+  };
+
+  // one K-tile from buffer `cur` (tile kt); `nxt` holds tile kt+1 and receives tile kt+2.  `bpend`: the B
+  // half of tile kt+1 is still to be issued (its A half went out at the previous K-tile's barrier)
+  auto ktile = [&](int kt, char* cur, char* nxt, bool steady, bool bpend) {
+    // k-step 0
+    rd_hi(cur, 0);
+    if (bpend) dma(kt + 1, nxt, !steady && kt + 1 >= KTF, 1);
+    mm_lo(b0);
+    pin<MH, MH * NJ, GB>();
+    rd_lo(cur, 1, b1);
+    mm_hi(b0);
+    pin<MH + NJ, MH * NJ>();
+    // k-step 1
+    rd_hi(cur, 1);
+    mm_lo(b1);
+    pin<MH, MH * NJ>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave is done reading `cur`
+    if (steady || kt + 1 < KT) {
+      if constexpr (!(abl & 1)) vm_wait<0>();                       // tile kt+1 has landed in `nxt`
+      if constexpr (!(abl & 4)) __builtin_amdgcn_s_barrier();       // ... for every wave; every wave is done reading `cur`
+      __builtin_amdgcn_sched_barrier(0);
+      if (steady) dma(kt + 2, cur, false, 0);
+      else if (kt + 2 < KT) dma(kt + 2, cur, kt + 2 >= KTF, 0);
+      rd_lo(nxt, 0, b0);
+    }
+    mm_hi(b1);
+    pin<MH + NJ, MH * NJ, GA>();
+  };
+
+  if (KT > 0) {
+    dma(0, smem, KTF < 1, 2);
+    if (KT > 1) dma(1, smem + SS, KTF < 2, 2);
+    if (KT > 1) vm_wait<G>();
+    else vm_wait<0>();
+    __builtin_amdgcn_s_barrier();
+    rd_lo(smem, 0, b0);
+  }
+  int kt = 0;
+  for (; kt + 4 <= KTF; kt += 2) {  // kt+2 and kt+3 exist and are full
+    ktile(kt, smem, smem + SS, true, kt > 0);
+    ktile(kt + 1, smem + SS, smem, true, true);
+  }
+  for (; kt < KT; kt += 2) {
+    ktile(kt, smem, smem + SS, false, kt > 0 && kt + 1 < KT);
+    if (kt + 1 < KT) ktile(kt + 1, smem + SS, smem, false, kt + 2 < KT);
+  }
+
+  // epilogue: lane holds C[m][n .. n+3], m = m0 + am0 + 16 i + (l & 15), n = n0 + bn0 + 16 j + 4 (l >> 4)
+  if constexpr ((abl & 8) != 0) return;
+  const int mr = l & 15, nc = 4 * (l >> 4);
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int mm = am0 + 16 * i + mr;
+    if (mm >= mvalid) continue;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int nn = bn0 + 16 * j + nc;
+      if (nn >= nvalid) continue;
+      const int64_t off = (int64_t)(m0 + mm) * a.ldc + n0 + nn;
+      if constexpr (EPI == 0) {
+        bf16_t* c = reinterpret_cast<bf16_t*>(a.C) + off;
+        *reinterpret_cast<uint2*>(c) = make_uint2(pack2(acc[i][j][0], acc[i][j][1]), pack2(acc[i][j][2], acc[i][j][3]));
+      } else {
+        float* c = reinterpret_cast<float*>(a.C) + (int64_t)split * a.split_stride + off;
+        float4 v = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+        if constexpr (EPI == 2) {
+          const float4 o = *reinterpret_cast<const float4*>(c);
+          v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+        }
+        *reinterpret_cast<float4*>(c) = v;
+      }
+    }
+  }
+}
+
+// out[i] (+)= sum_s part[s][i] in fixed order (the K-split slabs of a weight gradient)
+__global__ void gp_reduce_k(const float* __restrict__ part, int S, int64_t stride, int64_t n, float* __restrict__ out,
+                            bool accumulate) {
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i >= n) return;
+  float4 s = accumulate ? *reinterpret_cast<const float4*>(out + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int k = 0; k < S; ++k) {
+    const float4 v = *reinterpret_cast<const float4*>(part + (int64_t)k * stride + i);
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  *reinterpret_cast<float4*>(out + i) = s;
+}
+
+static int g_gp_ablate = 0;
+void gemm_pipe_set_ablate(int bits) { g_gp_ablate = bits; }
+
+bool gemm_pipe_supported(int la, int lb, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc) {
+  if (M <= 0 || N <= 0 || K <= 0) return false;
+  if (K % 8 || lda % 8 || ldb % 8 || ldc % 4 || N % 4) return false;
+  if (la == 1 && M % 8) return false;  // XC operand columns are DMA'd in 8-element chunks
+  if (lb == 1 && N % 8) return false;
+  if (la == 0 && lda < K) return false;
+  if (lb == 0 && ldb < K) return false;
+  return true;
+}
+
+int gemm_pipe_splits(int M, int N, int K) {
+  // one workgroup per CU (128 KB of LDS): aim at ~one full round of 256 workgroups, >= 16 stages per split
+  const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  int S = std::max(1, 256 / tiles);
+  while (S > 1 && K / S < 8 * GP_BK) --S;
+  return S;
+}
+
+hipError_t launch_gemm_pipe(int la, int lb, const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
+                            int64_t ldc, int M, int N, int K, int splits, int64_t split_stride, int epi, int bm,
+                            hipStream_t st) {
+  if (!gemm_pipe_supported(la, lb, M, N, K, lda, ldb, ldc)) return hipErrorInvalidValue;
+  if (splits < 1 || (splits > 1 && epi == 0)) return hipErrorInvalidValue;
+  GemmPipeArgs a;
+  a.A = (const bf16_t*)A; a.lda = lda; a.B = (const bf16_t*)B; a.ldb = ldb;
+  a.C = C; a.ldc = ldc; a.split_stride = split_stride;
+  a.M = M; a.N = N; a.K = K; a.splits = splits;
+  a.ablate = g_gp_ablate;
+  a.kslice = ((K + splits - 1) / splits + GP_BK - 1) / GP_BK * GP_BK;
+  const int BM = bm == 128 ? 128 : 256;
+  const int ntiles = ((M + BM - 1) / BM) * ((N + 255) / 256) * splits;
+  const int nwg = ntiles;
+#define GP_LAUNCH(LA_, LB_, MI_, EPI_) \
+  hipLaunchKernelGGL((gemm_pipe_k<LA_, LB_, MI_, EPI_>), dim3(nwg), dim3(GP_NT), 0, st, a)
+#define GP_EPI(LA_, LB_, MI_)                 \
+  switch (epi) {                              \
+    case 0: GP_LAUNCH(LA_, LB_, MI_, 0); break; \
+    case 1: GP_LAUNCH(LA_, LB_, MI_, 1); break; \
+    default: GP_LAUNCH(LA_, LB_, MI_, 2); break; \
+  }
+  if (a.ablate && la == 0 && lb == 0 && BM == 256 && epi == 0) {
+#define GP_ABL(B_) case B_: hipLaunchKernelGGL((gemm_pipe_k<0, 0, 8, 0, B_>), dim3(nwg), dim3(GP_NT), 0, st, a); break;
+    switch (a.ablate) { GP_ABL(1) GP_ABL(2) GP_ABL(4) GP_ABL(8) GP_ABL(5) GP_ABL(6) GP_ABL(14) default: break; }
+#undef GP_ABL
+  } else if (la == 0 && lb == 0) {
+    if (BM == 256) { GP_EPI(0, 0, 8) } else { GP_EPI(0, 0, 4) }
+  } else if (la == 0 && lb == 1) {
+    if (BM == 256) { GP_EPI(0, 1, 8) } else { GP_EPI(0, 1, 4) }
+  } else if (la == 1 && lb == 1) {
+    GP_EPI(1, 1, 8)
+  } else {
+    return hipErrorInvalidValue;
+  }
+#undef GP_EPI
+#undef GP_LAUNCH
+  return hipGetLastError();
+}
+
+hipError_t launch_gp_reduce(const float* part, int S, int64_t stride, int64_t n, float* out, bool accumulate,
+                            hipStream_t st) {
+  if (n % 4 || stride % 4) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(gp_reduce_k, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, st, part, S, stride, n, out,
+                     accumulate);
+  return hipGetLastError();
+}
+
+}  // namespace mamba_amd

@@ -70,6 +70,19 @@ hipError_t launch_gemm_wgrad_cm(const void* dY, int64_t ldy, const void* X, int6
 hipError_t launch_gemm_wgrad(const void* dY, int64_t ldy, const void* X, int64_t ldx, float* part, float* out,
                              int M, int P, int Q, bool accumulate, hipStream_t st);
 
+// ---- gemm_pipe.hip: pipelined 256x256 MFMA GEMM engine, C[M,N] (op)= A . B^T ----------------------------
+// la / lb: 0 = operand stored [rows][K] (K contiguous), 1 = stored [K][rows]; epi: 0 = bf16 C, 1 = fp32 C
+// (K split `splits` ways into slabs split_stride elements apart), 2 = fp32 C +=; bm: 256 or 128 tile rows
+bool gemm_pipe_supported(int la, int lb, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc);
+int gemm_pipe_splits(int M, int N, int K);
+void gemm_pipe_set_ablate(int bits);  // diagnostics only (scripts/gemm_bench.py --ablate)
+hipError_t launch_gemm_pipe(int la, int lb, const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
+                            int64_t ldc, int M, int N, int K, int splits, int64_t split_stride, int epi, int bm,
+                            hipStream_t st);
+// out[i] (+)= sum_s part[s * stride + i], fixed order
+hipError_t launch_gp_reduce(const float* part, int S, int64_t stride, int64_t n, float* out, bool accumulate,
+                            hipStream_t st);
+
 // ---- decode.hip (fused single-token Mamba-2 layer step; buffers preallocated, graph-capturable) --------
 int decode_max_batch();
 hipError_t launch_decode_inproj(const void* hn, const void* W, int n_out, int d, int b, float* zxbcdt, int conv_lo,
