@@ -74,9 +74,34 @@ std::tuple<Tensor, Tensor, Tensor> add_rmsnorm_fwd(Tensor x, optional<Tensor> re
   return {y, ro, rstd};
 }
 
+// Deferred parameter-gradient reductions: part_mode 0 = transient partials + column sum (plain call);
+// 1 / 2 = store / ADD this call's partial rows into the caller-kept buffer `part_buf` and skip the sum
+// (no-sync micro-steps); 3 / 4 = store / add, then sum (the sync micro-step).  Without the sum the returned
+// parameter gradients are empty (0-element) tensors.
+struct PartMode {
+  bool pacc, reduce;
+};
+static PartMode part_mode(int64_t m) {
+  TORCH_CHECK(m >= 0 && m <= 4, "part_mode must be 0..4");
+  return {m == 2 || m == 4, m == 0 || m == 3 || m == 4};
+}
+static Tensor part_tensor(const optional<Tensor>& buf, int64_t mode, at::IntArrayRef shape, const at::TensorOptions& o) {
+  if (mode == 0) return at::empty(shape, o.dtype(at::kFloat));
+  TORCH_CHECK(buf.has_value() && buf->defined(), "part_mode > 0 needs part_buf");
+  TORCH_CHECK(buf->scalar_type() == at::kFloat && buf->is_contiguous() && buf->sizes() == shape,
+              "part_buf must be contiguous fp32 of shape ", shape, " (got ", buf->sizes(), ")");
+  return *buf;
+}
+int64_t part_rows(std::string kind, int64_t a, int64_t b) {
+  if (kind == "add_rmsnorm") return mamba_amd::add_rmsnorm_bwd_partial_rows(a);
+  if (kind == "gated_rmsnorm") return mamba_amd::norm_bwd_partial_rows(a);
+  if (kind == "conv_cl") return mamba_amd::conv_cl_bwd_partial_rows((int)a, (int)b);
+  TORCH_CHECK(false, "part_rows: unknown kind ", kind);
+}
+
 std::tuple<Tensor, Tensor, Tensor> add_rmsnorm_bwd(Tensor dy, optional<Tensor> dres_out, Tensor res_out, Tensor weight,
                                                    Tensor rstd, at::ScalarType dx_dtype, at::ScalarType dres_dtype,
-                                                   bool write_dres) {
+                                                   bool write_dres, optional<Tensor> part_buf, int64_t part_mode_) {
   check_cuda(dy, "dy");
   at::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
   dy = dy.contiguous();
@@ -92,14 +117,15 @@ std::tuple<Tensor, Tensor, Tensor> add_rmsnorm_bwd(Tensor dy, optional<Tensor> d
   auto dx = at::empty({M, D}, dy.options().dtype(dx_dtype));
   Tensor dres = write_dres ? at::empty({M, D}, dy.options().dtype(dres_dtype)) : at::empty({0}, dy.options());
   const int rows = mamba_amd::add_rmsnorm_bwd_partial_rows(M);
-  auto part = at::empty({rows, D}, dy.options().dtype(at::kFloat));
-  auto dw = at::empty({D}, dy.options().dtype(at::kFloat));
+  const PartMode pm = part_mode(part_mode_);
+  Tensor part = part_tensor(part_buf, part_mode_, {rows, D}, dy.options());
+  auto dw = at::empty({pm.reduce ? D : 0}, dy.options().dtype(at::kFloat));
   HIPCHK(mamba_amd::launch_add_rmsnorm_bwd(dy.data_ptr(), dcode(dy.scalar_type()), dro.defined() ? dro.data_ptr() : nullptr,
                                            dro.defined() ? dcode(dro.scalar_type()) : 0, res_out.data_ptr(),
                                            dcode(res_out.scalar_type()), w.data_ptr<float>(), rstd.data_ptr<float>(),
                                            dx.data_ptr(), dcode(dx_dtype), write_dres ? dres.data_ptr() : nullptr,
-                                           dcode(dres_dtype), part.data_ptr<float>(), dw.data_ptr<float>(), M, (int)D,
-                                           cur_stream()));
+                                           dcode(dres_dtype), part.data_ptr<float>(),
+                                           pm.reduce ? dw.data_ptr<float>() : nullptr, pm.pacc, M, (int)D, cur_stream()));
   return {dx, dres, dw.to(weight.scalar_type())};
 }
 
@@ -125,7 +151,8 @@ std::tuple<Tensor, Tensor> gated_rmsnorm_fwd(Tensor x, Tensor z, Tensor weight, 
 
 std::tuple<Tensor, Tensor, Tensor> gated_rmsnorm_bwd(Tensor dy, Tensor x, Tensor z, Tensor weight, Tensor rstd,
                                                      int64_t group_size, bool norm_before_gate, optional<Tensor> dx_out,
-                                                     optional<Tensor> dz_out) {
+                                                     optional<Tensor> dz_out, optional<Tensor> part_buf,
+                                                     int64_t part_mode_) {
   check_cuda(dy, "dy");
   at::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
   dy = dy.contiguous();
@@ -139,13 +166,15 @@ std::tuple<Tensor, Tensor, Tensor> gated_rmsnorm_bwd(Tensor dy, Tensor x, Tensor
                   dz.scalar_type() == z.scalar_type(), "dz_out layout");
   Tensor w = f32c(weight);
   const int rows = mamba_amd::norm_bwd_partial_rows(M);
-  auto part = at::empty({rows, D}, dy.options().dtype(at::kFloat));
-  auto dw = at::empty({D}, dy.options().dtype(at::kFloat));
+  const PartMode pm = part_mode(part_mode_);
+  Tensor part = part_tensor(part_buf, part_mode_, {rows, D}, dy.options());
+  auto dw = at::empty({pm.reduce ? D : 0}, dy.options().dtype(at::kFloat));
   HIPCHK(mamba_amd::launch_gated_rmsnorm_bwd(dy.data_ptr(), dcode(dy.scalar_type()), x.data_ptr(), dcode(x.scalar_type()),
                                              x.stride(0), z.data_ptr(), dcode(z.scalar_type()), z.stride(0),
                                              w.data_ptr<float>(), rstd.data_ptr<float>(), dx.data_ptr(), dx.stride(0),
-                                             dz.data_ptr(), dz.stride(0), part.data_ptr<float>(), dw.data_ptr<float>(), M,
-                                             (int)D, (int)group_size, norm_before_gate, cur_stream()));
+                                             dz.data_ptr(), dz.stride(0), part.data_ptr<float>(),
+                                             pm.reduce ? dw.data_ptr<float>() : nullptr, pm.pacc, M, (int)D,
+                                             (int)group_size, norm_before_gate, cur_stream()));
   return {dx, dz, dw.to(weight.scalar_type())};
 }
 
@@ -192,7 +221,8 @@ Tensor conv1d_cf_fwd(Tensor x, Tensor weight, optional<Tensor> bias, bool silu) 
 }
 
 std::tuple<Tensor, Tensor, Tensor> conv1d_cf_bwd(Tensor x, Tensor weight, optional<Tensor> bias, Tensor dout, bool silu,
-                                                 optional<Tensor> dx_out) {
+                                                 optional<Tensor> dx_out, optional<Tensor> part_buf,
+                                                 int64_t part_mode_) {
   check_cuda(x, "x");
   at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1, "x must be (b, d, l) with unit time stride");
@@ -206,12 +236,14 @@ std::tuple<Tensor, Tensor, Tensor> conv1d_cf_bwd(Tensor x, Tensor weight, option
   TORCH_CHECK(dx.size(0) == B && dx.size(1) == D && dx.size(2) == L && dx.stride(2) == 1 &&
               dx.scalar_type() == x.scalar_type(), "dx_out layout");
   const int W = (int)w.size(1);
-  auto part = at::empty({B, D, W + 1}, x.options().dtype(at::kFloat));
-  auto dwb = at::empty({D, W + 1}, x.options().dtype(at::kFloat));  // [taps | bias] per channel
+  const PartMode pm = part_mode(part_mode_);
+  Tensor part = part_tensor(part_buf, part_mode_, {B, D, W + 1}, x.options());
+  auto dwb = at::empty({pm.reduce ? D : 0, W + 1}, x.options().dtype(at::kFloat));  // [taps | bias] per channel
   HIPCHK(mamba_amd::launch_conv_cf_bwd(x.data_ptr(), dcode(x.scalar_type()), x.stride(0), x.stride(1), w.data_ptr<float>(),
                                        fptr(bb), dout.data_ptr(), dout.stride(0), dout.stride(1), dx.data_ptr(),
-                                       dx.stride(0), dx.stride(1), part.data_ptr<float>(), dwb.data_ptr<float>(),
-                                       nullptr, (int)B, (int)D, (int)L, W, silu, cur_stream()));
+                                       dx.stride(0), dx.stride(1), part.data_ptr<float>(),
+                                       pm.reduce ? dwb.data_ptr<float>() : nullptr, nullptr, pm.pacc, (int)B, (int)D,
+                                       (int)L, W, silu, cur_stream()));
   return {dx, dwb.narrow(1, 0, W), dwb.select(1, W)};
 }
 
@@ -231,7 +263,8 @@ Tensor conv1d_cl_fwd(Tensor x, Tensor weight, optional<Tensor> bias, bool silu) 
 }
 
 std::tuple<Tensor, Tensor, Tensor> conv1d_cl_bwd(Tensor x, Tensor weight, optional<Tensor> bias, Tensor dout, bool silu,
-                                                 optional<Tensor> dx_out) {
+                                                 optional<Tensor> dx_out, optional<Tensor> part_buf,
+                                                 int64_t part_mode_) {
   check_cuda(x, "x");
   at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1, "x must be (b, l, c) with unit channel stride");
@@ -245,12 +278,15 @@ std::tuple<Tensor, Tensor, Tensor> conv1d_cl_bwd(Tensor x, Tensor weight, option
   TORCH_CHECK(dx.size(0) == B && dx.size(1) == L && dx.size(2) == C && dx.stride(2) == 1 &&
               dx.scalar_type() == x.scalar_type(), "dx_out layout");
   const int W = (int)w.size(1);
-  auto part = at::empty({mamba_amd::conv_cl_bwd_partial_rows((int)B, (int)L), C, W + 1}, x.options().dtype(at::kFloat));
-  auto dwb = at::empty({C, W + 1}, x.options().dtype(at::kFloat));  // [taps | bias] per channel
+  const PartMode pm = part_mode(part_mode_);
+  Tensor part = part_tensor(part_buf, part_mode_, {mamba_amd::conv_cl_bwd_partial_rows((int)B, (int)L), C, W + 1},
+                            x.options());
+  auto dwb = at::empty({pm.reduce ? C : 0, W + 1}, x.options().dtype(at::kFloat));  // [taps | bias] per channel
   HIPCHK(mamba_amd::launch_conv_cl_bwd(x.data_ptr(), dcode(x.scalar_type()), x.stride(0), x.stride(1), w.data_ptr<float>(),
                                        fptr(bb), dout.data_ptr(), dout.stride(0), dout.stride(1), dx.data_ptr(),
-                                       dx.stride(0), dx.stride(1), part.data_ptr<float>(), dwb.data_ptr<float>(),
-                                       nullptr, (int)B, (int)L, (int)C, W, silu, cur_stream()));
+                                       dx.stride(0), dx.stride(1), part.data_ptr<float>(),
+                                       pm.reduce ? dwb.data_ptr<float>() : nullptr, nullptr, pm.pacc, (int)B, (int)L,
+                                       (int)C, W, silu, cur_stream()));
   return {dx, dwb.narrow(1, 0, W), dwb.select(1, W)};
 }
 
@@ -345,7 +381,7 @@ std::vector<Tensor> ssd_bwd(Tensor dy, Tensor x, Tensor dt, Tensor A, Tensor Bm,
                             optional<Tensor> dt_bias, optional<Tensor> init, Tensor cum, Tensor dtp, Tensor states,
                             optional<Tensor> dfinal, int64_t chunk, bool softplus, double dt_min, double dt_max,
                             optional<Tensor> dx_out, optional<Tensor> ddt_out, optional<Tensor> dB_out,
-                            optional<Tensor> dC_out, bool A_is_log) {
+                            optional<Tensor> dC_out, bool A_is_log, optional<Tensor> part_buf, int64_t part_mode_) {
   check_cuda(x, "x");
   at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   mamba_amd::SSDArgs a{};
@@ -386,12 +422,15 @@ std::vector<Tensor> ssd_bwd(Tensor dy, Tensor x, Tensor dt, Tensor A, Tensor Bm,
   auto part_dcb = at::empty({a.B, a.nc, a.nhg, 64, 64}, fo);
   auto part_db = at::empty({a.B, a.nc, a.nhg, 64, a.N}, fo);
   auto part_dc = at::empty({a.B, a.nc, a.nhg, 64, a.N}, fo);
-  auto part_small = at::empty({a.B * a.nc, 3, a.H}, fo);
+  const PartMode pm = part_mode(part_mode_);
+  Tensor part_small = part_tensor(part_buf, part_mode_, {a.B * a.nc, 3, a.H}, x.options());
+  a.pacc = pm.pacc;
   a.part_dcb = part_dcb.data_ptr<float>(); a.part_db = part_db.data_ptr<float>(); a.part_dc = part_dc.data_ptr<float>();
   a.psl = 3 * a.H;
   a.part_dA = part_small.data_ptr<float>(); a.part_dD = a.part_dA + a.H; a.part_dbias = a.part_dA + 2 * a.H;
   a.a_log = A_is_log;
   HIPCHK(mamba_amd::launch_ssd_bwd(a, cur_stream()));
+  if (!pm.reduce) return {dx, ddt, at::empty({0}, fo), dB, dC, at::empty({0}, fo), at::empty({0}, fo), dinit};
   auto sums = at::empty({3, a.H}, fo);  // deterministic column sums over the (b, chunk) rows
   HIPCHK(mamba_amd::launch_colsum(part_small.data_ptr<float>(), a.B * a.nc, 3 * a.H, sums.data_ptr<float>(), cur_stream()));
   Tensor dA = sums[0].to(A.scalar_type());
@@ -673,15 +712,20 @@ Tensor gp_mm(Tensor A, Tensor B, optional<Tensor> out, int64_t la, int64_t lb, i
     C = *out;
   } else {
     TORCH_CHECK(mode != 2, "gp_mm: mode 2 accumulates into out");
-    C = splits > 1 ? at::empty({splits, M, N}, A.options().dtype(dt)) : at::empty({M, N}, A.options().dtype(dt));
+    // fp32 output is always (splits, M, N) (a 1-slab result reduces with gp_reduce like any other)
+    C = mode != 0 ? at::empty({splits, M, N}, A.options().dtype(dt)) : at::empty({M, N}, A.options().dtype(dt));
   }
   TORCH_CHECK(C.scalar_type() == dt && C.stride(-1) == 1 && C.size(-1) == N && C.size(-2) == M, "gp_mm: out shape/dtype");
   TORCH_CHECK(splits == 1 || (C.dim() == 3 && C.size(0) == splits && C.is_contiguous()), "gp_mm: split out (S, M, N)");
+  TORCH_CHECK(C.dim() == 2 || (C.dim() == 3 && C.size(0) == splits && C.is_contiguous()), "gp_mm: out rank");
   TORCH_CHECK((uintptr_t)C.data_ptr() % 16 == 0, "gp_mm: 16-B aligned out");
   const int64_t ldc = C.stride(-2);
-  TORCH_CHECK(mamba_amd::gemm_pipe_supported((int)la, (int)lb, (int)M, (int)N, (int)K, A.stride(0), B.stride(0), ldc),
-              "gp_mm: unsupported shape/strides (K, row strides % 8; XC operand rows % 8; N % 4)");
-  HIPCHK(mamba_amd::launch_gemm_pipe((int)la, (int)lb, A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0),
+  // a size-1 leading dim has an arbitrary stride in torch (e.g. (1, n) views): use the dense one
+  const int64_t lda = A.size(0) == 1 ? A.size(1) : A.stride(0), ldb = B.size(0) == 1 ? B.size(1) : B.stride(0);
+  TORCH_CHECK(mamba_amd::gemm_pipe_supported((int)la, (int)lb, (int)M, (int)N, (int)K, lda, ldb, ldc),
+              "gp_mm: unsupported shape/strides (M=", M, " N=", N, " K=", K, " lda=", lda, " ldb=", ldb, " ldc=", ldc,
+              "; needs row strides % 8, KC operands K % 8, XC operand rows % 8, N % 4)");
+  HIPCHK(mamba_amd::launch_gemm_pipe((int)la, (int)lb, A.data_ptr(), lda, B.data_ptr(), ldb,
                                      C.data_ptr(), ldc, (int)M, (int)N, (int)K, (int)splits, M * ldc, (int)mode,
                                      (int)bm, cur_stream()));
   return C;
@@ -778,25 +822,27 @@ TORCH_LIBRARY(mamba_amd, m) {
   m.def("add_rmsnorm_fwd(Tensor x, Tensor? residual, Tensor weight, float eps, ScalarType out_dtype, "
         "ScalarType res_dtype) -> (Tensor, Tensor, Tensor)");
   m.def("add_rmsnorm_bwd(Tensor dy, Tensor? dres_out, Tensor res_out, Tensor weight, Tensor rstd, "
-        "ScalarType dx_dtype, ScalarType dres_dtype, bool write_dres) -> (Tensor, Tensor, Tensor)");
+        "ScalarType dx_dtype, ScalarType dres_dtype, bool write_dres, Tensor(z!)? part_buf=None, int part_mode=0) "
+        "-> (Tensor, Tensor, Tensor)");
   m.def("gated_rmsnorm_fwd(Tensor x, Tensor z, Tensor weight, float eps, int group_size, bool norm_before_gate) "
         "-> (Tensor, Tensor)");
   m.def("gated_rmsnorm_bwd(Tensor dy, Tensor x, Tensor z, Tensor weight, Tensor rstd, int group_size, "
-        "bool norm_before_gate, Tensor(a!)? dx_out, Tensor(b!)? dz_out) -> (Tensor, Tensor, Tensor)");
+        "bool norm_before_gate, Tensor(a!)? dx_out, Tensor(b!)? dz_out, Tensor(z!)? part_buf=None, int part_mode=0) "
+        "-> (Tensor, Tensor, Tensor)");
   m.def("ce_fwd(Tensor logits, Tensor targets, int ignore_index, Tensor scale, Tensor(a!)? grad) -> Tensor");
   m.def("conv1d_cf_fwd(Tensor x, Tensor weight, Tensor? bias, bool silu) -> Tensor");
-  m.def("conv1d_cf_bwd(Tensor x, Tensor weight, Tensor? bias, Tensor dout, bool silu, Tensor(a!)? dx_out) "
-        "-> (Tensor, Tensor, Tensor)");
+  m.def("conv1d_cf_bwd(Tensor x, Tensor weight, Tensor? bias, Tensor dout, bool silu, Tensor(a!)? dx_out, "
+        "Tensor(z!)? part_buf=None, int part_mode=0) -> (Tensor, Tensor, Tensor)");
   m.def("conv1d_cl_fwd(Tensor x, Tensor weight, Tensor? bias, bool silu) -> Tensor");
-  m.def("conv1d_cl_bwd(Tensor x, Tensor weight, Tensor? bias, Tensor dout, bool silu, Tensor(a!)? dx_out) "
-        "-> (Tensor, Tensor, Tensor)");
+  m.def("conv1d_cl_bwd(Tensor x, Tensor weight, Tensor? bias, Tensor dout, bool silu, Tensor(a!)? dx_out, "
+        "Tensor(z!)? part_buf=None, int part_mode=0) -> (Tensor, Tensor, Tensor)");
   m.def("conv1d_update(Tensor x, Tensor(a!) conv_state, Tensor weight, Tensor? bias, bool silu) -> Tensor");
   m.def("ssd_fwd(Tensor x, Tensor dt, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? dt_bias, Tensor? init, "
         "int chunk, bool softplus, float dt_min, float dt_max, bool A_is_log=False) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("ssd_bwd(Tensor dy, Tensor x, Tensor dt, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? dt_bias, "
         "Tensor? init, Tensor cum, Tensor dtp, Tensor states, Tensor? dfinal, int chunk, bool softplus, float dt_min, "
         "float dt_max, Tensor(a!)? dx_out, Tensor(b!)? ddt_out, Tensor(c!)? dB_out, Tensor(d!)? dC_out, "
-        "bool A_is_log=False) -> Tensor[]");
+        "bool A_is_log=False, Tensor(z!)? part_buf=None, int part_mode=0) -> Tensor[]");
   m.def("selscan_fwd(Tensor u, Tensor delta, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? z, Tensor? delta_bias, "
         "bool softplus) -> (Tensor, Tensor, Tensor)");
   m.def("selscan_bwd(Tensor dout, Tensor u, Tensor delta, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? z, "
@@ -810,6 +856,7 @@ TORCH_LIBRARY(mamba_amd, m) {
         "bool x_cm=False) -> Tensor");
   m.def("gp_mm(Tensor A, Tensor B, Tensor(a!)? out=None, int la=0, int lb=0, int mode=0, int splits=1, int bm=256) -> Tensor");
   m.def("gp_splits(int M, int N, int K) -> int", &gp_splits);
+  m.def("part_rows(str kind, int a, int b=0) -> int", &part_rows);
   m.def("gp_set_ablate(int bits) -> ()", &gp_set_ablate);
   m.def("gp_reduce(Tensor part, Tensor(a!) out, bool accumulate=False) -> ()");
   m.def("gemm_skinny(Tensor A, Tensor B, Tensor(a!)? out=None, bool accumulate=False) -> Tensor");

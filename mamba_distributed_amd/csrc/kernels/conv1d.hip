@@ -117,7 +117,7 @@ __global__ __launch_bounds__(256) void conv_cf_bwd_k(const T* __restrict__ x, in
                                                      const float* __restrict__ w, const float* __restrict__ bias,
                                                      const T* __restrict__ dout, int64_t sgb, int64_t sgd,
                                                      T* __restrict__ dx, int64_t sdb, int64_t sdd,
-                                                     float* __restrict__ part, int Bn, int Dn, int L, bool silu) {
+                                                     float* __restrict__ part, bool pacc, int Bn, int Dn, int L, bool silu) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= (int64_t)Bn * Dn) return;
@@ -187,8 +187,8 @@ __global__ __launch_bounds__(256) void conv_cf_bwd_k(const T* __restrict__ x, in
   if (lane == 0) {
     float* pr = part + row * (W + 1);
 #pragma unroll
-    for (int k = 0; k < W; ++k) pr[k] = accw[k];
-    pr[W] = accb;
+    for (int k = 0; k < W; ++k) pr[k] = pacc ? pr[k] + accw[k] : accw[k];
+    pr[W] = pacc ? pr[W] + accb : accb;
   }
 }
 
@@ -262,7 +262,7 @@ __global__ __launch_bounds__(256) void conv_cl_bwd_k(const T* __restrict__ x, in
                                                      const float* __restrict__ w, const float* __restrict__ bias,
                                                      const T* __restrict__ dout, int64_t sgb, int64_t sgl,
                                                      T* __restrict__ dx, int64_t sdb, int64_t sdl,
-                                                     float* __restrict__ part, int Bn, int L, int C, bool silu) {
+                                                     float* __restrict__ part, bool pacc, int Bn, int L, int C, bool silu) {
   __shared__ float red[4][64 * 8 * (W + 1)];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = (blockIdx.x * 64 + lane) * 8;
@@ -361,8 +361,11 @@ __global__ __launch_bounds__(256) void conv_cl_bwd_k(const T* __restrict__ x, in
   const int64_t prow = (int64_t)blockIdx.z * gridDim.y + blockIdx.y;
   for (int i = threadIdx.x; i < 64 * 8 * (W + 1); i += 256) {
     const int ch = blockIdx.x * 512 + i / (W + 1);
-    if (ch < C) part[prow * (int64_t)C * (W + 1) + (int64_t)ch * (W + 1) + i % (W + 1)] =
-        red[0][i] + red[1][i] + red[2][i] + red[3][i];
+    if (ch < C) {
+      float* pp = part + prow * (int64_t)C * (W + 1) + (int64_t)ch * (W + 1) + i % (W + 1);
+      const float v = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+      *pp = pacc ? *pp + v : v;  // pacc: accumulate across micro-steps (reduced once per optimizer step)
+    }
   }
 }
 
@@ -445,7 +448,7 @@ __global__ __launch_bounds__(256) void conv_cl_bwd_bf16_k(const bf16_t* __restri
                                                           const float* __restrict__ w, const float* __restrict__ bias,
                                                           const bf16_t* __restrict__ dout, int64_t sgb, int64_t sgl,
                                                           bf16_t* __restrict__ dx, int64_t sdb, int64_t sdl,
-                                                          float* __restrict__ part, int L, int C, bool silu) {
+                                                          float* __restrict__ part, bool pacc, int L, int C, bool silu) {
   __shared__ float red[4][64 * 8 * (W + 1)];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = (blockIdx.x * 64 + lane) * 8;
@@ -542,8 +545,11 @@ __global__ __launch_bounds__(256) void conv_cl_bwd_bf16_k(const bf16_t* __restri
   const int64_t prow = (int64_t)blockIdx.z * gridDim.y + blockIdx.y;
   for (int i = threadIdx.x; i < 64 * 8 * (W + 1); i += 256) {
     const int ch = blockIdx.x * 512 + i / (W + 1);
-    if (ch < C) part[prow * (int64_t)C * (W + 1) + (int64_t)ch * (W + 1) + i % (W + 1)] =
-        red[0][i] + red[1][i] + red[2][i] + red[3][i];
+    if (ch < C) {
+      float* pp = part + prow * (int64_t)C * (W + 1) + (int64_t)ch * (W + 1) + i % (W + 1);
+      const float v = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+      *pp = pacc ? *pp + v : v;  // pacc: accumulate across micro-steps (reduced once per optimizer step)
+    }
   }
 }
 
@@ -605,31 +611,31 @@ hipError_t launch_conv_cf_fwd(const void* x, int dt, int64_t sxb, int64_t sxd, c
 template <typename T>
 static hipError_t cf_bwd(const T* x, int64_t sxb, int64_t sxd, const float* w, const float* bias, const T* g,
                          int64_t sgb, int64_t sgd, T* dx, int64_t sdb, int64_t sdd, float* part, float* dw, float* db,
-                         int Bn, int Dn, int L, int Wd, bool silu, hipStream_t st) {
+                         bool pacc, int Bn, int Dn, int L, int Wd, bool silu, hipStream_t st) {
   const bool vec = (L % 8 == 0) && (sxb % 8 == 0) && (sxd % 8 == 0) && (sgb % 8 == 0) && (sgd % 8 == 0) &&
                    (sdb % 8 == 0) && (sdd % 8 == 0) && ((uintptr_t)x % 16 == 0) && ((uintptr_t)g % 16 == 0) &&
                    ((uintptr_t)dx % 16 == 0);
   dim3 grid((unsigned)(((int64_t)Bn * Dn + 3) / 4)), block(256);
   W_SWITCH(Wd, {
     if (vec) hipLaunchKernelGGL((conv_cf_bwd_k<T, WW, true>), grid, block, 0, st, x, sxb, sxd, w, bias, g, sgb, sgd,
-                                dx, sdb, sdd, part, Bn, Dn, L, silu);
+                                dx, sdb, sdd, part, pacc, Bn, Dn, L, silu);
     else hipLaunchKernelGGL((conv_cf_bwd_k<T, WW, false>), grid, block, 0, st, x, sxb, sxd, w, bias, g, sgb, sgd, dx,
-                            sdb, sdd, part, Bn, Dn, L, silu);
+                            sdb, sdd, part, pacc, Bn, Dn, L, silu);
   });
   MAMBA_HIP_CHECK(hipGetLastError());
-  return launch_colsum(part, Bn, Dn * (Wd + 1), dw, st);  // dw buffer holds (D, W+1): [w taps | bias]
+  return dw ? launch_colsum(part, Bn, Dn * (Wd + 1), dw, st) : hipSuccess;  // dw buffer holds (D, W+1): [w taps | bias]
 }
 
 hipError_t launch_conv_cf_bwd(const void* x, int dt, int64_t sxb, int64_t sxd, const float* w, const float* bias,
                               const void* g, int64_t sgb, int64_t sgd, void* dx, int64_t sdb, int64_t sdd,
-                              float* part, float* dw, float* db, int Bn, int Dn, int L, int Wd, bool silu,
+                              float* part, float* dw, float* db, bool pacc, int Bn, int Dn, int L, int Wd, bool silu,
                               hipStream_t st) {
   if (dt == kBF16)
     return cf_bwd<bf16_t>((const bf16_t*)x, sxb, sxd, w, bias, (const bf16_t*)g, sgb, sgd, (bf16_t*)dx, sdb, sdd,
-                          part, dw, db, Bn, Dn, L, Wd, silu, st);
+                          part, dw, db, pacc, Bn, Dn, L, Wd, silu, st);
   if (dt == kF32)
     return cf_bwd<float>((const float*)x, sxb, sxd, w, bias, (const float*)g, sgb, sgd, (float*)dx, sdb, sdd, part,
-                         dw, db, Bn, Dn, L, Wd, silu, st);
+                         dw, db, pacc, Bn, Dn, L, Wd, silu, st);
   return hipErrorInvalidValue;
 }
 
@@ -672,7 +678,7 @@ int conv_cl_bwd_partial_rows(int Bn, int L) { return Bn * ((L + 4 * CLB_T - 1) /
 template <typename T>
 static hipError_t cl_bwd(const T* x, int64_t sxb, int64_t sxl, const float* w, const float* bias, const T* g,
                          int64_t sgb, int64_t sgl, T* dx, int64_t sdb, int64_t sdl, float* part, float* dw, float* db,
-                         int Bn, int L, int C, int Wd, bool silu, hipStream_t st) {
+                         bool pacc, int Bn, int L, int C, int Wd, bool silu, hipStream_t st) {
   const bool vec = (C % 8 == 0) && (sxb % 8 == 0) && (sxl % 8 == 0) && (sgb % 8 == 0) && (sgl % 8 == 0) &&
                    (sdb % 8 == 0) && (sdl % 8 == 0) && ((uintptr_t)x % 16 == 0) && ((uintptr_t)g % 16 == 0) &&
                    ((uintptr_t)dx % 16 == 0);
@@ -680,31 +686,31 @@ static hipError_t cl_bwd(const T* x, int64_t sxb, int64_t sxl, const float* w, c
   if constexpr (std::is_same<T, bf16_t>::value) {
     if (vec) {
       W_SWITCH(Wd, hipLaunchKernelGGL((conv_cl_bwd_bf16_k<WW, CLB_T>), grid, block, 0, st, x, sxb, sxl, w, bias, g,
-                                      sgb, sgl, dx, sdb, sdl, part, L, C, silu));
+                                      sgb, sgl, dx, sdb, sdl, part, pacc, L, C, silu));
       MAMBA_HIP_CHECK(hipGetLastError());
-      return launch_colsum(part, conv_cl_bwd_partial_rows(Bn, L), C * (Wd + 1), dw, st);
+      return dw ? launch_colsum(part, conv_cl_bwd_partial_rows(Bn, L), C * (Wd + 1), dw, st) : hipSuccess;
     }
   }
   W_SWITCH(Wd, {
     if (vec) hipLaunchKernelGGL((conv_cl_bwd_k<T, WW, true>), grid, block, 0, st, x, sxb, sxl, w, bias, g, sgb, sgl,
-                                dx, sdb, sdl, part, Bn, L, C, silu);
+                                dx, sdb, sdl, part, pacc, Bn, L, C, silu);
     else hipLaunchKernelGGL((conv_cl_bwd_k<T, WW, false>), grid, block, 0, st, x, sxb, sxl, w, bias, g, sgb, sgl, dx,
-                            sdb, sdl, part, Bn, L, C, silu);
+                            sdb, sdl, part, pacc, Bn, L, C, silu);
   });
   MAMBA_HIP_CHECK(hipGetLastError());
-  return launch_colsum(part, conv_cl_bwd_partial_rows(Bn, L), C * (Wd + 1), dw, st);  // (C, W+1)
+  return dw ? launch_colsum(part, conv_cl_bwd_partial_rows(Bn, L), C * (Wd + 1), dw, st) : hipSuccess;  // (C, W+1)
 }
 
 hipError_t launch_conv_cl_bwd(const void* x, int dt, int64_t sxb, int64_t sxl, const float* w, const float* bias,
                               const void* g, int64_t sgb, int64_t sgl, void* dx, int64_t sdb, int64_t sdl,
-                              float* part, float* dw, float* db, int Bn, int L, int C, int Wd, bool silu,
+                              float* part, float* dw, float* db, bool pacc, int Bn, int L, int C, int Wd, bool silu,
                               hipStream_t st) {
   if (dt == kBF16)
     return cl_bwd<bf16_t>((const bf16_t*)x, sxb, sxl, w, bias, (const bf16_t*)g, sgb, sgl, (bf16_t*)dx, sdb, sdl,
-                          part, dw, db, Bn, L, C, Wd, silu, st);
+                          part, dw, db, pacc, Bn, L, C, Wd, silu, st);
   if (dt == kF32)
     return cl_bwd<float>((const float*)x, sxb, sxl, w, bias, (const float*)g, sgb, sgl, (float*)dx, sdb, sdl, part,
-                         dw, db, Bn, L, C, Wd, silu, st);
+                         dw, db, pacc, Bn, L, C, Wd, silu, st);
   return hipErrorInvalidValue;
 }
 

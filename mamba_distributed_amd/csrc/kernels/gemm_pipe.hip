@@ -120,13 +120,17 @@ struct GemmPipeArgs {
 // four LDS-DMAs or an MFMA waiting on a fragment read issued fewer than 16 MFMAs earlier.
 // (A persistent variant that streams the next output tile's K-tiles behind this one's was measured slower:
 // the dynamic buffer parity and tile bookkeeping cost more in the K-loop than the hidden epilogue gained.)
-template <int LA, int LB, int MI, int EPI, int ABL = 0>
-__global__ __launch_bounds__(512) void gemm_pipe_k(GemmPipeArgs a) {
-  constexpr int NJ = 4;                       // 16-col tiles per wave (BN = 256)
-  constexpr int BM = 32 * MI, BN = 64 * NJ;
+template <int LA, int LB, int MI, int EPI, int ABL = 0, int WN = 4>
+__global__ __launch_bounds__(128 * WN) void gemm_pipe_k(GemmPipeArgs a) {
+  // WN = 4: 8 waves as 2 x 4, each (BM/2) x 64; WN = 2: 4 waves as 2 x 2, each (BM/2) x 128 (one wave per
+  // SIMD, accumulators in AGPRs, 1/3 fewer fragment bytes per MFMA)
+  constexpr int NT = 128 * WN;
+  constexpr int NJ = 16 / WN;                 // 16-col tiles per wave (BN = 256)
+  constexpr int BM = 32 * MI, BN = 16 * NJ * WN;
   constexpr int SA = BM * 128, SB = BN * 128;  // bytes per K-tile image
   constexpr int SS = SA + SB;
-  constexpr int GA = BM / 64, GB = BN / 64;    // DMA instructions per thread per K-tile and operand
+  constexpr int GA = BM * 8 / NT, GB = BN * 8 / NT;  // DMA instructions per thread per K-tile and operand
+  constexpr int IPH = 1024 / NT;                      // XC: DMA instructions per [64][128] half
   constexpr int G = GA + GB;
   constexpr int MH = MI / 2;
   __shared__ __attribute__((aligned(1024))) char smem[2 * SS];
@@ -141,8 +145,8 @@ __global__ __launch_bounds__(512) void gemm_pipe_k(GemmPipeArgs a) {
   const int KTF = (kend - kbeg) / GP_BK;  // full K-tiles (the rest, if any, takes the zero-page check)
   const int mvalid = min(BM, a.M - m0), nvalid = min(BN, a.N - n0);
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const int wr = w >> 2, wc = w & 3;
-  const int am0 = wr * (BM / 2), bn0 = wc * (BN / 4);
+  const int wr = w / WN, wc = w % WN;
+  const int am0 = wr * (BM / 2), bn0 = wc * (BN / WN);
   constexpr int abl = ABL;  // diagnostics only (0 in every real launch)
 
   // per-thread DMA sources as 32-bit BYTE offsets from the operand base at k = kbeg (host-checked to fit):
@@ -159,10 +163,10 @@ __global__ __launch_bounds__(512) void gemm_pipe_k(GemmPipeArgs a) {
       const int64_t ld = isA ? a.lda : a.ldb;
       int64_t e;
       if (L == 0) {
-        const int q = ii * GP_NT + tid, r = q >> 3, c = (q & 7) ^ (r & 7);
+        const int q = ii * NT + tid, r = q >> 3, c = (q & 7) ^ (r & 7);
         e = (int64_t)(base + min(r, valid - 1)) * ld + 8 * c;
       } else {
-        const int h = ii >> 1, q = (ii & 1) * GP_NT + tid, r = q >> 4, sx = q & 15;
+        const int h = ii / IPH, q = (ii % IPH) * NT + tid, r = q >> 4, sx = q & 15;
         const int c = min(h * 128 + 8 * (sx ^ (2 * xc_swz(r))), valid - 8);
         e = (int64_t)r * ld + base + c;
       }
@@ -192,14 +196,14 @@ __global__ __launch_bounds__(512) void gemm_pipe_k(GemmPipeArgs a) {
         const int tid = threadIdx.x;
         int kk;
         if (L == 0) {
-          const int q = ii * GP_NT + tid, r = q >> 3;
+          const int q = ii * NT + tid, r = q >> 3;
           kk = k0 + 8 * ((q & 7) ^ (r & 7));
         } else {
-          kk = k0 + (((ii & 1) * GP_NT + tid) >> 4);
+          kk = k0 + (((ii % IPH) * NT + tid) >> 4);
         }
         if (kk >= kend) p = (const void*)g_gp_zero;
       }
-      __builtin_amdgcn_global_load_lds(p, (lds_void*)(buf + (isA ? 0 : SA) + (ii * GP_NT + wu * 64) * 16), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(p, (lds_void*)(buf + (isA ? 0 : SA) + (ii * NT + wu * 64) * 16), 16, 0, 0);
     }
   };
 
@@ -342,11 +346,15 @@ void gemm_pipe_set_ablate(int bits) { g_gp_ablate = bits; }
 
 bool gemm_pipe_supported(int la, int lb, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc) {
   if (M <= 0 || N <= 0 || K <= 0) return false;
-  if (K % 8 || lda % 8 || ldb % 8 || ldc % 4 || N % 4) return false;
+  if (lda % 8 || ldb % 8 || ldc % 4 || N % 4) return false;
+  if ((la == 0 || lb == 0) && K % 8) return false;  // KC operands are DMA'd in 8-element k chunks
   if (la == 1 && M % 8) return false;  // XC operand columns are DMA'd in 8-element chunks
   if (lb == 1 && N % 8) return false;
   if (la == 0 && lda < K) return false;
   if (lb == 0 && ldb < K) return false;
+  // per-thread DMA offsets are 32-bit byte offsets from the K-tile base (KC operands span all rows)
+  if (la == 0 && ((int64_t)(M - 1) * lda + K) * 2 >= (int64_t)1 << 32) return false;
+  if (lb == 0 && ((int64_t)(N - 1) * ldb + K) * 2 >= (int64_t)1 << 32) return false;
   return true;
 }
 
@@ -370,10 +378,16 @@ hipError_t launch_gemm_pipe(int la, int lb, const void* A, int64_t lda, const vo
   a.ablate = g_gp_ablate;
   a.kslice = ((K + splits - 1) / splits + GP_BK - 1) / GP_BK * GP_BK;
   const int BM = bm == 128 ? 128 : 256;
+  // 256 x 256 on 4 waves of 128 x 128 (one wave per SIMD, AGPR accumulators): measured 16-27 % slower than
+  // the 8-wave tile under hipcc's schedule (profiles/r2_v3_gemm_pipe_bench.log); kept for A/B
+  const bool w4 = bm == 1256;
   const int ntiles = ((M + BM - 1) / BM) * ((N + 255) / 256) * splits;
   const int nwg = ntiles;
-#define GP_LAUNCH(LA_, LB_, MI_, EPI_) \
-  hipLaunchKernelGGL((gemm_pipe_k<LA_, LB_, MI_, EPI_>), dim3(nwg), dim3(GP_NT), 0, st, a)
+#define GP_LAUNCH(LA_, LB_, MI_, EPI_)                                                                 \
+  if (w4 && LA_ == 0 && LB_ == 0)                                                                      \
+    hipLaunchKernelGGL((gemm_pipe_k<0, 0, MI_, EPI_, 0, 2>), dim3(nwg), dim3(256), 0, st, a);           \
+  else                                                                                                 \
+    hipLaunchKernelGGL((gemm_pipe_k<LA_, LB_, MI_, EPI_>), dim3(nwg), dim3(GP_NT), 0, st, a)
 #define GP_EPI(LA_, LB_, MI_)                 \
   switch (epi) {                              \
     case 0: GP_LAUNCH(LA_, LB_, MI_, 0); break; \

@@ -7,6 +7,9 @@
 
 namespace mamba_amd {
 
+// Backward kernels with a `part` buffer write one fp32 partial row per workgroup for a parameter
+// gradient; pacc = true ADDS into the rows instead (accumulation across the no-sync micro-steps of one
+// optimizer step), and dw == nullptr skips the final column sum (deferred to the sync micro-step).
 // deterministic column sum of a (nrows, ncols) fp32 partial matrix (norm.hip)
 hipError_t launch_colsum(float* part, int nrows, int ncols, float* out, hipStream_t st);  // clobbers part
 
@@ -17,14 +20,14 @@ hipError_t launch_add_rmsnorm_fwd(const void* x, int xdt, int64_t sx, const void
 int add_rmsnorm_bwd_partial_rows(int64_t M);
 hipError_t launch_add_rmsnorm_bwd(const void* dy, int ydt, const void* dro, int drodt, const void* ro, int rodt,
                                   const float* w, const float* rstd, void* dx, int xdt, void* dres, int rdt,
-                                  float* part, float* dw, int64_t M, int D, hipStream_t st);
+                                  float* part, float* dw, bool pacc, int64_t M, int D, hipStream_t st);
 hipError_t launch_gated_rmsnorm_fwd(const void* x, int xdt, int64_t sx, const void* z, int zdt, int64_t sz,
                                     const float* w, void* y, int ydt, float* rstd, int64_t M, int D, int G,
                                     float eps, bool nbg, hipStream_t st);
 int norm_bwd_partial_rows(int64_t M);
 hipError_t launch_gated_rmsnorm_bwd(const void* dy, int ydt, const void* x, int xdt, int64_t sx, const void* z,
                                     int zdt, int64_t sz, const float* w, const float* rstd, void* dx, int64_t sdx,
-                                    void* dz, int64_t sdz, float* part, float* dw, int64_t M, int D, int G,
+                                    void* dz, int64_t sdz, float* part, float* dw, bool pacc, int64_t M, int D, int G,
                                     bool nbg, hipStream_t st);
 
 // ---- cross_entropy.hip ------------------------------------------------------------------------
@@ -38,7 +41,7 @@ hipError_t launch_conv_cf_fwd(const void* x, int dt, int64_t sxb, int64_t sxd, c
                               hipStream_t st);
 hipError_t launch_conv_cf_bwd(const void* x, int dt, int64_t sxb, int64_t sxd, const float* w, const float* bias,
                               const void* g, int64_t sgb, int64_t sgd, void* dx, int64_t sdb, int64_t sdd,
-                              float* part, float* dw, float* db, int Bn, int Dn, int L, int Wd, bool silu,
+                              float* part, float* dw, float* db, bool pacc, int Bn, int Dn, int L, int Wd, bool silu,
                               hipStream_t st);
 hipError_t launch_conv_cl_fwd(const void* x, int dt, int64_t sxb, int64_t sxl, const float* w, const float* bias,
                               void* out, int64_t sob, int64_t sol, int Bn, int L, int C, int Wd, bool silu,
@@ -46,7 +49,7 @@ hipError_t launch_conv_cl_fwd(const void* x, int dt, int64_t sxb, int64_t sxl, c
 int conv_cl_bwd_partial_rows(int Bn, int L);
 hipError_t launch_conv_cl_bwd(const void* x, int dt, int64_t sxb, int64_t sxl, const float* w, const float* bias,
                               const void* g, int64_t sgb, int64_t sgl, void* dx, int64_t sdb, int64_t sdl,
-                              float* part, float* dw, float* db, int Bn, int L, int C, int Wd, bool silu,
+                              float* part, float* dw, float* db, bool pacc, int Bn, int L, int C, int Wd, bool silu,
                               hipStream_t st);
 hipError_t launch_conv_update(const void* x, int dt, int64_t sxb, void* state, int64_t ssb, int64_t ssc,
                               const float* w, const float* bias, void* out, int Bn, int C, int Wd, bool silu,

@@ -73,7 +73,7 @@ __global__ __launch_bounds__(256) void add_rmsnorm_fwd_k(
 
 // block-level partial reduction of per-wave dw accumulators -> part[blockIdx.x][D]
 template <int NCH>
-__device__ __forceinline__ void block_dw_partial(float (&acc)[NCH][4], float* part, int D, float* lds) {
+__device__ __forceinline__ void block_dw_partial(float (&acc)[NCH][4], float* part, int D, float* lds, bool pacc) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
@@ -85,7 +85,9 @@ __device__ __forceinline__ void block_dw_partial(float (&acc)[NCH][4], float* pa
   }
   __syncthreads();
   for (int col = threadIdx.x; col < D; col += blockDim.x) {
-    part[(int64_t)blockIdx.x * D + col] = lds[col] + lds[D + col] + lds[2 * D + col] + lds[3 * D + col];
+    const int64_t i = (int64_t)blockIdx.x * D + col;
+    const float v = lds[col] + lds[D + col] + lds[2 * D + col] + lds[3 * D + col];
+    part[i] = pacc ? part[i] + v : v;  // pacc: accumulate across micro-steps (reduced once per optimizer step)
   }
 }
 
@@ -93,7 +95,7 @@ template <int NCH>
 __global__ __launch_bounds__(256) void add_rmsnorm_bwd_k(
     const void* __restrict__ dy, int ydt, const void* __restrict__ dro, int drodt,
     const void* __restrict__ ro, int rodt, const float* __restrict__ w, const float* __restrict__ rstd,
-    void* __restrict__ dx, int xdt, void* __restrict__ dres, int rdt, float* __restrict__ part,
+    void* __restrict__ dx, int xdt, void* __restrict__ dres, int rdt, float* __restrict__ part, bool pacc,
     int64_t M, int D) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int lane = threadIdx.x & 63;
@@ -142,7 +144,7 @@ __global__ __launch_bounds__(256) void add_rmsnorm_bwd_k(
       }
     }
   }
-  block_dw_partial<NCH>(acc, part, D, lds);
+  block_dw_partial<NCH>(acc, part, D, lds, pacc);
 }
 
 // out[c] = sum_r part[r * rstride + c] in a fixed order.  Block = 64 columns x 16 row-groups (1024
@@ -280,7 +282,7 @@ __global__ __launch_bounds__(256) void gated_rmsnorm_bwd_k(
     const void* __restrict__ dy, int ydt, const void* __restrict__ x, int xdt, int64_t sx,
     const void* __restrict__ z, int zdt, int64_t sz, const float* __restrict__ w,
     const float* __restrict__ rstd, void* __restrict__ dx, int64_t sdx, void* __restrict__ dz, int64_t sdz,
-    float* __restrict__ part, int64_t M, int D, int G) {
+    float* __restrict__ part, bool pacc, int64_t M, int D, int G) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int lane = threadIdx.x & 63;
   const int ngroups = D / G;
@@ -358,7 +360,7 @@ __global__ __launch_bounds__(256) void gated_rmsnorm_bwd_k(
       }
     }
   }
-  block_dw_partial<NCH>(acc, part, D, lds);
+  block_dw_partial<NCH>(acc, part, D, lds, pacc);
 }
 
 // bf16 fast path of the gated backward: x / z / dy stay PACKED (4 bf16 = 2 VGPRs per chunk) between
@@ -372,7 +374,7 @@ template <int NCH, bool NBG>
 __global__ __launch_bounds__(256) void gated_rmsnorm_bwd_bf16_k(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, int64_t sx, const bf16_t* __restrict__ z,
     int64_t sz, const float* __restrict__ w, const float* __restrict__ rstd, bf16_t* __restrict__ dx, int64_t sdx,
-    bf16_t* __restrict__ dz, int64_t sdz, float* __restrict__ part, int64_t M, int D, int G) {
+    bf16_t* __restrict__ dz, int64_t sdz, float* __restrict__ part, bool pacc, int64_t M, int D, int G) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int lane = threadIdx.x & 63;
   const int ngroups = D / G;
@@ -461,7 +463,7 @@ __global__ __launch_bounds__(256) void gated_rmsnorm_bwd_bf16_k(
       }
     }
   }
-  block_dw_partial<NCH>(acc, part, D, lds);
+  block_dw_partial<NCH>(acc, part, D, lds, pacc);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -528,7 +530,7 @@ template <int NCH>
 __global__ __launch_bounds__(256) void gated_rmsnorm_bwd_v8_k(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, int64_t sx, const bf16_t* __restrict__ z,
     int64_t sz, const float* __restrict__ w, const float* __restrict__ rstd, bf16_t* __restrict__ dx, int64_t sdx,
-    bf16_t* __restrict__ dz, int64_t sdz, float* __restrict__ part, int64_t M, int D) {
+    bf16_t* __restrict__ dz, int64_t sdz, float* __restrict__ part, bool pacc, int64_t M, int D) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float acc[NCH][8];
@@ -601,8 +603,11 @@ __global__ __launch_bounds__(256) void gated_rmsnorm_bwd_v8_k(
     for (int j = 0; j < 8; ++j) lds[wave * D + col + j] = acc[c][j];
   }
   __syncthreads();
-  for (int col = threadIdx.x; col < D; col += blockDim.x)
-    part[(int64_t)blockIdx.x * D + col] = lds[col] + lds[D + col] + lds[2 * D + col] + lds[3 * D + col];
+  for (int col = threadIdx.x; col < D; col += blockDim.x) {
+    const int64_t i = (int64_t)blockIdx.x * D + col;
+    const float v = lds[col] + lds[D + col] + lds[2 * D + col] + lds[3 * D + col];
+    part[i] = pacc ? part[i] + v : v;
+  }
 }
 
 #define NCH8_SWITCH(D, ...)                                         \
@@ -672,13 +677,13 @@ int add_rmsnorm_bwd_partial_rows(int64_t M) { return bwd_grid(M); }
 
 hipError_t launch_add_rmsnorm_bwd(const void* dy, int ydt, const void* dro, int drodt, const void* ro, int rodt,
                                   const float* w, const float* rstd, void* dx, int xdt, void* dres, int rdt,
-                                  float* part, float* dw, int64_t M, int D, hipStream_t st) {
+                                  float* part, float* dw, bool pacc, int64_t M, int D, hipStream_t st) {
   const int g = bwd_grid(M);
   const size_t lds = 4 * (size_t)D * sizeof(float);
   NCH_SWITCH(D, hipLaunchKernelGGL((add_rmsnorm_bwd_k<NCH>), dim3(g), dim3(256), lds, st, dy, ydt, dro, drodt, ro,
-                                   rodt, w, rstd, dx, xdt, dres, rdt, part, M, D));
+                                   rodt, w, rstd, dx, xdt, dres, rdt, part, pacc, M, D));
   MAMBA_HIP_CHECK(hipGetLastError());
-  return launch_colsum(part, g, D, dw, st);
+  return dw ? launch_colsum(part, g, D, dw, st) : hipSuccess;
 }
 
 hipError_t launch_gated_rmsnorm_fwd(const void* x, int xdt, int64_t sx, const void* z, int zdt, int64_t sz,
@@ -703,7 +708,7 @@ hipError_t launch_gated_rmsnorm_fwd(const void* x, int xdt, int64_t sx, const vo
 
 hipError_t launch_gated_rmsnorm_bwd(const void* dy, int ydt, const void* x, int xdt, int64_t sx, const void* z,
                                     int zdt, int64_t sz, const float* w, const float* rstd, void* dx, int64_t sdx,
-                                    void* dz, int64_t sdz, float* part, float* dw, int64_t M, int D, int G,
+                                    void* dz, int64_t sdz, float* part, float* dw, bool pacc, int64_t M, int D, int G,
                                     bool nbg, hipStream_t st) {
   const int g = bwd_grid(M);
   const size_t lds = 4 * (size_t)D * sizeof(float);
@@ -712,24 +717,24 @@ hipError_t launch_gated_rmsnorm_bwd(const void* dy, int ydt, const void* x, int 
       (uintptr_t)dx % 16 == 0 && (uintptr_t)dz % 16 == 0 && (uintptr_t)dy % 16 == 0) {
     NCH8_SWITCH(D, hipLaunchKernelGGL((gated_rmsnorm_bwd_v8_k<NCH>), dim3(g), dim3(256), lds, st, (const bf16_t*)dy,
                                       (const bf16_t*)x, sx, (const bf16_t*)z, sz, w, rstd, (bf16_t*)dx, sdx,
-                                      (bf16_t*)dz, sdz, part, M, D));
+                                      (bf16_t*)dz, sdz, part, pacc, M, D));
   } else if (fast && nbg) {
     NCH_SWITCH(D, hipLaunchKernelGGL((gated_rmsnorm_bwd_bf16_k<NCH, true>), dim3(g), dim3(256), lds, st,
                                      (const bf16_t*)dy, (const bf16_t*)x, sx, (const bf16_t*)z, sz, w, rstd,
-                                     (bf16_t*)dx, sdx, (bf16_t*)dz, sdz, part, M, D, G));
+                                     (bf16_t*)dx, sdx, (bf16_t*)dz, sdz, part, pacc, M, D, G));
   } else if (fast) {
     NCH_SWITCH(D, hipLaunchKernelGGL((gated_rmsnorm_bwd_bf16_k<NCH, false>), dim3(g), dim3(256), lds, st,
                                      (const bf16_t*)dy, (const bf16_t*)x, sx, (const bf16_t*)z, sz, w, rstd,
-                                     (bf16_t*)dx, sdx, (bf16_t*)dz, sdz, part, M, D, G));
+                                     (bf16_t*)dx, sdx, (bf16_t*)dz, sdz, part, pacc, M, D, G));
   } else if (nbg) {
     NCH_SWITCH(D, hipLaunchKernelGGL((gated_rmsnorm_bwd_k<NCH, true>), dim3(g), dim3(256), lds, st, dy, ydt, x,
-                                     xdt, sx, z, zdt, sz, w, rstd, dx, sdx, dz, sdz, part, M, D, G));
+                                     xdt, sx, z, zdt, sz, w, rstd, dx, sdx, dz, sdz, part, pacc, M, D, G));
   } else {
     NCH_SWITCH(D, hipLaunchKernelGGL((gated_rmsnorm_bwd_k<NCH, false>), dim3(g), dim3(256), lds, st, dy, ydt, x,
-                                     xdt, sx, z, zdt, sz, w, rstd, dx, sdx, dz, sdz, part, M, D, G));
+                                     xdt, sx, z, zdt, sz, w, rstd, dx, sdx, dz, sdz, part, pacc, M, D, G));
   }
   MAMBA_HIP_CHECK(hipGetLastError());
-  return launch_colsum(part, g, D, dw, st);
+  return dw ? launch_colsum(part, g, D, dw, st) : hipSuccess;
 }
 
 int norm_bwd_partial_rows(int64_t M) { return bwd_grid(M); }

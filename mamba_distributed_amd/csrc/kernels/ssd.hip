@@ -467,12 +467,15 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
       const float dbp = wave_sum(gdt);
       if (l == 0) {
         const int64_t pi = ((int64_t)b * a.nc + c) * a.psl + h;
-        a.part_dA[pi] = a.a_log ? dAp * Ah : dAp;  // d/dA_log = dA * A
-        a.part_dbias[pi] = dbp;
+        const float pa = a.a_log ? dAp * Ah : dAp;  // d/dA_log = dA * A
         float dd = 0.f;
 #pragma unroll
         for (int v = 0; v < 8; ++v) dd += redw[sl][v];
-        a.part_dD[pi] = dd;
+        if (a.pacc) {
+          a.part_dA[pi] += pa; a.part_dbias[pi] += dbp; a.part_dD[pi] += dd;
+        } else {
+          a.part_dA[pi] = pa; a.part_dbias[pi] = dbp; a.part_dD[pi] = dd;
+        }
       }
       // recycle this head's slots for head hh + 8 (the next head's top barrier orders it)
 #pragma unroll

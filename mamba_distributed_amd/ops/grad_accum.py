@@ -12,6 +12,12 @@ projection gradients.  Inside an ``accumulation_scope`` on the no-sync micro-ste
   * every other parameter gradient produced by a native op is queued and applied by ONE
     ``torch._foreach_add_`` when the backward pass finishes.
 
+  * parameter gradients that kernels produce as per-workgroup partial rows (norm weights, conv taps,
+    A_log / D / dt_bias) or as K-split fp32 slabs (projection weights) are NOT reduced on the no-sync
+    micro-steps at all: the kernels add into persistent per-parameter buffers (``deferred``) and the
+    column sum / slab sum runs once, on the sync micro-step, whose autograd return then carries the
+    whole step's gradient (set MAMBA_AMD_DEFER_REDUCE=0 to reduce on every micro-step instead).
+
 The last micro-step (the one that triggers DDP's bucketed all-reduce) and anything outside a scope
 use the normal autograd path, so DDP's gradient hooks fire exactly as usual.  The scope also caches
 bf16 copies of the projection weights: weights cannot change between the micro-steps of one
@@ -32,6 +38,7 @@ _side_dirty = set()   # devices whose side stream has work the main stream has n
 _pending: List[Tuple[torch.Tensor, torch.Tensor]] = []
 _flush_queued = False
 _wcache: Dict[Tuple[int, torch.dtype], Tuple[torch.Tensor, torch.Tensor]] = {}
+_bufs: Dict[Tuple[int, str], list] = {}  # (id(param), tag) -> [param, fp32 buffer, holds this step's partials]
 
 
 @contextlib.contextmanager
@@ -46,6 +53,8 @@ def accumulation_scope():
         if _scope_depth == 0:
             _direct = False
             _wcache.clear()
+            for ent in _bufs.values():  # buffers are kept (reused next step); their contents are dead
+                ent[2] = False
             join_side()
 
 
@@ -81,6 +90,36 @@ def join_side() -> None:
     for idx in list(_side_dirty):
         torch.cuda.current_stream(idx).wait_stream(_side[idx])
     _side_dirty.clear()
+
+
+def deferred(param, tag: str, shape, device):
+    """Deferred reduction of ``param``'s gradient inside an accumulation scope.
+
+    Returns None outside a scope (the op reduces as usual), else ``(buffer, part_mode)``: a persistent fp32
+    buffer of ``shape`` owned by (param, tag) and the mode for the op -- 1 / 2: store / add this
+    micro-step's partials, no reduction, the op returns an empty gradient (no-sync micro-step); 3 / 4:
+    store / add, then reduce: the op returns the gradient of every micro-step of this optimizer step
+    (sync micro-step).  A second call in the same sync micro-step starts over (3) and its gradient is
+    added by autograd as usual."""
+    import os
+    if (_scope_depth == 0 or not isinstance(param, torch.Tensor) or not param.requires_grad
+            or os.environ.get("MAMBA_AMD_DEFER_REDUCE", "1") == "0"):
+        return None
+    key = (id(param), tag)
+    shape = tuple(int(v) for v in shape)
+    ent = _bufs.get(key)
+    if ent is None or ent[0] is not param or tuple(ent[1].shape) != shape or ent[1].device != device:
+        ent = [param, torch.empty(shape, device=device, dtype=torch.float32), False]
+        _bufs[key] = ent
+    final = not _direct
+    mode = (4 if ent[2] else 3) if final else (2 if ent[2] else 1)
+    ent[2] = not final
+    return ent[1], mode
+
+
+def release_buffers() -> None:
+    """Free every deferred-reduction buffer (e.g. before switching models)."""
+    _bufs.clear()
 
 
 def in_scope() -> bool:

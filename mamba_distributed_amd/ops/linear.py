@@ -1,11 +1,13 @@
 """Bias-free projection (nn.Linear without bias) with a native weight-gradient GEMM.
 
-Forward and input-gradient GEMMs stay on hipBLASLt (the pinned TunableOp solutions reach
-~1000 TF/s on these shapes).  The weight gradient dW = dY^T X reduces over all B*T tokens into a
-small output (768 x 1536 for out_proj), where the library leaves most CUs idle: the native
-``gemm_wgrad`` splits the token dimension across workgroups (256 x 256 MFMA tiles, LDS-DMA staged,
-fixed-order fp32 reduction) and returns the gradient directly in fp32 -- the parameter's dtype --
-so the bf16 -> fp32 cast kernel disappears as well (csrc/kernels/gemm.hip).
+Forward and input-gradient GEMMs are plain GEMMs (no fusion) and run on whichever of hipBLASLt (pinned
+TunableOp table) and the native engine is faster for the shape (``utils/gemm_tuning``).  The weight
+gradient dW = dY^T X reduces over all B*T tokens into a small output (3352 x 768 for in_proj), where the
+library leaves most CUs idle: the native engine (csrc/kernels/gemm_pipe.hip, ``gp_mm`` with both operands
+token-major) splits the tokens into S K-slices written as fp32 slabs.  Inside an accumulation scope the
+slabs are PERSISTENT per weight: the no-sync micro-steps add into them (on a side stream, beside the rest
+of the backward) and the fixed-order slab sum runs once per optimizer step, on the sync micro-step, which
+returns the whole step's gradient in fp32 -- the parameter's dtype.
 Autocast semantics match ``F.linear`` under ``torch.autocast``: compute in the autocast dtype.
 """
 from __future__ import annotations
@@ -27,6 +29,38 @@ def _native_ok(dy: torch.Tensor, x: torch.Tensor) -> bool:
     return (dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and dy.stride(-1) == 1 and x.stride(-1) == 1
             and dy.shape[-1] % 8 == 0 and x.shape[-1] % 8 == 0 and dy.stride(0) % 8 == 0 and x.stride(0) % 8 == 0
             and dy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0)
+
+
+def _wgrad_native(p, dy2: torch.Tensor, x2: torch.Tensor):
+    """dW = dy2^T x2 (fp32) on the native engine; None when deferred to the sync micro-step."""
+    ops = _ext.ops()
+    T, P, Q = dy2.shape[0], dy2.shape[1], x2.shape[1]
+    S = ops.gp_splits(P, Q, T)
+    d = grad_accum.deferred(p, "wgrad", (S, P, Q), dy2.device)
+    if d is None:  # outside an accumulation scope: transient slabs, reduce now
+        part = ops.gp_mm(dy2, x2, None, 1, 1, 1, S, 256)
+        dw = torch.empty(P, Q, device=dy2.device, dtype=torch.float32)
+        ops.gp_reduce(part, dw, False)
+        return dw
+    buf, mode = d
+    slab_mode = 1 if mode in (1, 3) else 2  # store / add
+    if mode <= 2:
+        # no-sync micro-step: nothing consumes the slabs before the sync step, so the GEMM runs on the side
+        # stream beside the rest of the backward (joined before the sync micro-step)
+        side = grad_accum.side_stream(dy2.device)
+        if side is None:
+            ops.gp_mm(dy2, x2, buf, 1, 1, slab_mode, S, 256)
+        else:
+            side.wait_stream(torch.cuda.current_stream(dy2.device))
+            with torch.cuda.stream(side):
+                ops.gp_mm(dy2, x2, buf, 1, 1, slab_mode, S, 256)
+            dy2.record_stream(side)
+            x2.record_stream(side)
+        return None
+    ops.gp_mm(dy2, x2, buf, 1, 1, slab_mode, S, 256)
+    dw = torch.empty(P, Q, device=dy2.device, dtype=torch.float32)
+    ops.gp_reduce(buf, dw, False)
+    return dw
 
 
 class _ProjFn(torch.autograd.Function):
@@ -53,23 +87,12 @@ class _ProjFn(torch.autograd.Function):
         dw = None
         if ctx.needs_input_grad[1]:
             p = ctx.param
-            native = _native_ok(dy2, x2)
-            if (native and grad_accum.accumulable(p) and p.grad.dtype == torch.float32 and p.grad.is_contiguous()
-                    and p.grad.shape == w.shape):
-                # no-sync micro-step: the split-K reduction adds straight into p.grad, on a side stream
-                # beside the rest of the backward (grad_accum.side_stream; joined before the sync step)
-                side = grad_accum.side_stream(dy2.device)
-                if side is None:
-                    _ext.ops().gemm_wgrad(dy2, x2, p.grad, True)
-                else:
-                    side.wait_stream(torch.cuda.current_stream(dy2.device))
-                    with torch.cuda.stream(side):
-                        _ext.ops().gemm_wgrad(dy2, x2, p.grad, True)
-                    dy2.record_stream(side)
-                    x2.record_stream(side)
+            if _native_ok(dy2, x2):
+                dw = _wgrad_native(p, dy2, x2)
+                if dw is not None:
+                    dw = grad_accum.defer(p, dw.to(ctx.wdtype))
             else:
-                dw = _ext.ops().gemm_wgrad(dy2, x2, None, False) if native else torch.mm(dy2.t(), x2)
-                dw = grad_accum.defer(p, dw.to(ctx.wdtype))
+                dw = grad_accum.defer(p, torch.mm(dy2.t(), x2).to(ctx.wdtype))
         return (dx.view(ctx.xshape) if dx is not None else None), dw, None
 
 

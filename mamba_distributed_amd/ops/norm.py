@@ -61,9 +61,14 @@ class _AddRMSNormFn(torch.autograd.Function):
         # the same gradient flows to x and to residual: write it once per needed dtype
         want_res = ctx.has_residual and ctx.needs_input_grad[2]
         res_dtype = ctx.res_dtype if want_res else None
-        dx, dres, dw = _ext.ops().add_rmsnorm_bwd(dy2, dr2, res_out, weight, rstd, ctx.x_dtype,
-                                                  res_dtype if res_dtype is not None else ctx.x_dtype,
-                                                  want_res and res_dtype != ctx.x_dtype)
+        ops = _ext.ops()
+        d = grad_accum.deferred(ctx.param, "rmsnorm", (ops.part_rows("add_rmsnorm", dy2.shape[0]), dy2.shape[1]),
+                                dy2.device) if ctx.needs_input_grad[1] else None
+        dx, dres, dw = ops.add_rmsnorm_bwd(dy2, dr2, res_out, weight, rstd, ctx.x_dtype,
+                                           res_dtype if res_dtype is not None else ctx.x_dtype,
+                                           want_res and res_dtype != ctx.x_dtype, *(d or (None, 0)))
+        if dw.numel() == 0:  # deferred to the sync micro-step
+            dw = None
         dx = dx.view(shape)
         dresidual = None
         if want_res:
@@ -113,8 +118,13 @@ class _GatedRMSNormFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x2, z2, weight, rstd = ctx.saved_tensors
-        dx, dz, dw = _ext.ops().gated_rmsnorm_bwd(_rows(dy), x2, z2, weight, rstd, ctx.group_size,
-                                                  ctx.nbg, None, None)
+        ops = _ext.ops()
+        d = grad_accum.deferred(ctx.param, "gated_rmsnorm", (ops.part_rows("gated_rmsnorm", x2.shape[0]),
+                                                             x2.shape[1]), x2.device)
+        dx, dz, dw = ops.gated_rmsnorm_bwd(_rows(dy), x2, z2, weight, rstd, ctx.group_size, ctx.nbg, None, None,
+                                           *(d or (None, 0)))
+        if dw.numel() == 0:
+            dw = None
         return dx.view(ctx.shape), dz.view(ctx.shape), grad_accum.defer(ctx.param, dw), None, None, None
 
 

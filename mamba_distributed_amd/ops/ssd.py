@@ -126,10 +126,16 @@ class _Mamba2InnerFn(torch.autograd.Function):
         conv_dim = di + 2 * gn
         dz_all = torch.empty_like(zxbcdt)
         z = zxbcdt[..., :di]
+        pw, pb, pdtb, pA, pD, pn = ctx.params
+        dev = zxbcdt.device
+        # parameter-gradient partials are reduced once per optimizer step (grad_accum.deferred)
+        d_n = grad_accum.deferred(pn, "gated_rmsnorm", (ops.part_rows("gated_rmsnorm", b * l), di), dev)
+        d_s = grad_accum.deferred(pA, "ssd_small", (b * ((l + NATIVE_CHUNK - 1) // NATIVE_CHUNK), 3, H), dev)
+        d_c = grad_accum.deferred(pw, "conv_cl", (ops.part_rows("conv_cl", b, l), conv_dim, w2.shape[1] + 1), dev)
         # gated norm backward writes dz straight into its slice of d(zxbcdt)
         dy, _, dnorm_w = ops.gated_rmsnorm_bwd(dyn.reshape(b * l, di), y.view(b * l, di),
                                                z.flatten(0, 1), norm_w, rstd, di // ngroups, nbg,
-                                               None, dz_all[..., :di].flatten(0, 1))
+                                               None, dz_all[..., :di].flatten(0, 1), *(d_n or (None, 0)))
         x = xBC_c[..., :di].unflatten(-1, (H, headdim))
         Bm = xBC_c[..., di:di + gn].unflatten(-1, (ngroups, d_state))
         Cm = xBC_c[..., di + gn:].unflatten(-1, (ngroups, d_state))
@@ -140,15 +146,18 @@ class _Mamba2InnerFn(torch.autograd.Function):
                         dxBC_c[..., :di].unflatten(-1, (H, headdim)),
                         dz_all[..., di + conv_dim:],
                         dxBC_c[..., di:di + gn].unflatten(-1, (ngroups, d_state)),
-                        dxBC_c[..., di + gn:].unflatten(-1, (ngroups, d_state)), a_log)
+                        dxBC_c[..., di + gn:].unflatten(-1, (ngroups, d_state)), a_log, *(d_s or (None, 0)))
         _, _, dA, _, _, dD, ddt_bias, _ = g
         xBC = zxbcdt[..., di:di + conv_dim]
-        _, dw, db = ops.conv1d_cl_bwd(xBC, w2, conv_b, dxBC_c, True, dz_all[..., di:di + conv_dim])
-        pw, pb, pdtb, pA, pD, pn = ctx.params
+        _, dw, db = ops.conv1d_cl_bwd(xBC, w2, conv_b, dxBC_c, True, dz_all[..., di:di + conv_dim],
+                                      *(d_c or (None, 0)))
         d = grad_accum.defer
-        return (dz_all, d(pw, dw.reshape(ctx.wshape).to(w2.dtype)),
-                d(pb, db.to(conv_b.dtype)) if conv_b is not None else None,
-                d(pdtb, ddt_bias), d(pA, dA), d(pD, dD), d(pn, dnorm_w), None, None, None, None, None, None, None, None)
+        nz = lambda t: t if t.numel() else None  # noqa: E731  (empty = deferred to the sync micro-step)
+        dw = nz(dw)
+        return (dz_all, d(pw, dw.reshape(ctx.wshape).to(w2.dtype)) if dw is not None else None,
+                d(pb, nz(db).to(conv_b.dtype)) if (conv_b is not None and db.numel()) else None,
+                d(pdtb, nz(ddt_bias)), d(pA, nz(dA)), d(pD, nz(dD)), d(pn, nz(dnorm_w)),
+                None, None, None, None, None, None, None, None)
 
 
 def mamba2_inner_ref(zxbcdt, conv_w, conv_b, dt_bias, A, D, norm_w, eps, headdim, ngroups, d_state,

@@ -79,12 +79,15 @@ def main():
     cases = {
         # name: (flop, {arm: fn})
         "in_fwd": (2 * T * d * dp, {"lib": lambda: torch.nn.functional.linear(x, W_in),
-                                    "gp": lambda: ops.gp_mm(x, W_in, None, 0, 0, 0, 1, 256)}),
+                                    "gp": lambda: ops.gp_mm(x, W_in, None, 0, 0, 0, 1, 256),
+                                    "gp4w": lambda: ops.gp_mm(x, W_in, None, 0, 0, 0, 1, 1256)}),
         "in_dgrad": (2 * T * d * dp, {"lib": lambda: torch.mm(zx, W_in),
-                                      "gp": lambda: ops.gp_mm(zx, W_in, None, 0, 1, 0, 1, 256)}),
+                                      "gp": lambda: ops.gp_mm(zx, W_in, None, 0, 1, 0, 1, 256),
+                                      "gp128": lambda: ops.gp_mm(zx, W_in, None, 0, 1, 0, 1, 128)}),
         "out_fwd": (2 * T * d * di, {"lib": lambda: torch.nn.functional.linear(y, W_out),
                                      "gp": lambda: ops.gp_mm(y, W_out, None, 0, 0, 0, 1, 256),
-                                     "gp128": lambda: ops.gp_mm(y, W_out, None, 0, 0, 0, 1, 128)}),
+                                     "gp128": lambda: ops.gp_mm(y, W_out, None, 0, 0, 0, 1, 128),
+                                     "gp4w": lambda: ops.gp_mm(y, W_out, None, 0, 0, 0, 1, 1256)}),
         "out_dgrad": (2 * T * d * di, {"lib": lambda: torch.mm(dout, W_out),
                                        "gp": lambda: ops.gp_mm(dout, W_out, None, 0, 1, 0, 1, 256)}),
     }

@@ -34,12 +34,14 @@ def _rel(a, b):
 @pytest.mark.parametrize("la,lb", [(0, 0), (0, 1), (1, 1)])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 768), (300, 264, 200), (1000, 3352, 96),
                                    (768, 520, 1544), (64, 8, 32), (512, 256, 1024)])
-@pytest.mark.parametrize("bm", [256, 128])
+@pytest.mark.parametrize("bm", [256, 128, 1256])
 def test_gp_bf16(cuda, la, lb, M, N, K, bm):
     if la == 1 and (M % 8):
         pytest.skip("XC A needs M % 8 == 0")
     if la == 1 and bm == 128:
         pytest.skip("XC A is instantiated at BM = 256 only")
+    if bm == 1256 and (la, lb) != (0, 0):
+        pytest.skip("the 4-wave tile is instantiated for KC.KC only")
     ops = _ops()
     g = torch.Generator(device=cuda).manual_seed(M * 7 + N * 3 + K)
     A, B = _mk(M, K, la, cuda, g), _mk(N, K, lb, cuda, g)
@@ -58,7 +60,7 @@ def test_gp_fp32_modes_and_splits(cuda, la, lb):
     A, B = _mk(M, K, la, cuda, g), _mk(N, K, lb, cuda, g)
     ref = _ref(A, B, la, lb)
     C = ops.gp_mm(A, B, None, la, lb, 1, 1, 256)
-    assert C.dtype == torch.float32 and _rel(C, ref) < 1e-5
+    assert C.dtype == torch.float32 and C.shape == (1, M, N) and _rel(C[0], ref) < 1e-5
     acc = torch.randn(M, N, device=cuda, generator=g)
     acc0 = acc.clone()
     ops.gp_mm(A, B, acc, la, lb, 2, 1, 256)
@@ -72,6 +74,18 @@ def test_gp_fp32_modes_and_splits(cuda, la, lb):
         # deterministic: identical bits on a second run
         part2 = ops.gp_mm(A, B, None, la, lb, 1, S, 256)
         assert torch.equal(part, part2)
+
+
+def test_gp_xc_ragged_k(cuda):
+    """Weight-gradient layout (both operands token-major) with a token count that is not a multiple of 8."""
+    ops = _ops()
+    g = torch.Generator(device=cuda).manual_seed(4)
+    for T in (318, 1, 65):
+        A, B = _mk(264, T, 1, cuda, g), _mk(136, T, 1, cuda, g)
+        part = ops.gp_mm(A, B, None, 1, 1, 1, 1, 256)
+        out = torch.zeros(264, 136, device=cuda)
+        ops.gp_reduce(part, out, False)
+        assert _rel(out, _ref(A, B, 1, 1)) < 1e-5, T
 
 
 def test_gp_strided_views(cuda):
