@@ -296,13 +296,15 @@ Tensor conv1d_update(Tensor x, Tensor conv_state, Tensor weight, optional<Tensor
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be (b, c)");
   const int64_t B = x.size(0), C = x.size(1);
   Tensor w = f32c(weight);
-  TORCH_CHECK(w.size(0) == C && conv_state.size(0) == B && conv_state.size(1) == C && conv_state.size(2) == w.size(1) - 1 &&
-              conv_state.stride(2) == 1 && conv_state.scalar_type() == x.scalar_type(), "conv_state layout");
+  TORCH_CHECK(w.size(0) == C && conv_state.size(0) == B && conv_state.size(1) == C && conv_state.size(2) >= w.size(1) - 1 &&
+              conv_state.size(2) <= 16 && conv_state.stride(2) == 1 && conv_state.scalar_type() == x.scalar_type(),
+              "conv_state must be (b, c, state_len >= w-1) with unit last stride");
   Tensor bb = f32c_opt(bias);
   auto out = at::empty({B, C}, x.options());
   HIPCHK(mamba_amd::launch_conv_update(x.data_ptr(), dcode(x.scalar_type()), x.stride(0), conv_state.data_ptr(),
                                        conv_state.stride(0), conv_state.stride(1), w.data_ptr<float>(), fptr(bb),
-                                       out.data_ptr(), (int)B, (int)C, (int)w.size(1), silu, cur_stream()));
+                                       out.data_ptr(), (int)B, (int)C, (int)w.size(1), (int)conv_state.size(2), silu,
+                                       cur_stream()));
   return out;
 }
 
@@ -765,8 +767,10 @@ void decode_inproj(Tensor hn, Tensor W, Tensor zxbcdt, int64_t conv_lo, int64_t 
   const int64_t C = conv_hi - conv_lo;
   TORCH_CHECK(conv_lo >= 0 && conv_hi <= n_out && C > 0, "decode: conv range");
   TORCH_CHECK(conv_state.scalar_type() == at::kBFloat16 && conv_state.dim() == 3 && conv_state.size(0) == b &&
-              conv_state.size(1) == C && conv_state.stride(2) == 1, "decode: conv_state (b, C, W-1) bf16");
-  const int64_t Wd = conv_state.size(2) + 1;
+              conv_state.size(1) == C && conv_state.stride(2) == 1, "decode: conv_state (b, C, state_len) bf16");
+  TORCH_CHECK(conv_w.numel() % C == 0, "decode: conv_w (C, W)");
+  const int64_t Wd = conv_w.numel() / C;
+  TORCH_CHECK(conv_state.size(2) >= Wd - 1 && conv_state.size(2) <= 16, "decode: state_len >= W-1");
   chk_f32(conv_w, C * Wd, "conv_w");
   const float* cb = nullptr;
   if (conv_b.has_value() && conv_b->defined()) {
@@ -775,7 +779,8 @@ void decode_inproj(Tensor hn, Tensor W, Tensor zxbcdt, int64_t conv_lo, int64_t 
   }
   HIPCHK(mamba_amd::launch_decode_inproj(hn.data_ptr(), W.data_ptr(), (int)n_out, (int)d, (int)b,
                                          zxbcdt.data_ptr<float>(), (int)conv_lo, (int)conv_hi, conv_state.data_ptr(),
-                                         conv_state.stride(0), conv_state.stride(1), conv_w.data_ptr<float>(), cb,
+                                         conv_state.stride(0), conv_state.stride(1), (int)conv_state.size(2),
+                                         conv_w.data_ptr<float>(), cb,
                                          (int)Wd, cur_stream()));
 }
 

@@ -557,20 +557,20 @@ __global__ __launch_bounds__(256) void conv_cl_bwd_bf16_k(const bf16_t* __restri
 template <typename T, int W>
 __global__ void conv_update_k(const T* __restrict__ x, int64_t sxb, T* __restrict__ state, int64_t ssb,
                               int64_t ssc, const float* __restrict__ w, const float* __restrict__ bias,
-                              T* __restrict__ out, int Bn, int C, bool silu) {
+                              T* __restrict__ out, int Bn, int C, int SL, bool silu) {
+  // state (SL >= W-1 columns, oldest first; causal-conv1d >= 1.4 semantics): the output uses its last W-1
+  // entries and x; afterwards the state holds the last SL inputs (shifted by one, x appended)
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= Bn * C) return;
   const int b = i / C, c = i % C;
   T* sp = state + b * ssb + c * ssc;
-  float win[W];
-#pragma unroll
-  for (int k = 0; k < W - 1; ++k) win[k] = ld(sp + k);
-  win[W - 1] = ld(x + b * sxb + c);
+  const float xv = ld(x + b * sxb + c);
   float a = bias ? bias[c] : 0.f;
 #pragma unroll
-  for (int k = 0; k < W; ++k) a += w[c * W + k] * win[k];
-#pragma unroll
-  for (int k = 0; k < W - 1; ++k) st(sp + k, win[k + 1]);
+  for (int k = 0; k < W - 1; ++k) a += w[c * W + k] * ld(sp + SL - (W - 1) + k);
+  a += w[c * W + W - 1] * xv;
+  for (int k = 0; k + 1 < SL; ++k) st(sp + k, ld(sp + k + 1));
+  if (SL > 0) st(sp + SL - 1, xv);
   st(out + (int64_t)b * C + c, act_fwd(a, silu));
 }
 
@@ -715,16 +715,17 @@ hipError_t launch_conv_cl_bwd(const void* x, int dt, int64_t sxb, int64_t sxl, c
 }
 
 hipError_t launch_conv_update(const void* x, int dt, int64_t sxb, void* state, int64_t ssb, int64_t ssc,
-                              const float* w, const float* bias, void* out, int Bn, int C, int Wd, bool silu,
+                              const float* w, const float* bias, void* out, int Bn, int C, int Wd, int SL, bool silu,
                               hipStream_t st) {
+  if (SL < Wd - 1) return hipErrorInvalidValue;
   const int n = Bn * C;
   dim3 grid((n + 255) / 256), block(256);
   if (dt == kBF16) {
     W_SWITCH(Wd, hipLaunchKernelGGL((conv_update_k<bf16_t, WW>), grid, block, 0, st, (const bf16_t*)x, sxb,
-                                    (bf16_t*)state, ssb, ssc, w, bias, (bf16_t*)out, Bn, C, silu));
+                                    (bf16_t*)state, ssb, ssc, w, bias, (bf16_t*)out, Bn, C, SL, silu));
   } else if (dt == kF32) {
     W_SWITCH(Wd, hipLaunchKernelGGL((conv_update_k<float, WW>), grid, block, 0, st, (const float*)x, sxb,
-                                    (float*)state, ssb, ssc, w, bias, (float*)out, Bn, C, silu));
+                                    (float*)state, ssb, ssc, w, bias, (float*)out, Bn, C, SL, silu));
   } else {
     return hipErrorInvalidValue;
   }

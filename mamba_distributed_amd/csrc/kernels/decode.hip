@@ -118,7 +118,7 @@ template <int MB>  // batch-row capacity (1, 4 or 16); the transpose-reduce leav
 __global__ __launch_bounds__(256) void dec_inproj_k(const bf16_t* __restrict__ hn, const bf16_t* __restrict__ W,
                                                     int n_out, int d, int b, float* __restrict__ zxbcdt, int conv_lo,
                                                     int conv_hi, bf16_t* __restrict__ conv_state, int64_t csb,
-                                                    int64_t csc, const float* __restrict__ cw,
+                                                    int64_t csc, int SL, const float* __restrict__ cw,
                                                     const float* __restrict__ cb, int Wd) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* xs = reinterpret_cast<bf16_t*>(smem);  // [b][d]
@@ -150,14 +150,15 @@ __global__ __launch_bounds__(256) void dec_inproj_k(const bf16_t* __restrict__ h
   const int q = idx / MB, r = idx % MB, o = o0 + q;
   if (lane < K1_RPW * MB && r < b && o < n_out) {
     if (o >= conv_lo && o < conv_hi) {
-      // causal conv window: state holds the previous Wd-1 inputs of channel c (oldest first)
+      // causal conv window: the state holds the last SL >= Wd-1 inputs of channel c (oldest first); the
+      // output uses its last Wd-1 entries and v, then the state shifts by one and takes v
       const int c = o - conv_lo;
       bf16_t* st = conv_state + (int64_t)r * csb + (int64_t)c * csc;
       float a = cb ? cb[c] : 0.f;
-      for (int k = 0; k < Wd - 1; ++k) a = fmaf(cw[c * Wd + k], bf2f(st[k]), a);
+      for (int k = 0; k < Wd - 1; ++k) a = fmaf(cw[c * Wd + k], bf2f(st[SL - (Wd - 1) + k]), a);
       a = fmaf(cw[c * Wd + Wd - 1], v, a);
-      for (int k = 0; k + 1 < Wd - 1; ++k) st[k] = st[k + 1];
-      if (Wd > 1) st[Wd - 2] = f2bf(v);
+      for (int k = 0; k + 1 < SL; ++k) st[k] = st[k + 1];
+      if (SL > 0) st[SL - 1] = f2bf(v);
       v = a * sigmoidf_(a);
     }
     zxbcdt[(int64_t)r * n_out + o] = v;
@@ -269,14 +270,14 @@ __global__ __launch_bounds__(256) void dec_outproj_k(const bf16_t* __restrict__ 
 int decode_max_batch() { return DEC_MAXB; }
 
 hipError_t launch_decode_inproj(const void* hn, const void* W, int n_out, int d, int b, float* zxbcdt, int conv_lo,
-                                int conv_hi, void* conv_state, int64_t csb, int64_t csc, const float* cw,
+                                int conv_hi, void* conv_state, int64_t csb, int64_t csc, int SL, const float* cw,
                                 const float* cb, int Wd, hipStream_t st) {
-  if (b < 1 || b > DEC_MAXB || d % 8 || (size_t)b * d * 2 > 65536) return hipErrorInvalidValue;
+  if (b < 1 || b > DEC_MAXB || d % 8 || (size_t)b * d * 2 > 65536 || SL < Wd - 1) return hipErrorInvalidValue;
   const int rows_per_wg = 4 * K1_RPW;
   const dim3 grid((n_out + rows_per_wg - 1) / rows_per_wg);
   const size_t lds = (size_t)b * d * 2;
 #define DEC_K1(MB) hipLaunchKernelGGL(dec_inproj_k<MB>, grid, dim3(256), lds, st, (const bf16_t*)hn, (const bf16_t*)W, \
-                                      n_out, d, b, zxbcdt, conv_lo, conv_hi, (bf16_t*)conv_state, csb, csc, cw, cb, Wd)
+                                      n_out, d, b, zxbcdt, conv_lo, conv_hi, (bf16_t*)conv_state, csb, csc, SL, cw, cb, Wd)
   if (b == 1) DEC_K1(1);
   else if (b <= 4) DEC_K1(4);
   else DEC_K1(16);

@@ -52,8 +52,8 @@ hipError_t launch_conv_cl_bwd(const void* x, int dt, int64_t sxb, int64_t sxl, c
                               float* part, float* dw, float* db, bool pacc, int Bn, int L, int C, int Wd, bool silu,
                               hipStream_t st);
 hipError_t launch_conv_update(const void* x, int dt, int64_t sxb, void* state, int64_t ssb, int64_t ssc,
-                              const float* w, const float* bias, void* out, int Bn, int C, int Wd, bool silu,
-                              hipStream_t st);
+                              const float* w, const float* bias, void* out, int Bn, int C, int Wd, int SL, bool silu,
+                              hipStream_t st);  // state: (Bn, C, SL >= Wd-1), upstream layout SL = Wd
 
 // ---- gemm.hip ---------------------------------------------------------------------------------
 // C[M, N] = A[M, K] . B[N, K]^T, bf16 in/out, fp32 accumulate (K % 64 == 0, N % 8 == 0)
@@ -89,7 +89,7 @@ hipError_t launch_gp_reduce(const float* part, int S, int64_t stride, int64_t n,
 // ---- decode.hip (fused single-token Mamba-2 layer step; buffers preallocated, graph-capturable) --------
 int decode_max_batch();
 hipError_t launch_decode_inproj(const void* hn, const void* W, int n_out, int d, int b, float* zxbcdt, int conv_lo,
-                                int conv_hi, void* conv_state, int64_t csb, int64_t csc, const float* cw,
+                                int conv_hi, void* conv_state, int64_t csb, int64_t csc, int SL, const float* cw,
                                 const float* cb, int Wd, hipStream_t st);
 hipError_t launch_decode_ssm(const float* zxbcdt, int n_out, float* state, const float* A, const float* D,
                              const float* dt_bias, int H, int P, int G, int N, int b, void* g_out, float* part,

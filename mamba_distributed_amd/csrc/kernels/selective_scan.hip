@@ -253,8 +253,8 @@ __global__ __launch_bounds__(256) void selscan_fwd_k(SelScanArgs a) {
 }
 
 // ============================== backward =======================================================
-// A 512-thread workgroup owns SB_KC channels of one batch row and walks the SB_T-step tiles from
-// the last to the first; inside a tile it takes the channels one at a time with all 8 waves:
+// A 256-thread workgroup (SB_W = 4 waves) owns SB_KC channels of one batch row and walks the SB_T-step
+// tiles from the last to the first; inside a tile it takes the channels one at a time with all 4 waves:
 // wave w owns states [w NW, (w+1) NW).  For its states a wave
 //   * replays the forward from the saved tile-start state (DPP prefix scan) keeping h_t,
 //   * runs the adjoint x_t = exp(dt_t A)(dy_t C_t + x_{t+1}) as a DPP suffix scan, whose carry into
@@ -262,7 +262,7 @@ __global__ __launch_bounds__(256) void selscan_fwd_k(SelScanArgs a) {
 //   * accumulates dB[t,n] and dC[t,n] for ITS states over all channels of the group in REGISTERS
 //     (written once per tile as the group's partial; deterministic, no atomics).
 // Sums over n (du, ddelta, y for dz) go through one LDS row per wave and are finished item-parallel
-// (thread = time step, fixed-order sum over the 8 rows, coalesced I/O).
+// (thread = time step, fixed-order sum over the SB_W rows, coalesced I/O).
 template <typename T, int N, bool VEC>
 __global__ __launch_bounds__(256) void selscan_bwd_k(SelScanArgs a) {
   constexpr int NW = N >= SB_W ? N / SB_W : 1;

@@ -126,18 +126,57 @@ class SyntheticTokens:
         self.gen.set_state(s["generator"])
 
 
+def markov_tokens(n: int, vocab_size: int, rng, p_follow: float = 0.75, zipf_a: float = 1.1,
+                  succ: Optional[np.ndarray] = None) -> np.ndarray:
+    """A LEARNABLE synthetic token stream: with probability ``p_follow`` the next token is a fixed
+    successor of the previous one (a random permutation ``succ``), otherwise it is drawn from a Zipf
+    unigram.  A model that learns the unigram and the successor map reaches a loss far below ln(V)
+    (uniform random tokens cannot go below it), so training curves on it show real learning.
+    Generated run-wise (runs of successors have geometric length), vectorised over runs."""
+    if succ is None:
+        succ = rng.permutation(vocab_size)
+    ranks = np.arange(1, vocab_size + 1, dtype=np.float64)
+    pz = ranks ** -zipf_a
+    pz /= pz.sum()
+    zipf_map = rng.permutation(vocab_size)  # which token gets which Zipf rank
+    # run lengths: 1 Zipf draw followed by Geometric(1 - p_follow) - 1 successors
+    lens = rng.geometric(1.0 - p_follow, size=n // max(1, int(1 / (1 - p_follow))) + 16)
+    while lens.sum() < n:
+        lens = np.concatenate([lens, rng.geometric(1.0 - p_follow, size=len(lens))])
+    lens = lens[: np.searchsorted(np.cumsum(lens), n) + 1]
+    starts = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    out = np.empty(int(lens.sum()), dtype=np.int64)
+    cur = zipf_map[rng.choice(vocab_size, size=len(lens), p=pz)]
+    idx = starts.copy()
+    alive = np.arange(len(lens))
+    k = 0
+    while len(alive):
+        out[idx[alive]] = cur[alive]
+        k += 1
+        alive = alive[lens[alive] > k]
+        cur[alive] = succ[cur[alive]]
+        idx[alive] += 1
+    return out[:n]
+
+
 def write_synthetic_shards(root: str, n_train: int = 2, n_val: int = 1, tokens_per_shard: int = 1 << 16,
-                           vocab_size: int = 50304, seed: int = 0, dtype=np.uint16) -> List[str]:
-    """Write edu_fineweb-style ``*_train_XXXXXX.npy`` / ``*_val_XXXXXX.npy`` shards."""
+                           vocab_size: int = 50304, seed: int = 0, dtype=np.uint16,
+                           kind: str = "uniform") -> List[str]:
+    """Write edu_fineweb-style ``*_train_XXXXXX.npy`` / ``*_val_XXXXXX.npy`` shards.
+    kind = "uniform": i.i.d. uniform tokens (throughput runs); "markov": ``markov_tokens`` (learning runs;
+    train and val share the successor map)."""
     os.makedirs(root, exist_ok=True)
     rng = np.random.default_rng(seed)
+    succ = rng.permutation(vocab_size)
     paths = []
     for split, n in (("val", n_val), ("train", n_train)):
         for i in range(n):
             p = os.path.join(root, f"edufineweb_{split}_{i:06d}.npy")
-            np.save(p, rng.integers(0, vocab_size, size=tokens_per_shard, dtype=np.int64).astype(dtype))
+            if kind == "markov":
+                toks = markov_tokens(tokens_per_shard, vocab_size, rng, succ=succ)
+            else:
+                toks = rng.integers(0, vocab_size, size=tokens_per_shard, dtype=np.int64)
+            np.save(p, toks.astype(dtype))
             paths.append(p)
     return paths
 
-
-_ = Optional

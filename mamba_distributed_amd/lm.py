@@ -24,7 +24,6 @@ import inspect
 from typing import Optional
 
 import torch
-import torch.nn.functional as F
 
 from .config import MambaConfig
 from .models.mixer_seq import InferenceParams, MambaLMHeadModel
@@ -158,5 +157,3 @@ class LMHeadModel(MambaLMHeadModel):
             print(f"using fused AdamW: {use_fused}")
         return torch.optim.AdamW(optim_groups, lr=learning_rate, betas=betas, eps=eps, fused=use_fused)
 
-
-_ = F

@@ -7,7 +7,6 @@ supports cached decoding next to the SSM caches.
 """
 from __future__ import annotations
 
-import math
 
 import torch
 import torch.nn as nn
@@ -105,5 +104,3 @@ class MHA(nn.Module):
         o = o.transpose(1, 2).reshape(b, l, hq * hd)
         return self.out_proj(o)
 
-
-_ = math

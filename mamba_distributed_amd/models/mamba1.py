@@ -272,7 +272,8 @@ class Mamba(nn.Module):
         xz3 = _cm(xz, b, l)
         if conv_state is not None:  # prefill: remember the last d_conv-1 inputs for decoding
             x = xz3[:, :self.d_inner]
-            conv_state.copy_(F.pad(x, (max(0, self.d_conv - 1 - l), 0))[..., -(self.d_conv - 1):])
+            sl = conv_state.shape[-1]  # upstream layout: the last d_conv inputs
+            conv_state.copy_(F.pad(x, (max(0, sl - l), 0))[..., -sl:])
             y, last = self._inner_with_state(xz3, A)
             ssm_state.copy_(last)
         else:
@@ -317,7 +318,7 @@ class Mamba(nn.Module):
     def allocate_inference_cache(self, batch_size, max_seqlen, dtype=None, **kwargs):
         device = self.out_proj.weight.device
         conv_dtype = self.conv1d.weight.dtype if dtype is None else dtype
-        conv_state = torch.zeros(batch_size, self.d_inner, self.d_conv - 1, device=device, dtype=conv_dtype)
+        conv_state = torch.zeros(batch_size, self.d_inner, self.d_conv, device=device, dtype=conv_dtype)  # upstream width
         ssm_state = torch.zeros(batch_size, self.d_inner, self.d_state, device=device, dtype=torch.float32)
         return conv_state, ssm_state
 

@@ -113,8 +113,8 @@ class Mamba2(nn.Module):
         di, gn, H = self.d_ssm, self.ngroups * self.d_state, self.nheads
         z, xBC, dt = torch.split(zxbcdt, [di, di + 2 * gn, H], dim=-1)
         xt = xBC.transpose(1, 2)
-        w = self.d_conv
-        conv_state.copy_(F.pad(xt, (max(0, w - 1 - xt.shape[-1]), 0))[..., -(w - 1):])
+        sl = conv_state.shape[-1]  # upstream layout: the last d_conv inputs
+        conv_state.copy_(F.pad(xt, (max(0, sl - xt.shape[-1]), 0))[..., -sl:])
         xBC = causal_conv1d_fn(xt, self.conv1d.weight, self.conv1d.bias, "silu").transpose(1, 2)
         x, Bm, Cm = torch.split(xBC, [di, gn, gn], dim=-1)
         y, last = mamba_chunk_scan_combined(x.unflatten(-1, (H, self.headdim)), dt, A,
@@ -146,7 +146,7 @@ class Mamba2(nn.Module):
     def allocate_inference_cache(self, batch_size, max_seqlen, dtype=None, **kwargs):
         device = self.out_proj.weight.device
         conv_dtype = self.conv1d.weight.dtype if dtype is None else dtype
-        conv_state = torch.zeros(batch_size, self.conv1d.weight.shape[0], self.d_conv - 1, device=device,
+        conv_state = torch.zeros(batch_size, self.conv1d.weight.shape[0], self.d_conv, device=device,
                                  dtype=conv_dtype)
         ssm_state = torch.zeros(batch_size, self.nheads, self.headdim, self.d_state, device=device,
                                 dtype=torch.float32)

@@ -14,7 +14,6 @@ Semantics follow what the reference reaches through its dependencies (SURVEY.md 
 """
 from __future__ import annotations
 
-import math
 from typing import Optional, Tuple
 
 import torch
@@ -111,16 +110,19 @@ def causal_conv1d_ref(
 
 
 def causal_conv1d_update_ref(x, conv_state, weight, bias=None, activation=None):
-    """One decode step.  x: (b, d); conv_state: (b, d, w-1) updated IN PLACE (rolling window)."""
+    """One decode step.  x: (b, d); conv_state: (b, d, state_len >= w-1) updated IN PLACE (causal-conv1d
+    >= 1.4 semantics: the output uses the last w-1 entries and x; the state keeps the last state_len
+    inputs).  Upstream Mamba / Mamba2 caches use state_len = d_conv."""
     dtype = x.dtype
     w = weight.shape[-1]
-    window = torch.cat([_f(conv_state), _f(x).unsqueeze(-1)], dim=-1)  # (b, d, w)
+    full = torch.cat([_f(conv_state), _f(x).unsqueeze(-1)], dim=-1)  # (b, d, state_len + 1)
+    window = full[..., -w:]
     out = (window * _f(weight)).sum(-1)
     if bias is not None:
         out = out + _f(bias)
     if activation in ("silu", "swish"):
         out = F.silu(out)
-    conv_state.copy_(window[..., 1:].to(conv_state.dtype))
+    conv_state.copy_(full[..., 1:].to(conv_state.dtype))
     return out.to(dtype)
 
 
@@ -385,4 +387,3 @@ def softplus_inverse(x: torch.Tensor) -> torch.Tensor:
 
 
 __all__ = [n for n in dir() if n.endswith("_ref")] + ["ssd_dt_transform", "softplus_inverse"]
-_ = math

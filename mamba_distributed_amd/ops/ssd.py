@@ -3,20 +3,24 @@
 Call surface mirrors upstream ``mamba_chunk_scan_combined`` / ``mamba_split_conv1d_scan_combined``
 (SURVEY.md D11/D12, T1-T5, T8); the reference reaches them through ``Mamba2.forward``.
 
-GPU implementation (csrc/kernels/ssd.hip), MI355X-first decomposition:
-  fwd  1. ``ssd_chunk_state``  grid (chunk, head, batch): dt = softplus(dt+bias), in-chunk cumsum of
-          dt*A (wave prefix scan), local chunk state  X^T (w*B)  on MFMA 32x32x16 bf16.
-       2. ``ssd_state_pass``   grid (pn-slice, head, batch): sequential over chunks in fp32 registers,
-          writes the state entering every chunk (bf16) + final state.
-       3. ``ssd_chunk_scan``   grid (chunk, head, batch): CB = C B^T, causal decay mask, y_diag,
-          y_off = e^cum C S_in^T, +D x, all on MFMA, CB tile kept in LDS.
-  bwd  mirrors it: dstate pass (reverse, fp32), chunk-parallel dX/ddt/dcum with head-summed dCB
-       tiles, then one dB/dC GEMM kernel over the head-concatenated K dimension.
+GPU implementation (csrc/kernels/ssd.hip; 64-step chunks on v_mfma_f32_16x16x32_bf16):
+  fwd  1. ``ssd_cumsum``     wave per (b, h, chunk): dt = softplus(dt + bias) (clamped), in-chunk wave64
+          inclusive scan of dt*A.
+       2. ``ssd_fused_fwd``  one workgroup per (h, b) walks the chunks in order with the running state
+          S (P x N) in MFMA accumulators: per chunk y = e^{cum} C S^T + (C B^T o L o dt) x + D x (the
+          masked C B^T accumulator feeds the next MFMA as its operand) and S <- e^{cum_last} S + (w x)^T B;
+          the state entering every chunk is saved (bf16) for the backward.
+  bwd  3. ``ssd_dstate_bwd`` reverse chunk walk per (h, b): dS entering every chunk (bf16), dS_init.
+       4. ``ssd_chunk_bwd``  workgroup per (chunk, head group, b): dM, M, dX, ddt (with the in-chunk
+          reverse cumsum of dcum), dA / dD / dt_bias partial rows; head-summed dCB, dB_off, dC_off stay
+          in registers across the heads of the group.
+       5. ``ssd_dbc_bwd``    workgroup per (chunk, group, b): dC = sum dC_off + dCB B, dB = sum dB_off
+          + dCB^T C.
+  No float atomics: every cross-workgroup sum goes through fixed-order partials (bitwise deterministic).
 CPU: ``reference.ssd_chunked_ref`` under autograd.
 """
 from __future__ import annotations
 
-import math
 from typing import Optional
 
 import torch
@@ -208,5 +212,3 @@ def mamba_split_conv1d_scan_combined(zxbcdt, conv1d_weight, conv1d_bias, dt_bias
         y = F.linear(y, outproj_weight, outproj_bias)
     return y
 
-
-_ = math

@@ -19,12 +19,10 @@ Checkpoint timing follows the reference: ``model_{step}.pt`` is written at the S
 """
 from __future__ import annotations
 
-import contextlib
 import json
-import math
 import os
 import time
-from dataclasses import asdict, dataclass, field
+from dataclasses import dataclass
 from typing import Optional
 
 import torch
@@ -63,7 +61,7 @@ class TrainArgs:
     val_every: int = 250
     val_steps: int = 20
     ckpt_every: int = 1000
-    sample_every: int = 250
+    sample_every: int = 250              # <= 0: never sample
     data_root: str = "edu_fineweb10B"
     synthetic: bool = False
     log_dir: str = "log"
@@ -80,6 +78,8 @@ class TrainArgs:
     sample_prompt: str = "Hello, I'm a language model,"
     device_type: str = "auto"
     tuned_gemms: bool = True             # replay the shipped gfx950 GEMM solution table
+    fp32_matmul_precision: str = "highest"  # reference train.py uses "high" (A100 TF32); gfx950 has no
+                                            # xf32 and the tuned GEMM table needs "highest" (utils/gemm_tuning)
     tp: int = 1                          # tensor parallel degree (Mamba-2 heads; parallel/tensor_parallel.py)
     cp: int = 1                          # context parallel degree (sequence shards; parallel/context_parallel.py)
     sequence_parallel: bool = False      # with tp > 1: shard the residual stream over tokens as well
@@ -129,7 +129,7 @@ class Trainer:
             self.train_loader = DataLoaderLite(a.B, a.T, data_rank, world, "train", self.master, a.data_root)
             self.val_loader = DataLoaderLite(a.B, a.T, data_rank, world, "val", self.master, a.data_root)
         if self.device_type == "cuda":
-            torch.set_float32_matmul_precision("high")
+            torch.set_float32_matmul_precision(a.fp32_matmul_precision)
             if a.tuned_gemms:
                 from .utils.gemm_tuning import enable_tuned_gemms
                 enable_tuned_gemms()
@@ -245,7 +245,11 @@ class Trainer:
         while xgen.size(1) < max_length:
             with self._autocast():
                 logits, _ = self.model(xgen)
-            probs = F.softmax(logits[:, -1, :].float(), dim=-1)
+            last = logits[:, -1, :].float()
+            if not bool(torch.isfinite(last).all()):  # multinomial would hit a device-side assert
+                print(f"rank {self.info.rank} sample: non-finite logits, skipping")
+                return
+            probs = F.softmax(last, dim=-1)
             topk_probs, topk_indices = torch.topk(probs, 50, dim=-1)
             ix = torch.multinomial(topk_probs, 1, generator=sample_rng)
             xgen = torch.cat((xgen, torch.gather(topk_indices, -1, ix)), dim=1)
@@ -331,7 +335,8 @@ class Trainer:
                         f.write(f"{step} val {val_loss:.4f}\n")
                 if step > 0 and (step % a.ckpt_every == 0 or last_step):
                     self.save(step, val_loss)
-            if ((step > 0 and step % a.sample_every == 0) or last_step) and not resumed_here:
+            if (a.sample_every > 0 and ((step > 0 and step % a.sample_every == 0) or last_step)
+                    and not resumed_here):
                 eval_step = True
                 self.sample()
             self._maybe_inject_fault(step)
@@ -364,4 +369,3 @@ class Trainer:
         destroy()
 
 
-_ = (asdict, field, contextlib, math)

@@ -38,6 +38,16 @@ def enable_tuned_gemms(path: Optional[str] = None, tune: bool = False, max_tunin
     path = path or DEFAULT_TABLE
     if not tune and (not os.path.exists(path) or _arch() != "gfx950"):
         return False
+    # The table is keyed by GEMM signatures recorded at the default fp32 matmul precision.  With
+    # torch.set_float32_matmul_precision("high") (the reference's A100/TF32 setting) the replayed
+    # solutions compute garbage on ROCm 7 / gfx950 (measured: a 280M forward collapses to loss = ln V and
+    # the first backward is NaN; the same run without the table, or at "highest", trains).  gfx950 has no
+    # xf32 MFMA, so "high" buys nothing: replay always runs at "highest".
+    if torch.get_float32_matmul_precision() != "highest":
+        import warnings
+        warnings.warn("enable_tuned_gemms: forcing torch.set_float32_matmul_precision('highest') "
+                      "(the gfx950 solution table is only valid there; gfx950 has no TF32/xf32 mode)")
+        torch.set_float32_matmul_precision("highest")
     tunable = torch.cuda.tunable
     tunable.enable(True)
     tunable.set_filename(path)

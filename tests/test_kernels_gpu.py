@@ -701,3 +701,51 @@ def test_gemm_wgrad_channel_major_x(cuda, dy_cm, x_cm, P, M, Q):
     _ext.ops().gemm_wgrad_cm(dY_arg, X_arg, out, True, dy_cm, x_cm)
     ref = dY.float() @ X.float().t() + base
     assert rel(out, ref) < 2e-3, rel(out, ref)
+
+
+@pytest.mark.parametrize("sl_extra", [-1, 0, 3])
+def test_conv_update_native_state_len(cuda, sl_extra):
+    """Native conv1d_update with the upstream cache width (state_len = d_conv) and others vs the fp64
+    reference: outputs and the rolled state."""
+    from mamba_distributed_amd.ops import _ext
+    from mamba_distributed_amd.ops.reference import causal_conv1d_update_ref
+    torch.manual_seed(0)
+    b, d, w = 3, 1792, 4
+    sl = w + sl_extra
+    st0 = torch.randn(b, d, sl, device=cuda).to(torch.bfloat16)
+    wt = torch.randn(d, w, device=cuda) * 0.3
+    bias = torch.randn(d, device=cuda)
+    sn, sr = st0.clone(), st0.double()
+    for t in range(5):
+        x = torch.randn(b, d, device=cuda).to(torch.bfloat16)
+        on = _ext.ops().conv1d_update(x, sn, wt, bias, True)
+        orf = causal_conv1d_update_ref(x.double(), sr, wt.double(), bias.double(), "silu")
+        assert rel(on, orf) < 1e-2, (t, rel(on, orf))
+        sr.copy_(sr.to(torch.bfloat16).double())  # the native state is bf16
+        assert torch.equal(sn, sr.to(torch.bfloat16)), t
+
+
+def test_tuned_gemm_table_forces_highest_precision(cuda):
+    """Regression: replaying the gfx950 TunableOp table under torch.set_float32_matmul_precision("high")
+    (the reference's setting) produced garbage projections (280M forward at loss = ln V, NaN backward).
+    enable_tuned_gemms must force "highest", and a 280M-shaped block must match the untuned forward."""
+    from mamba_distributed_amd import LMHeadModel, MambaConfig
+    from mamba_distributed_amd.utils import gemm_tuning
+    prev = torch.get_float32_matmul_precision()
+    try:
+        torch.set_float32_matmul_precision("high")
+        with pytest.warns(UserWarning):
+            on = gemm_tuning.enable_tuned_gemms()
+        assert torch.get_float32_matmul_precision() == "highest"
+        torch.manual_seed(0)
+        m = LMHeadModel(MambaConfig(d_model=768, n_layer=1, vocab_size=50304, ssm_cfg={"layer": "Mamba2"}),
+                        device=cuda)
+        ids = torch.randint(0, 50304, (32, 1025), device=cuda)
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+            _, l_tuned = m(ids[:, :-1], ids[:, 1:], return_logits=False)
+            torch.cuda.tunable.enable(False)
+            _, l_plain = m(ids[:, :-1], ids[:, 1:], return_logits=False)
+        assert torch.isfinite(l_tuned) and abs(l_tuned.item() - l_plain.item()) < 1e-2, (l_tuned, l_plain, on)
+    finally:
+        torch.cuda.tunable.enable(False)
+        torch.set_float32_matmul_precision(prev)

@@ -138,3 +138,22 @@ def test_mamba1_mixer_matches_transformers_oracle():
     out = hf.eval()(u)
     out = out[0] if isinstance(out, tuple) else out
     torch.testing.assert_close(ours(u), out, rtol=1e-7, atol=1e-8)
+
+
+@pytest.mark.parametrize("extra", [-1, 0, 2])
+def test_conv_update_state_len_semantics(extra):
+    """causal-conv1d >= 1.4 update semantics for any state_len >= w-1 (upstream Mamba / Mamba2 caches use
+    state_len = d_conv): stepping token by token reproduces the full causal conv, and the state holds the
+    last state_len inputs (zero-padded at the start)."""
+    from mamba_distributed_amd.ops.reference import causal_conv1d_ref, causal_conv1d_update_ref
+    torch.manual_seed(0)
+    b, d, L, w = 2, 5, 9, 4
+    sl = w + extra
+    x = torch.randn(b, d, L, dtype=torch.float64)
+    wt = torch.randn(d, w, dtype=torch.float64)
+    bias = torch.randn(d, dtype=torch.float64)
+    full = causal_conv1d_ref(x, wt, bias, "silu")
+    state = torch.zeros(b, d, sl, dtype=torch.float64)
+    outs = [causal_conv1d_update_ref(x[..., t], state, wt, bias, "silu") for t in range(L)]
+    torch.testing.assert_close(torch.stack(outs, -1), full)
+    torch.testing.assert_close(state, x[..., L - sl:])
