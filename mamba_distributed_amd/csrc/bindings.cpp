@@ -96,6 +96,7 @@ int64_t part_rows(std::string kind, int64_t a, int64_t b) {
   if (kind == "add_rmsnorm") return mamba_amd::add_rmsnorm_bwd_partial_rows(a);
   if (kind == "gated_rmsnorm") return mamba_amd::norm_bwd_partial_rows(a);
   if (kind == "conv_cl") return mamba_amd::conv_cl_bwd_partial_rows((int)a, (int)b);
+  if (kind == "conv_cl_var") return mamba_amd::conv_cl_var_partial_rows((int)a, (int)b);
   TORCH_CHECK(false, "part_rows: unknown kind ", kind);
 }
 
@@ -290,6 +291,82 @@ std::tuple<Tensor, Tensor, Tensor> conv1d_cl_bwd(Tensor x, Tensor weight, option
   return {dx, dwb.narrow(1, 0, W), dwb.select(1, W)};
 }
 
+// varlen / state hand-off conv (kernels/conv1d.hip ConvVarArgs), channel-last x (b, l, c):
+// seq_idx (b, l) int, initial_states (b, c, W-1), final states returned when want_final.
+static void conv_var_common(mamba_amd::ConvVarArgs& a, const Tensor& x, const Tensor& w, const Tensor& bb,
+                            const optional<Tensor>& seq_idx, const optional<Tensor>& init, Tensor& sq, Tensor& ini) {
+  TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1, "x must be (b, l, c) with unit channel stride");
+  a.Bn = (int)x.size(0); a.L = (int)x.size(1); a.C = (int)x.size(2); a.Wd = (int)w.size(1);
+  TORCH_CHECK(w.dim() == 2 && w.size(0) == a.C && a.Wd >= 2 && a.Wd <= 4, "weight must be (c, w), 2<=w<=4");
+  a.dt = dcode(x.scalar_type());
+  a.x = x.data_ptr(); a.sxb = x.stride(0); a.sxl = x.stride(1);
+  a.w = w.data_ptr<float>(); a.bias = fptr(bb);
+  if (seq_idx.has_value() && seq_idx->defined()) {
+    sq = seq_idx->to(at::kInt).contiguous();
+    TORCH_CHECK(sq.dim() == 2 && sq.size(0) == a.Bn && sq.size(1) == a.L, "seq_idx must be (b, l)");
+    a.seq = sq.data_ptr<int>(); a.sqb = sq.stride(0);
+  }
+  if (init.has_value() && init->defined()) {
+    ini = *init;
+    if (ini.stride(2) != 1) ini = ini.contiguous();
+    TORCH_CHECK(ini.dim() == 3 && ini.size(0) == a.Bn && ini.size(1) == a.C && ini.size(2) == a.Wd - 1 &&
+                ini.scalar_type() == x.scalar_type(), "initial_states must be (b, c, w-1), x's dtype");
+    a.init = ini.data_ptr(); a.sib = ini.stride(0); a.sic = ini.stride(1);
+  }
+}
+
+std::tuple<Tensor, Tensor> conv1d_cl_var_fwd(Tensor x, Tensor weight, optional<Tensor> bias, bool silu,
+                                            optional<Tensor> seq_idx, optional<Tensor> initial_states, bool want_final) {
+  check_cuda(x, "x");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  mamba_amd::ConvVarArgs a{};
+  Tensor w = f32c(weight), bb = f32c_opt(bias), sq, ini;
+  conv_var_common(a, x, w, bb, seq_idx, initial_states, sq, ini);
+  auto out = at::empty({a.Bn, a.L, a.C}, x.options());
+  a.out = out.data_ptr(); a.sob = out.stride(0); a.sol = out.stride(1);
+  Tensor fin = want_final ? at::empty({a.Bn, a.C, a.Wd - 1}, x.options()) : at::empty({0}, x.options());
+  if (want_final) { a.fin = fin.data_ptr(); a.sfb = fin.stride(0); a.sfc = fin.stride(1); }
+  a.silu = silu; a.backward = false;
+  HIPCHK(mamba_amd::launch_conv_cl_var(a, cur_stream()));
+  return {out, fin};
+}
+
+std::tuple<Tensor, Tensor, Tensor, Tensor> conv1d_cl_var_bwd(Tensor x, Tensor weight, optional<Tensor> bias,
+                                                             Tensor dout, bool silu, optional<Tensor> seq_idx,
+                                                             optional<Tensor> initial_states, optional<Tensor> dfinal,
+                                                             optional<Tensor> dx_out, optional<Tensor> part_buf,
+                                                             int64_t part_mode_) {
+  check_cuda(x, "x");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  mamba_amd::ConvVarArgs a{};
+  Tensor w = f32c(weight), bb = f32c_opt(bias), sq, ini;
+  conv_var_common(a, x, w, bb, seq_idx, initial_states, sq, ini);
+  if (dout.stride(2) != 1) dout = dout.contiguous();
+  TORCH_CHECK(dout.sizes() == x.sizes() && dout.scalar_type() == x.scalar_type(), "dout mismatch");
+  a.g = dout.data_ptr(); a.sgb = dout.stride(0); a.sgl = dout.stride(1);
+  Tensor dfin;
+  if (dfinal.has_value() && dfinal->defined()) {
+    dfin = dfinal->to(x.scalar_type());
+    if (dfin.stride(2) != 1) dfin = dfin.contiguous();
+    TORCH_CHECK(dfin.dim() == 3 && dfin.size(0) == a.Bn && dfin.size(1) == a.C && dfin.size(2) == a.Wd - 1,
+                "dfinal must be (b, c, w-1)");
+    a.dfin = dfin.data_ptr(); a.sdfb = dfin.stride(0); a.sdfc = dfin.stride(1);
+  }
+  Tensor dx = dx_out.has_value() && dx_out->defined() ? *dx_out : at::empty({a.Bn, a.L, a.C}, x.options());
+  TORCH_CHECK(dx.sizes() == x.sizes() && dx.stride(2) == 1 && dx.scalar_type() == x.scalar_type(), "dx_out layout");
+  a.dx = dx.data_ptr(); a.sdb = dx.stride(0); a.sdl = dx.stride(1);
+  Tensor dinit = a.init ? at::empty({a.Bn, a.C, a.Wd - 1}, x.options()) : at::empty({0}, x.options());
+  if (a.init) { a.dinit = dinit.data_ptr(); a.sdib = dinit.stride(0); a.sdic = dinit.stride(1); }
+  const PartMode pm = part_mode(part_mode_);
+  Tensor part = part_tensor(part_buf, part_mode_, {mamba_amd::conv_cl_var_partial_rows(a.Bn, a.L), a.C, a.Wd + 1},
+                            x.options());
+  auto dwb = at::empty({pm.reduce ? a.C : 0, a.Wd + 1}, x.options().dtype(at::kFloat));
+  a.part = part.data_ptr<float>(); a.dw = pm.reduce ? dwb.data_ptr<float>() : nullptr; a.pacc = pm.pacc;
+  a.silu = silu; a.backward = true;
+  HIPCHK(mamba_amd::launch_conv_cl_var(a, cur_stream()));
+  return {dx, dwb.narrow(1, 0, a.Wd), dwb.select(1, a.Wd), dinit};
+}
+
 Tensor conv1d_update(Tensor x, Tensor conv_state, Tensor weight, optional<Tensor> bias, bool silu) {
   check_cuda(x, "x");
   at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
@@ -355,7 +432,8 @@ void ssd_common(mamba_amd::SSDArgs& a, const Tensor& x, const Tensor& dt, const 
 std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> ssd_fwd(Tensor x, Tensor dt, Tensor A, Tensor Bm, Tensor Cm,
                                                            optional<Tensor> D, optional<Tensor> dt_bias,
                                                            optional<Tensor> init, int64_t chunk, bool softplus,
-                                                           double dt_min, double dt_max, bool A_is_log) {
+                                                           double dt_min, double dt_max, bool A_is_log,
+                                                           optional<Tensor> seq_idx) {
   check_cuda(x, "x");
   at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   mamba_amd::SSDArgs a{};
@@ -366,6 +444,12 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> ssd_fwd(Tensor x, Tensor dt, 
   if (bf.defined()) TORCH_CHECK(bf.numel() == a.H, "dt_bias must be (h,)");
   if (If.defined()) TORCH_CHECK(If.numel() == (int64_t)a.B * a.H * 64 * a.N, "initial_states must be (b,h,p,n)");
   a.A = Af.data_ptr<float>(); a.D = fptr(Df); a.dt_bias = fptr(bf); a.init = fptr(If);
+  Tensor sq;
+  if (seq_idx.has_value() && seq_idx->defined()) {
+    sq = seq_idx->to(at::kInt);
+    TORCH_CHECK(sq.dim() == 2 && sq.size(0) == a.B && sq.size(1) == a.L && sq.is_cuda(), "seq_idx must be (b, l)");
+    a.seq = sq.data_ptr<int>(); a.sqb = sq.stride(0); a.sql = sq.stride(1);
+  }
   auto fo = x.options().dtype(at::kFloat);
   auto dtp = at::empty({a.B, a.H, a.Lp}, fo);
   auto cum = at::empty({a.B, a.H, a.Lp}, fo);
@@ -841,9 +925,15 @@ TORCH_LIBRARY(mamba_amd, m) {
   m.def("conv1d_cl_fwd(Tensor x, Tensor weight, Tensor? bias, bool silu) -> Tensor");
   m.def("conv1d_cl_bwd(Tensor x, Tensor weight, Tensor? bias, Tensor dout, bool silu, Tensor(a!)? dx_out, "
         "Tensor(z!)? part_buf=None, int part_mode=0) -> (Tensor, Tensor, Tensor)");
+  m.def("conv1d_cl_var_fwd(Tensor x, Tensor weight, Tensor? bias, bool silu, Tensor? seq_idx, "
+        "Tensor? initial_states, bool want_final) -> (Tensor, Tensor)");
+  m.def("conv1d_cl_var_bwd(Tensor x, Tensor weight, Tensor? bias, Tensor dout, bool silu, Tensor? seq_idx, "
+        "Tensor? initial_states, Tensor? dfinal, Tensor(a!)? dx_out, Tensor(z!)? part_buf=None, int part_mode=0) "
+        "-> (Tensor, Tensor, Tensor, Tensor)");
   m.def("conv1d_update(Tensor x, Tensor(a!) conv_state, Tensor weight, Tensor? bias, bool silu) -> Tensor");
   m.def("ssd_fwd(Tensor x, Tensor dt, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? dt_bias, Tensor? init, "
-        "int chunk, bool softplus, float dt_min, float dt_max, bool A_is_log=False) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
+        "int chunk, bool softplus, float dt_min, float dt_max, bool A_is_log=False, Tensor? seq_idx=None) "
+        "-> (Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("ssd_bwd(Tensor dy, Tensor x, Tensor dt, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? dt_bias, "
         "Tensor? init, Tensor cum, Tensor dtp, Tensor states, Tensor? dfinal, int chunk, bool softplus, float dt_min, "
         "float dt_max, Tensor(a!)? dx_out, Tensor(b!)? ddt_out, Tensor(c!)? dB_out, Tensor(d!)? dC_out, "
@@ -891,6 +981,8 @@ TORCH_LIBRARY_IMPL(mamba_amd, CUDA, m) {
   m.impl("conv1d_cl_fwd", &conv1d_cl_fwd);
   m.impl("conv1d_cl_bwd", &conv1d_cl_bwd);
   m.impl("conv1d_update", &conv1d_update);
+  m.impl("conv1d_cl_var_fwd", &conv1d_cl_var_fwd);
+  m.impl("conv1d_cl_var_bwd", &conv1d_cl_var_bwd);
   m.impl("ssd_fwd", &ssd_fwd);
   m.impl("ssd_bwd", &ssd_bwd);
   m.impl("selscan_fwd", &selscan_fwd);

@@ -553,6 +553,148 @@ __global__ __launch_bounds__(256) void conv_cl_bwd_bf16_k(const bf16_t* __restri
   }
 }
 
+// =========================== varlen / state hand-off (channel-last) =========================
+// causal-conv1d >= 1.4 interface: seq_idx (b, l) int32 -- a tap never reads a token of another
+// sequence; initial_states (b, c, W-1) -- the inputs before t = 0; final_states (b, c, W-1) -- the last
+// W-1 inputs (for decode or the next context-parallel shard).  Used only when one of them is given (the
+// dense kernels above stay the hot path): thread = one channel, wave = CV_T steps, fp32 math.
+constexpr int CV_T = 16;
+
+template <typename T, int W>
+struct VarIO {
+  const T* x; int64_t sxb, sxl;
+  const int* seq; int64_t sqb;
+  const T* init; int64_t sib, sic;
+  int b, c, L;
+  __device__ __forceinline__ int sq(int t) const { return seq ? seq[b * sqb + t] : 0; }
+  // input at time s as seen by an output of sequence sqt (s < 0: initial state slot W-1+s)
+  __device__ __forceinline__ float in(int s, int sqt) const {
+    // the initial states precede the first sequence of the row only
+    if (s < 0) return init && (!seq || seq[b * sqb] == sqt) ? ld(init + b * sib + (int64_t)c * sic + (W - 1) + s) : 0.f;
+    if (seq && seq[b * sqb + s] != sqt) return 0.f;
+    return ld(x + b * sxb + (int64_t)s * sxl + c);
+  }
+};
+
+template <typename T, int W>
+__global__ __launch_bounds__(256) void conv_cl_fwd_var_k(VarIO<T, W> io, const float* __restrict__ w,
+                                                         const float* __restrict__ bias, T* __restrict__ out,
+                                                         int64_t sob, int64_t sol, T* __restrict__ fin, int64_t sfb,
+                                                         int64_t sfc, int C, bool silu) {
+  io.c = blockIdx.x * 64 + (threadIdx.x & 63);
+  io.b = blockIdx.z;
+  const int t0 = (blockIdx.y * 4 + (threadIdx.x >> 6)) * CV_T;
+  if (io.c >= C) return;
+  float wk[W];
+#pragma unroll
+  for (int k = 0; k < W; ++k) wk[k] = w[io.c * W + k];
+  const float bs = bias ? bias[io.c] : 0.f;
+  for (int t = t0; t < min(t0 + CV_T, io.L); ++t) {
+    const int sqt = io.sq(t);
+    float a = bs;
+#pragma unroll
+    for (int k = 0; k < W; ++k) a += wk[k] * io.in(t - (W - 1) + k, sqt);
+    st(out + io.b * sob + (int64_t)t * sol + io.c, act_fwd(a, silu));
+  }
+  if (fin && t0 == 0) {  // the last W-1 inputs, initial states in front when L < W-1
+#pragma unroll
+    for (int j = 0; j < W - 1; ++j) {
+      const int s = io.L - (W - 1) + j;
+      const float v = s >= 0 ? ld(io.x + io.b * io.sxb + (int64_t)s * io.sxl + io.c) : io.in(s, io.sq(0));
+      st(fin + io.b * sfb + (int64_t)io.c * sfc + j, v);
+    }
+  }
+}
+
+// dx, d(initial_states), per-block (W taps + bias) partial rows; dfin: gradient of final_states (or null)
+template <typename T, int W>
+__global__ __launch_bounds__(256) void conv_cl_bwd_var_k(VarIO<T, W> io, const float* __restrict__ w,
+                                                         const float* __restrict__ bias, const T* __restrict__ g,
+                                                         int64_t sgb, int64_t sgl, const T* __restrict__ dfin,
+                                                         int64_t sdfb, int64_t sdfc, T* __restrict__ dx, int64_t sdb,
+                                                         int64_t sdl, T* __restrict__ dinit, int64_t sdib,
+                                                         int64_t sdic, float* __restrict__ part, bool pacc, int C,
+                                                         bool silu) {
+  __shared__ float red[4][64][W + 1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  io.c = blockIdx.x * 64 + lane;
+  io.b = blockIdx.z;
+  const int t0 = (blockIdx.y * 4 + wave) * CV_T;
+  const bool on = io.c < C;
+  float accw[W + 1];
+#pragma unroll
+  for (int k = 0; k < W + 1; ++k) accw[k] = 0.f;
+  if (on) {
+    float wk[W];
+#pragma unroll
+    for (int k = 0; k < W; ++k) wk[k] = w[io.c * W + k];
+    const float bs = bias ? bias[io.c] : 0.f;
+    // g'(t) = dout(t) act'(pre(t)) for the outputs this tile's inputs feed: t in [t0, t0 + CV_T + W - 1)
+    auto gp = [&](int t) -> float {
+      if (t < 0 || t >= io.L) return 0.f;
+      const int sqt = io.sq(t);
+      float a = bs;
+#pragma unroll
+      for (int k = 0; k < W; ++k) a += wk[k] * io.in(t - (W - 1) + k, sqt);
+      return act_bwd(a, ld(g + io.b * sgb + (int64_t)t * sgl + io.c), silu);
+    };
+    float gw[CV_T + W - 1];
+#pragma unroll
+    for (int i = 0; i < CV_T + W - 1; ++i) gw[i] = gp(t0 + i);
+    // weight / bias partials over this tile's outputs
+#pragma unroll
+    for (int i = 0; i < CV_T; ++i) {
+      const int t = t0 + i;
+      if (t < io.L) {
+        const int sqt = io.sq(t);
+#pragma unroll
+        for (int k = 0; k < W; ++k) accw[k] += gw[i] * io.in(t - (W - 1) + k, sqt);
+        accw[W] += gw[i];
+      }
+    }
+    // dx(s) = sum_k w_k g'(s + W-1-k) [same sequence]  (+ d final_states for the last W-1 inputs)
+    for (int i = 0; i < CV_T && t0 + i < io.L; ++i) {
+      const int s = t0 + i, sqs = io.sq(s);
+      float d = 0.f;
+#pragma unroll
+      for (int k = 0; k < W; ++k) {
+        const int t = s + (W - 1) - k;
+        if (t < io.L && (!io.seq || io.sq(t) == sqs)) d += wk[k] * gw[i + (W - 1) - k];
+      }
+      const int j = s - (io.L - (W - 1));
+      if (dfin && j >= 0) d += ld(dfin + io.b * sdfb + (int64_t)io.c * sdfc + j);
+      st(dx + io.b * sdb + (int64_t)s * sdl + io.c, d);
+    }
+    if (dinit && t0 == 0) {  // initial-state slot j = W-1+s (s < 0) feeds output t = s + (W-1) - k
+#pragma unroll
+      for (int j = 0; j < W - 1; ++j) {
+        const int s = j - (W - 1);
+        float d = 0.f;
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+          const int t = s + (W - 1) - k;
+          if (t >= 0 && t < io.L && (!io.seq || io.sq(t) == io.sq(0))) d += wk[k] * gp(t);
+        }
+        const int jf = s - (io.L - (W - 1));  // final_states may reach back into the initial states
+        if (dfin && jf >= 0) d += ld(dfin + io.b * sdfb + (int64_t)io.c * sdfc + jf);
+        st(dinit + io.b * sdib + (int64_t)io.c * sdic + j, d);
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < W + 1; ++k) red[wave][lane][k] = accw[k];
+  __syncthreads();
+  const int64_t prow = (int64_t)blockIdx.z * gridDim.y + blockIdx.y;
+  for (int i = threadIdx.x; i < 64 * (W + 1); i += 256) {
+    const int ch = blockIdx.x * 64 + i / (W + 1), k = i % (W + 1);
+    if (ch < C) {
+      float* pp = part + prow * (int64_t)C * (W + 1) + (int64_t)ch * (W + 1) + k;
+      const float v = red[0][i / (W + 1)][k] + red[1][i / (W + 1)][k] + red[2][i / (W + 1)][k] + red[3][i / (W + 1)][k];
+      *pp = pacc ? *pp + v : v;
+    }
+  }
+}
+
 // =========================== decode update ===============================================
 template <typename T, int W>
 __global__ void conv_update_k(const T* __restrict__ x, int64_t sxb, T* __restrict__ state, int64_t ssb,
@@ -730,6 +872,45 @@ hipError_t launch_conv_update(const void* x, int dt, int64_t sxb, void* state, i
     return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+int conv_cl_var_partial_rows(int Bn, int L) { return Bn * ((L + 4 * CV_T - 1) / (4 * CV_T)); }
+
+template <typename T>
+static hipError_t cl_var(const T* x, int64_t sxb, int64_t sxl, const int* seq, int64_t sqb, const T* init,
+                         int64_t sib, int64_t sic, const float* w, const float* bias, T* out, int64_t sob, int64_t sol,
+                         T* fin, int64_t sfb, int64_t sfc, const T* g, int64_t sgb, int64_t sgl, const T* dfin,
+                         int64_t sdfb, int64_t sdfc, T* dx, int64_t sdb, int64_t sdl, T* dinit, int64_t sdib,
+                         int64_t sdic, float* part, float* dw, bool pacc, int Bn, int L, int C, int Wd, bool silu,
+                         bool backward, hipStream_t st) {
+  dim3 grid((C + 63) / 64, (L + 4 * CV_T - 1) / (4 * CV_T), Bn), block(256);
+  W_SWITCH(Wd, {
+    VarIO<T, WW> io{x, sxb, sxl, seq, sqb, init, sib, sic, 0, 0, L};
+    if (!backward)
+      hipLaunchKernelGGL((conv_cl_fwd_var_k<T, WW>), grid, block, 0, st, io, w, bias, out, sob, sol, fin, sfb, sfc, C,
+                         silu);
+    else
+      hipLaunchKernelGGL((conv_cl_bwd_var_k<T, WW>), grid, block, 0, st, io, w, bias, g, sgb, sgl, dfin, sdfb, sdfc,
+                         dx, sdb, sdl, dinit, sdib, sdic, part, pacc, C, silu);
+  });
+  MAMBA_HIP_CHECK(hipGetLastError());
+  if (backward && dw) return launch_colsum(part, conv_cl_var_partial_rows(Bn, L), C * (Wd + 1), dw, st);
+  return hipSuccess;
+}
+
+hipError_t launch_conv_cl_var(const ConvVarArgs& a, hipStream_t st) {
+  if (a.dt == kBF16)
+    return cl_var<bf16_t>((const bf16_t*)a.x, a.sxb, a.sxl, a.seq, a.sqb, (const bf16_t*)a.init, a.sib, a.sic, a.w,
+                          a.bias, (bf16_t*)a.out, a.sob, a.sol, (bf16_t*)a.fin, a.sfb, a.sfc, (const bf16_t*)a.g,
+                          a.sgb, a.sgl, (const bf16_t*)a.dfin, a.sdfb, a.sdfc, (bf16_t*)a.dx, a.sdb, a.sdl,
+                          (bf16_t*)a.dinit, a.sdib, a.sdic, a.part, a.dw, a.pacc, a.Bn, a.L, a.C, a.Wd, a.silu,
+                          a.backward, st);
+  if (a.dt == kF32)
+    return cl_var<float>((const float*)a.x, a.sxb, a.sxl, a.seq, a.sqb, (const float*)a.init, a.sib, a.sic, a.w,
+                         a.bias, (float*)a.out, a.sob, a.sol, (float*)a.fin, a.sfb, a.sfc, (const float*)a.g, a.sgb,
+                         a.sgl, (const float*)a.dfin, a.sdfb, a.sdfc, (float*)a.dx, a.sdb, a.sdl, (float*)a.dinit,
+                         a.sdib, a.sdic, a.part, a.dw, a.pacc, a.Bn, a.L, a.C, a.Wd, a.silu, a.backward, st);
+  return hipErrorInvalidValue;
 }
 
 }  // namespace mamba_amd

@@ -55,6 +55,26 @@ hipError_t launch_conv_update(const void* x, int dt, int64_t sxb, void* state, i
                               const float* w, const float* bias, void* out, int Bn, int C, int Wd, int SL, bool silu,
                               hipStream_t st);  // state: (Bn, C, SL >= Wd-1), upstream layout SL = Wd
 
+// varlen / state hand-off channel-last conv (seq_idx, initial_states, final_states), fwd or bwd
+struct ConvVarArgs {
+  int dt;                                   // dtype of x / out / g / dx / states
+  const void* x; int64_t sxb, sxl;          // (b, l, c), unit channel stride
+  const int* seq; int64_t sqb;              // (b, l) int32, unit time stride; null = one sequence per row
+  const void* init; int64_t sib, sic;       // (b, c, W-1), unit last stride; null = zeros
+  const float* w; const float* bias;        // (c, W) fp32, (c) or null
+  void* out; int64_t sob, sol;              // fwd output
+  void* fin; int64_t sfb, sfc;              // fwd: (b, c, W-1) final states or null
+  const void* g; int64_t sgb, sgl;          // bwd: d out
+  const void* dfin; int64_t sdfb, sdfc;     // bwd: d final_states or null
+  void* dx; int64_t sdb, sdl;               // bwd: d x
+  void* dinit; int64_t sdib, sdic;          // bwd: d initial_states or null
+  float* part; float* dw; bool pacc;        // bwd: partial rows (conv_cl_var_partial_rows, c, W+1), dw (c, W+1) or null
+  int Bn, L, C, Wd;
+  bool silu, backward;
+};
+int conv_cl_var_partial_rows(int Bn, int L);
+hipError_t launch_conv_cl_var(const ConvVarArgs& a, hipStream_t st);
+
 // ---- gemm.hip ---------------------------------------------------------------------------------
 // C[M, N] = A[M, K] . B[N, K]^T, bf16 in/out, fp32 accumulate (K % 64 == 0, N % 8 == 0)
 bool gemm_tn_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc);

@@ -17,6 +17,7 @@ struct SSDArgs {
   bool a_log;                 // A holds A_log: kernels use A = -exp(A_log), dA partials become dA_log
   int psl;                    // row stride of the (b*nc, 3, H) small-partials block (= 3H)
   bool pacc;                  // add into the small partials (deferred reduction across micro-steps)
+  const int* seq; int64_t sqb, sql;  // seq_idx (b, l) int32 or null: packed variable-length sequences
   const float* init;      // (b, h, p, n) or null
   // forward outputs / saved
   float* dtp; float* cum; // (b, h, Lp)

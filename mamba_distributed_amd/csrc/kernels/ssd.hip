@@ -27,6 +27,7 @@ namespace mamba_amd {
 constexpr int Q = 64;
 constexpr int P = 64;
 constexpr int LD64 = 80;  // padded LDS row (elements) for 64-wide bf16 tiles: conflict-free b128 / tr_perm fragment reads
+constexpr float kSeqBreak = -256.f;  // e^{-256 + O(10)} == 0 in fp32
 
 __device__ __forceinline__ float ld_any(const void* p, int dt, int64_t i) {
   return dt == kF32 ? reinterpret_cast<const float*>(p)[i] : bf2f(reinterpret_cast<const bf16_t*>(p)[i]);
@@ -63,6 +64,13 @@ __global__ __launch_bounds__(256) void ssd_cumsum_k(SSDArgs a) {
     v = fminf(fmaxf(v, a.dt_min), a.dt_max);
   }
   float x = v * (a.a_log ? -__expf(a.A[h]) : a.A[h]);
+  // seq_idx: a sequence start is a decay to zero.  Adding kSeqBreak to the in-chunk cumsum makes every
+  // e^{cum_i - cum_j} across the break (intra-chunk L, the decay of the carried state, the state inputs
+  // of earlier tokens) underflow to exactly 0 in fp32, i.e. upstream's seq_idx masks, with no change to
+  // any other term or to the backward (the offset is a constant: d cum / d dt is unchanged).
+  if (a.seq && t > 0 && t < a.L &&
+      a.seq[(int64_t)b * a.sqb + (int64_t)t * a.sql] != a.seq[(int64_t)b * a.sqb + (int64_t)(t - 1) * a.sql])
+    x += kSeqBreak;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
     const float y = __shfl_up(x, off, 64);

@@ -127,7 +127,7 @@ class SyntheticTokens:
 
 
 def markov_tokens(n: int, vocab_size: int, rng, p_follow: float = 0.75, zipf_a: float = 1.1,
-                  succ: Optional[np.ndarray] = None) -> np.ndarray:
+                  succ: Optional[np.ndarray] = None, zipf_map: Optional[np.ndarray] = None) -> np.ndarray:
     """A LEARNABLE synthetic token stream: with probability ``p_follow`` the next token is a fixed
     successor of the previous one (a random permutation ``succ``), otherwise it is drawn from a Zipf
     unigram.  A model that learns the unigram and the successor map reaches a loss far below ln(V)
@@ -138,7 +138,8 @@ def markov_tokens(n: int, vocab_size: int, rng, p_follow: float = 0.75, zipf_a: 
     ranks = np.arange(1, vocab_size + 1, dtype=np.float64)
     pz = ranks ** -zipf_a
     pz /= pz.sum()
-    zipf_map = rng.permutation(vocab_size)  # which token gets which Zipf rank
+    if zipf_map is None:
+        zipf_map = rng.permutation(vocab_size)  # which token gets which Zipf rank
     # run lengths: 1 Zipf draw followed by Geometric(1 - p_follow) - 1 successors
     lens = rng.geometric(1.0 - p_follow, size=n // max(1, int(1 / (1 - p_follow))) + 16)
     while lens.sum() < n:
@@ -164,16 +165,17 @@ def write_synthetic_shards(root: str, n_train: int = 2, n_val: int = 1, tokens_p
                            kind: str = "uniform") -> List[str]:
     """Write edu_fineweb-style ``*_train_XXXXXX.npy`` / ``*_val_XXXXXX.npy`` shards.
     kind = "uniform": i.i.d. uniform tokens (throughput runs); "markov": ``markov_tokens`` (learning runs;
-    train and val share the successor map)."""
+    every train and val shard shares the successor map and the unigram, i.e. one stationary source)."""
     os.makedirs(root, exist_ok=True)
     rng = np.random.default_rng(seed)
     succ = rng.permutation(vocab_size)
+    zipf_map = rng.permutation(vocab_size)
     paths = []
     for split, n in (("val", n_val), ("train", n_train)):
         for i in range(n):
             p = os.path.join(root, f"edufineweb_{split}_{i:06d}.npy")
             if kind == "markov":
-                toks = markov_tokens(tokens_per_shard, vocab_size, rng, succ=succ)
+                toks = markov_tokens(tokens_per_shard, vocab_size, rng, succ=succ, zipf_map=zipf_map)
             else:
                 toks = rng.integers(0, vocab_size, size=tokens_per_shard, dtype=np.int64)
             np.save(p, toks.astype(dtype))

@@ -18,12 +18,12 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.conv1d import causal_conv1d_fn, causal_conv1d_update
+from ..ops.conv1d import causal_conv1d_update
 from ..ops.linear import linear
 from ..ops.norm import RMSNormGated
 from ..ops.reference import softplus_inverse
 from ..ops.selective_scan import selective_state_update
-from ..ops.ssd import mamba2_inner_fn, mamba_chunk_scan_combined
+from ..ops.ssd import mamba2_inner_fn
 
 
 class Mamba2(nn.Module):
@@ -94,7 +94,10 @@ class Mamba2(nn.Module):
                 out, _, _ = self.step(u, conv_state, ssm_state)
                 return out
         zxbcdt = linear(u, self.in_proj)
+        if seq_idx is None and cu_seqlens is not None:
+            seq_idx = seq_idx_from_cu_seqlens(cu_seqlens, l, u.device).expand(b, l)
         if self.cp_group is not None and conv_state is None:
+            assert seq_idx is None, "packed sequences (seq_idx) are not supported with context parallelism"
             from ..parallel.context_parallel import mamba2_inner_parallel
             y = mamba2_inner_parallel(zxbcdt, self.conv1d.weight, self.conv1d.bias, self.dt_bias, self.A_log,
                                       self.D, self.norm.weight, self.norm.eps, self.headdim, self.ngroups,
@@ -103,28 +106,24 @@ class Mamba2(nn.Module):
             y = mamba2_inner_fn(zxbcdt, self.conv1d.weight, self.conv1d.bias, self.dt_bias, self.A_log, self.D,
                                 self.norm.weight, self.norm.eps, self.headdim, self.ngroups, self.d_state,
                                 self.dt_limit, self.norm_before_gate, ref_chunk_size=min(64, self.chunk_size),
-                                A_is_log=True)
+                                A_is_log=True, seq_idx=seq_idx)
         else:
-            y = self._prefill(zxbcdt, -torch.exp(self.A_log.float()), conv_state, ssm_state)
+            y = self._prefill(zxbcdt, conv_state, ssm_state)
         return linear(y, self.out_proj)
 
-    def _prefill(self, zxbcdt, A, conv_state, ssm_state):
-        """Prompt pass that also fills the decode cache (conv window + final SSM state)."""
-        di, gn, H = self.d_ssm, self.ngroups * self.d_state, self.nheads
-        z, xBC, dt = torch.split(zxbcdt, [di, di + 2 * gn, H], dim=-1)
-        xt = xBC.transpose(1, 2)
+    def _prefill(self, zxbcdt, conv_state, ssm_state):
+        """Prompt pass that also fills the decode cache (conv window + final SSM state): the same fused
+        native chain as training (conv1d -> SSD -> gated norm) with ``return_final_states``."""
+        di, gn = self.d_ssm, self.ngroups * self.d_state
+        xt = zxbcdt[..., di:2 * di + 2 * gn].transpose(1, 2)
         sl = conv_state.shape[-1]  # upstream layout: the last d_conv inputs
         conv_state.copy_(F.pad(xt, (max(0, sl - xt.shape[-1]), 0))[..., -sl:])
-        xBC = causal_conv1d_fn(xt, self.conv1d.weight, self.conv1d.bias, "silu").transpose(1, 2)
-        x, Bm, Cm = torch.split(xBC, [di, gn, gn], dim=-1)
-        y, last = mamba_chunk_scan_combined(x.unflatten(-1, (H, self.headdim)), dt, A,
-                                            Bm.unflatten(-1, (self.ngroups, self.d_state)),
-                                            Cm.unflatten(-1, (self.ngroups, self.d_state)),
-                                            min(64, self.chunk_size), D=self.D, dt_bias=self.dt_bias,
-                                            dt_softplus=True, dt_limit=self.dt_limit, return_final_states=True)
-        y = y.to(zxbcdt.dtype)
+        y, last = mamba2_inner_fn(zxbcdt, self.conv1d.weight, self.conv1d.bias, self.dt_bias, self.A_log, self.D,
+                                  self.norm.weight, self.norm.eps, self.headdim, self.ngroups, self.d_state,
+                                  self.dt_limit, self.norm_before_gate, ref_chunk_size=min(64, self.chunk_size),
+                                  A_is_log=True, return_final_states=True)
         ssm_state.copy_(last)
-        return self.norm(y.flatten(-2), z)
+        return y
 
     @torch.no_grad()
     def step(self, hidden_states, conv_state, ssm_state):
@@ -158,3 +157,12 @@ class Mamba2(nn.Module):
             inference_params.key_value_memory_dict[self.layer_idx] = self.allocate_inference_cache(
                 batch_size, inference_params.max_seqlen)
         return inference_params.key_value_memory_dict[self.layer_idx]
+
+
+def seq_idx_from_cu_seqlens(cu_seqlens: torch.Tensor, seqlen: int, device=None) -> torch.Tensor:
+    """(1, seqlen) int32 sequence index of every packed token from cumulative lengths [0, l1, l1+l2, ...]."""
+    cu = cu_seqlens.to(device=device, dtype=torch.long)
+    lens = (cu[1:] - cu[:-1]).clamp(min=0)
+    idx = torch.repeat_interleave(torch.arange(lens.numel(), device=cu.device, dtype=torch.int32), lens)
+    assert idx.numel() == seqlen, f"cu_seqlens covers {idx.numel()} tokens, sequence has {seqlen}"
+    return idx.unsqueeze(0)

@@ -85,10 +85,13 @@ def causal_conv1d_ref(
     activation: Optional[str] = None,
     initial_states: Optional[torch.Tensor] = None,
     return_final_states: bool = False,
+    seq_idx: Optional[torch.Tensor] = None,
 ):
     """x: (b, d, l) channel-first (any strides); weight: (d, w); initial_states: (b, d, w-1).
 
     out[b,c,t] = act(bias_c + sum_k w[c,k] * x[b,c,t-(w-1)+k]), zero (or initial_states) left pad.
+    seq_idx (b, l): a tap contributes only if its input belongs to the output's sequence (the initial
+    states belong to the row's first sequence).
     """
     dtype = x.dtype
     b, d, l = x.shape
@@ -98,8 +101,17 @@ def causal_conv1d_ref(
         xp = F.pad(xf, (w - 1, 0))
     else:
         xp = torch.cat([_f(initial_states), xf], dim=-1)
-    out = F.conv1d(xp, _f(weight).unsqueeze(1), _f(bias) if bias is not None else None, groups=d)
-    out = out[..., :l]
+    if seq_idx is None:
+        out = F.conv1d(xp, _f(weight).unsqueeze(1), _f(bias) if bias is not None else None, groups=d)
+        out = out[..., :l]
+    else:
+        sq = seq_idx.long()
+        sqp = torch.cat([sq[:, :1].expand(b, w - 1), sq], dim=1)        # pad slots: first sequence
+        wf = _f(weight)
+        out = xf.new_zeros(b, d, l) + (_f(bias)[None, :, None] if bias is not None else 0.0)
+        for k in range(w):
+            same = (sqp[:, k:k + l] == sq).to(xf.dtype)[:, None, :]     # input t-(w-1)+k vs output t
+            out = out + wf[None, :, k:k + 1] * xp[..., k:k + l] * same
     if activation in ("silu", "swish"):
         out = F.silu(out)
     out = out.to(dtype)
@@ -296,12 +308,16 @@ def ssd_chunked_ref(
     dt_limit=(0.0, float("inf")),
     initial_states: Optional[torch.Tensor] = None,  # (b, h, p, n)
     return_final_states: bool = False,
+    seq_idx: Optional[torch.Tensor] = None,         # (b, l) int, non-decreasing per row
 ):
     """Chunked SSD.  Exact semantics of upstream ``mamba_chunk_scan_combined``:
 
     dt' = softplus(dt + dt_bias) ; a_t = dt'_t A_h ; within chunk cum = cumsum(a)
     y_t = sum_{s<=t in chunk} (C_t.B_s) e^{cum_t-cum_s} dt'_s x_s + e^{cum_t} C_t . S_prev + D x_t
     S_next = e^{cum_last} S_prev + sum_s e^{cum_last-cum_s} dt'_s x_s B_s^T
+    seq_idx (packed rows): explicit masks -- every term that links two tokens (or a token and the
+    carried state) of different sequences is dropped; the initial state belongs to the row's first
+    sequence; the final state is the last sequence's.
     """
     dtype = x.dtype
     b, l, h, p = x.shape
@@ -316,6 +332,13 @@ def ssd_chunked_ref(
         Cf = F.pad(Cf, (0, 0, 0, 0, 0, pad))
         dtp = F.pad(dtp, (0, 0, 0, pad))
     nc = (l + pad) // q
+    if seq_idx is not None:
+        sq = seq_idx.long()
+        if pad:
+            sq = torch.cat([sq, sq[:, -1:].expand(b, pad)], dim=1)
+        sq = sq.reshape(b, nc, q)
+        sq_last = sq[:, :, -1]                                         # (b,c)
+        sq_prev = torch.cat([sq[:, :1, 0], sq_last[:, :-1]], dim=1)   # state owner entering chunk c
     xf = xf.reshape(b, nc, q, h, p)
     Bf = Bf.reshape(b, nc, q, g, n).repeat_interleave(h // g, dim=3)
     Cf = Cf.reshape(b, nc, q, g, n).repeat_interleave(h // g, dim=3)
@@ -324,20 +347,29 @@ def ssd_chunked_ref(
     cum = torch.cumsum(a, dim=2)                                   # (b,c,q,h)
     seg = cum[:, :, :, None, :] - cum[:, :, None, :, :]            # (b,c,t,s,h)
     mask = torch.ones(q, q, dtype=torch.bool, device=x.device).tril()[None, None, :, :, None]
+    if seq_idx is not None:
+        mask = mask & (sq[:, :, :, None] == sq[:, :, None, :])[..., None]
     Ldec = torch.exp(seg.masked_fill(~mask, float("-inf")))
     CB = torch.einsum("bcthn,bcshn->bctsh", Cf, Bf)
     xdt = xf * dtc[..., None]
     y = torch.einsum("bctsh,bcshp->bcthp", CB * Ldec, xdt)
     decay_states = torch.exp(cum[:, :, -1:, :] - cum)              # (b,c,q,h)
+    if seq_idx is not None:
+        decay_states = decay_states * (sq == sq_last[..., None]).to(cum.dtype)[..., None]
     states = torch.einsum("bcshn,bcsh,bcshp->bchpn", Bf, decay_states, xdt)
     S = xf.new_zeros(b, h, p, n) if initial_states is None else _f(initial_states)
     chunk_decay = torch.exp(cum[:, :, -1, :])                       # (b,c,h)
+    if seq_idx is not None:
+        chunk_decay = chunk_decay * (sq_last == sq_prev).to(cum.dtype)[..., None]
     s_in = []
     for c in range(nc):
         s_in.append(S)
         S = chunk_decay[:, c, :, None, None] * S + states[:, c]
     S_in = torch.stack(s_in, dim=1)                                  # (b,c,h,p,n)
-    y = y + torch.einsum("bcthn,bchpn->bcthp", Cf, S_in) * torch.exp(cum)[..., None]
+    state_w = torch.exp(cum)
+    if seq_idx is not None:
+        state_w = state_w * (sq == sq_prev[..., None]).to(cum.dtype)[..., None]
+    y = y + torch.einsum("bcthn,bchpn->bcthp", Cf, S_in) * state_w[..., None]
     y = y.reshape(b, nc * q, h, p)[:, :l]
     if D is not None:
         Df = _f(D)
@@ -349,8 +381,10 @@ def ssd_chunked_ref(
 
 
 def ssd_sequential_ref(x, dt, A, B, C, D=None, z=None, dt_bias=None, dt_softplus=True,
-                       dt_limit=(0.0, float("inf")), initial_states=None, return_final_states=False):
-    """Token-by-token Mamba-2 recurrence (definition; tests only)."""
+                       dt_limit=(0.0, float("inf")), initial_states=None, return_final_states=False,
+                       seq_idx=None):
+    """Token-by-token Mamba-2 recurrence (definition; tests only).  seq_idx: the state restarts
+    from zero wherever seq_idx changes."""
     dtype = x.dtype
     b, l, h, p = x.shape
     g, n = B.shape[2], B.shape[3]
@@ -361,6 +395,8 @@ def ssd_sequential_ref(x, dt, A, B, C, D=None, z=None, dt_bias=None, dt_softplus
     ys = []
     for t in range(l):
         dA = torch.exp(dtp[:, t] * _f(A))  # (b,h)
+        if seq_idx is not None and t > 0:
+            dA = dA * (seq_idx[:, t] == seq_idx[:, t - 1]).to(dA.dtype)[:, None]
         S = S * dA[..., None, None] + (dtp[:, t, :, None] * _f(x[:, t]))[..., None] * Bh[:, t, :, None, :]
         ys.append(torch.einsum("bhpn,bhn->bhp", S, Ch[:, t]))
     y = torch.stack(ys, dim=1)

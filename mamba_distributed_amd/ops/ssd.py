@@ -39,10 +39,10 @@ NATIVE_CHUNK = 64
 class _SSDFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, dt, A, B, C, D, dt_bias, initial_states, dt_softplus, dt_min, dt_max,
-                return_final_states):
+                return_final_states, seq_idx=None):
         ops = _ext.ops()
         y, cum, dtp, states, final = ops.ssd_fwd(x, dt, A, B, C, D, dt_bias, initial_states,
-                                                  NATIVE_CHUNK, dt_softplus, dt_min, dt_max)
+                                                  NATIVE_CHUNK, dt_softplus, dt_min, dt_max, False, seq_idx)
         ctx.save_for_backward(x, dt, A, B, C, D, dt_bias, initial_states, cum, dtp, states)
         ctx.flags = (dt_softplus, dt_min, dt_max)
         ctx.return_final = return_final_states
@@ -65,23 +65,27 @@ class _SSDFn(torch.autograd.Function):
                 d(pD, dD) if D is not None else None,
                 d(pdtb, ddt_bias) if dt_bias is not None else None,
                 dinit if init is not None else None,
-                None, None, None, None)
+                None, None, None, None, None)
 
 
 def mamba_chunk_scan_combined(x, dt, A, B, C, chunk_size=256, D=None, z=None, dt_bias=None,
                               initial_states=None, seq_idx=None, dt_softplus=False,
                               dt_limit=(0.0, _INF), return_final_states=False):
-    """x (b,l,h,p), dt (b,l,h), A (h), B/C (b,l,g,n) -> y (b,l,h,p) [, final_states (b,h,p,n)]."""
-    assert seq_idx is None, "seq_idx (packed variable-length) is not supported yet"
+    """x (b,l,h,p), dt (b,l,h), A (h), B/C (b,l,g,n) -> y (b,l,h,p) [, final_states (b,h,p,n)].
+
+    ``seq_idx`` (b,l) int, non-decreasing per row: packed variable-length sequences; the scan state
+    restarts at every change (native: the in-chunk cumsum gets a -256 offset at each sequence
+    start, so every decay factor across the boundary is exactly 0 in fp32 -- the same masks as
+    upstream, with unchanged gradients).  ``initial_states`` belong to the row's first sequence."""
     # native kernels are bf16 (the training/serving dtype); fp32 activations (e.g. the reference's
     # fp32 HellaSwag eval) take the fp32 reference path
     if x.dtype == torch.bfloat16 and _ext.use_native(x) and z is None and (D is None or D.dim() == 1):
         out = _SSDFn.apply(x, dt, A, B, C, D, dt_bias, initial_states, dt_softplus,
-                           float(dt_limit[0]), float(dt_limit[1]), return_final_states)
+                           float(dt_limit[0]), float(dt_limit[1]), return_final_states, seq_idx)
         return out
     return ssd_chunked_ref(x, dt, A, B, C, chunk_size, D=D, z=z, dt_bias=dt_bias,
                            dt_softplus=dt_softplus, dt_limit=dt_limit, initial_states=initial_states,
-                           return_final_states=return_final_states)
+                           return_final_states=return_final_states, seq_idx=seq_idx)
 
 
 # ----------------------------------------------------------------------------------------
@@ -91,7 +95,8 @@ def mamba_chunk_scan_combined(x, dt, A, B, C, chunk_size=256, D=None, z=None, dt
 class _Mamba2InnerFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, zxbcdt, conv_w, conv_b, dt_bias, A, D, norm_w, eps, headdim, ngroups, d_state,
-                dt_min, dt_max, norm_before_gate, A_is_log=False):
+                dt_min, dt_max, norm_before_gate, A_is_log=False, initial_states=None, seq_idx=None,
+                return_final_states=False):
         ops = _ext.ops()
         b, l, dproj = zxbcdt.shape
         H = dt_bias.shape[0]
@@ -104,23 +109,31 @@ class _Mamba2InnerFn(torch.autograd.Function):
         xBC = zxbcdt[..., di:di + conv_dim]
         dt = zxbcdt[..., di + conv_dim:]
         w2 = conv_w.reshape(conv_dim, -1)
-        xBC_c = ops.conv1d_cl_fwd(xBC, w2, conv_b, True)                # (b, l, conv_dim)
+        if seq_idx is None:
+            xBC_c = ops.conv1d_cl_fwd(xBC, w2, conv_b, True)                # (b, l, conv_dim)
+        else:
+            xBC_c, _ = ops.conv1d_cl_var_fwd(xBC, w2, conv_b, True, seq_idx, None, False)
         x = xBC_c[..., :di].unflatten(-1, (H, headdim))
         Bm = xBC_c[..., di:di + ngroups * d_state].unflatten(-1, (ngroups, d_state))
         Cm = xBC_c[..., di + ngroups * d_state:].unflatten(-1, (ngroups, d_state))
-        y, cum, dtp, states, _ = ops.ssd_fwd(x, dt, A, Bm, Cm, D, dt_bias, None, NATIVE_CHUNK,
-                                             True, dt_min, dt_max, A_is_log)
+        y, cum, dtp, states, final = ops.ssd_fwd(x, dt, A, Bm, Cm, D, dt_bias, initial_states, NATIVE_CHUNK,
+                                                 True, dt_min, dt_max, A_is_log, seq_idx)
         y2 = y.view(b * l, di)
         yn, rstd = ops.gated_rmsnorm_fwd(y2, z.flatten(0, 1), norm_w, eps, di // ngroups, norm_before_gate)
-        ctx.save_for_backward(zxbcdt, w2, conv_b, dt_bias, A, D, norm_w, xBC_c, y, rstd, cum, dtp, states)
+        ctx.save_for_backward(zxbcdt, w2, conv_b, dt_bias, A, D, norm_w, xBC_c, y, rstd, cum, dtp, states,
+                              initial_states, seq_idx)
         ctx.meta = (eps, headdim, ngroups, d_state, dt_min, dt_max, norm_before_gate, A_is_log)
         ctx.wshape = conv_w.shape
         ctx.params = (conv_w, conv_b, dt_bias, A, D, norm_w)
-        return yn.view(b, l, di)
+        ctx.ret_final = return_final_states
+        if not return_final_states:
+            ctx.mark_non_differentiable(final)
+        return yn.view(b, l, di), final
 
     @staticmethod
-    def backward(ctx, dyn):
-        (zxbcdt, w2, conv_b, dt_bias, A, D, norm_w, xBC_c, y, rstd, cum, dtp, states) = ctx.saved_tensors
+    def backward(ctx, dyn, dfinal):
+        (zxbcdt, w2, conv_b, dt_bias, A, D, norm_w, xBC_c, y, rstd, cum, dtp, states, init,
+         seq_idx) = ctx.saved_tensors
         eps, headdim, ngroups, d_state, dt_min, dt_max, nbg, a_log = ctx.meta
         ops = _ext.ops()
         b, l, dproj = zxbcdt.shape
@@ -135,7 +148,8 @@ class _Mamba2InnerFn(torch.autograd.Function):
         # parameter-gradient partials are reduced once per optimizer step (grad_accum.deferred)
         d_n = grad_accum.deferred(pn, "gated_rmsnorm", (ops.part_rows("gated_rmsnorm", b * l), di), dev)
         d_s = grad_accum.deferred(pA, "ssd_small", (b * ((l + NATIVE_CHUNK - 1) // NATIVE_CHUNK), 3, H), dev)
-        d_c = grad_accum.deferred(pw, "conv_cl", (ops.part_rows("conv_cl", b, l), conv_dim, w2.shape[1] + 1), dev)
+        ck = "conv_cl" if seq_idx is None else "conv_cl_var"
+        d_c = grad_accum.deferred(pw, ck, (ops.part_rows(ck, b, l), conv_dim, w2.shape[1] + 1), dev)
         # gated norm backward writes dz straight into its slice of d(zxbcdt)
         dy, _, dnorm_w = ops.gated_rmsnorm_bwd(dyn.reshape(b * l, di), y.view(b * l, di),
                                                z.flatten(0, 1), norm_w, rstd, di // ngroups, nbg,
@@ -145,55 +159,75 @@ class _Mamba2InnerFn(torch.autograd.Function):
         Cm = xBC_c[..., di + gn:].unflatten(-1, (ngroups, d_state))
         dt = zxbcdt[..., di + conv_dim:]
         dxBC_c = torch.empty_like(xBC_c)
-        g = ops.ssd_bwd(dy.view(b, l, H, headdim), x, dt, A, Bm, Cm, D, dt_bias, None, cum, dtp, states,
-                        None, NATIVE_CHUNK, True, dt_min, dt_max,
+        g = ops.ssd_bwd(dy.view(b, l, H, headdim), x, dt, A, Bm, Cm, D, dt_bias, init, cum, dtp, states,
+                        dfinal if ctx.ret_final else None, NATIVE_CHUNK, True, dt_min, dt_max,
                         dxBC_c[..., :di].unflatten(-1, (H, headdim)),
                         dz_all[..., di + conv_dim:],
                         dxBC_c[..., di:di + gn].unflatten(-1, (ngroups, d_state)),
                         dxBC_c[..., di + gn:].unflatten(-1, (ngroups, d_state)), a_log, *(d_s or (None, 0)))
-        _, _, dA, _, _, dD, ddt_bias, _ = g
+        _, _, dA, _, _, dD, ddt_bias, dinit = g
         xBC = zxbcdt[..., di:di + conv_dim]
-        _, dw, db = ops.conv1d_cl_bwd(xBC, w2, conv_b, dxBC_c, True, dz_all[..., di:di + conv_dim],
-                                      *(d_c or (None, 0)))
+        if seq_idx is None:
+            _, dw, db = ops.conv1d_cl_bwd(xBC, w2, conv_b, dxBC_c, True, dz_all[..., di:di + conv_dim],
+                                          *(d_c or (None, 0)))
+        else:
+            _, dw, db, _ = ops.conv1d_cl_var_bwd(xBC, w2, conv_b, dxBC_c, True, seq_idx, None, None,
+                                                 dz_all[..., di:di + conv_dim], *(d_c or (None, 0)))
         d = grad_accum.defer
         nz = lambda t: t if t.numel() else None  # noqa: E731  (empty = deferred to the sync micro-step)
         dw = nz(dw)
         return (dz_all, d(pw, dw.reshape(ctx.wshape).to(w2.dtype)) if dw is not None else None,
                 d(pb, nz(db).to(conv_b.dtype)) if (conv_b is not None and db.numel()) else None,
                 d(pdtb, nz(ddt_bias)), d(pA, nz(dA)), d(pD, nz(dD)), d(pn, nz(dnorm_w)),
-                None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None,
+                dinit if init is not None else None, None, None)
 
 
 def mamba2_inner_ref(zxbcdt, conv_w, conv_b, dt_bias, A, D, norm_w, eps, headdim, ngroups, d_state,
-                     dt_limit=(0.0, _INF), norm_before_gate=False, chunk_size=64):
+                     dt_limit=(0.0, _INF), norm_before_gate=False, chunk_size=64, initial_states=None,
+                     seq_idx=None, return_final_states=False):
     b, l, dproj = zxbcdt.shape
     H = dt_bias.shape[0]
     di = H * headdim
     gn = ngroups * d_state
     conv_dim = di + 2 * gn
     z, xBC, dt = torch.split(zxbcdt, [di, conv_dim, H], dim=-1)
-    xBC = causal_conv1d_ref(xBC.transpose(1, 2), conv_w.reshape(conv_dim, -1), conv_b, "silu").transpose(1, 2)
+    xBC = causal_conv1d_ref(xBC.transpose(1, 2), conv_w.reshape(conv_dim, -1), conv_b, "silu",
+                            seq_idx=seq_idx).transpose(1, 2)
     x, Bm, Cm = torch.split(xBC, [di, gn, gn], dim=-1)
     y = ssd_chunked_ref(x.unflatten(-1, (H, headdim)), dt, A, Bm.unflatten(-1, (ngroups, d_state)),
                         Cm.unflatten(-1, (ngroups, d_state)), chunk_size, D=D, dt_bias=dt_bias,
-                        dt_softplus=True, dt_limit=dt_limit)
-    y = y.flatten(-2)
-    return gated_rms_norm_ref(y, z, norm_w, eps, di // ngroups, norm_before_gate)
+                        dt_softplus=True, dt_limit=dt_limit, initial_states=initial_states,
+                        return_final_states=return_final_states, seq_idx=seq_idx)
+    y, final = y if return_final_states else (y, None)
+    y = gated_rms_norm_ref(y.flatten(-2), z, norm_w, eps, di // ngroups, norm_before_gate)
+    return (y, final) if return_final_states else y
 
 
 def mamba2_inner_fn(zxbcdt, conv_w, conv_b, dt_bias, A, D, norm_w, eps, headdim, ngroups, d_state,
-                    dt_limit=(0.0, _INF), norm_before_gate=False, ref_chunk_size=64, A_is_log=False):
-    """conv1d+SiLU -> SSD -> gated RMSNorm on the in_proj output; returns (b, l, d_inner).
+                    dt_limit=(0.0, _INF), norm_before_gate=False, ref_chunk_size=64, A_is_log=False,
+                    initial_states=None, seq_idx=None, return_final_states=False):
+    """conv1d+SiLU -> SSD -> gated RMSNorm on the in_proj output; returns (b, l, d_inner)
+    [, final SSM states (b, h, p, n) fp32].
     ``A_is_log``: ``A`` is the A_log parameter; the kernels apply A = -exp(A_log) and return dA_log
-    (saves the per-layer exp/neg launches and their backward)."""
+    (saves the per-layer exp/neg launches and their backward).  ``initial_states`` (b, h, p, n) SSM
+    states entering the sequence (gradients flow); ``seq_idx`` (b, l) packed variable-length rows
+    (conv taps and the scan state never cross a change)."""
     if zxbcdt.dtype == torch.bfloat16 and _ext.use_native(zxbcdt):
-        return _Mamba2InnerFn.apply(zxbcdt, conv_w, conv_b, dt_bias, A, D, norm_w, eps, headdim,
-                                    ngroups, d_state, float(dt_limit[0]), float(dt_limit[1]),
-                                    norm_before_gate, A_is_log)
+        if seq_idx is not None:
+            seq_idx = seq_idx.to(torch.int32).contiguous()
+        if initial_states is not None:
+            initial_states = initial_states.float().contiguous()
+        y, final = _Mamba2InnerFn.apply(zxbcdt, conv_w, conv_b, dt_bias, A, D, norm_w, eps, headdim,
+                                        ngroups, d_state, float(dt_limit[0]), float(dt_limit[1]),
+                                        norm_before_gate, A_is_log, initial_states, seq_idx,
+                                        return_final_states)
+        return (y, final) if return_final_states else y
     if A_is_log:
         A = -torch.exp(A.float())
     return mamba2_inner_ref(zxbcdt, conv_w, conv_b, dt_bias, A, D, norm_w, eps, headdim, ngroups,
-                            d_state, dt_limit, norm_before_gate, ref_chunk_size)
+                            d_state, dt_limit, norm_before_gate, ref_chunk_size, initial_states,
+                            seq_idx, return_final_states)
 
 
 def mamba_split_conv1d_scan_combined(zxbcdt, conv1d_weight, conv1d_bias, dt_bias, A, D, chunk_size,
@@ -201,14 +235,18 @@ def mamba_split_conv1d_scan_combined(zxbcdt, conv1d_weight, conv1d_bias, dt_bias
                                      return_final_states=False, activation="silu",
                                      rmsnorm_weight=None, rmsnorm_eps=1e-6, outproj_weight=None,
                                      outproj_bias=None, headdim=None, ngroups=1, norm_before_gate=True):
-    """Upstream-compatible entry point (D11).  Requires rmsnorm_weight (the Mamba2 default)."""
-    assert initial_states is None and seq_idx is None and not return_final_states
+    """Upstream-compatible entry point (D11).  Requires rmsnorm_weight (the Mamba2 default).
+    ``initial_states`` (b, h, p, n), ``seq_idx`` (b, l) and ``return_final_states`` run through the
+    fused native chain (conv1d_cl_var / ssd_fwd with seq_idx and initial states)."""
     assert activation in ("silu", "swish") and rmsnorm_weight is not None
     H = dt_bias.shape[0]
     d_state = (zxbcdt.shape[-1] - H - 2 * H * headdim) // (2 * ngroups)
-    y = mamba2_inner_fn(zxbcdt, conv1d_weight, conv1d_bias, dt_bias, A, D, rmsnorm_weight, rmsnorm_eps,
-                        headdim, ngroups, d_state, dt_limit, norm_before_gate, chunk_size)
+    out = mamba2_inner_fn(zxbcdt, conv1d_weight, conv1d_bias, dt_bias, A, D, rmsnorm_weight, rmsnorm_eps,
+                          headdim, ngroups, d_state, dt_limit, norm_before_gate, chunk_size,
+                          initial_states=initial_states, seq_idx=seq_idx,
+                          return_final_states=return_final_states)
+    y, final = out if return_final_states else (out, None)
     if outproj_weight is not None:
         y = F.linear(y, outproj_weight, outproj_bias)
-    return y
+    return (y, final) if return_final_states else y
 

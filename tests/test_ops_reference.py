@@ -157,3 +157,61 @@ def test_conv_update_state_len_semantics(extra):
     outs = [causal_conv1d_update_ref(x[..., t], state, wt, bias, "silu") for t in range(L)]
     torch.testing.assert_close(torch.stack(outs, -1), full)
     torch.testing.assert_close(state, x[..., L - sl:])
+
+
+# ------------------------------------------------------------------------------------------
+# packed variable-length sequences (seq_idx) — references vs running each sequence on its own
+# ------------------------------------------------------------------------------------------
+def _seq_idx(lens):
+    return torch.cat([torch.full((n,), i, dtype=torch.int32) for i, n in enumerate(lens)])[None]
+
+
+def test_conv_ref_seq_idx_matches_separate_sequences():
+    torch.manual_seed(0)
+    lens = [5, 1, 9, 3]
+    d, w = 6, 4
+    x = torch.randn(1, d, sum(lens), dtype=torch.float64)
+    wt = torch.randn(d, w, dtype=torch.float64)
+    bias = torch.randn(d, dtype=torch.float64)
+    init = torch.randn(1, d, w - 1, dtype=torch.float64)
+    out, fin = R.causal_conv1d_ref(x, wt, bias, "silu", initial_states=init, return_final_states=True,
+                                   seq_idx=_seq_idx(lens))
+    parts, s = [], 0
+    for i, n in enumerate(lens):
+        parts.append(R.causal_conv1d_ref(x[..., s:s + n], wt, bias, "silu", initial_states=init if i == 0 else None))
+        s += n
+    torch.testing.assert_close(out, torch.cat(parts, -1))
+    torch.testing.assert_close(fin, x[..., -(w - 1):])
+
+
+@pytest.mark.parametrize("lens", [[70, 58], [64, 64, 3], [10, 1, 100, 17]])
+def test_ssd_ref_seq_idx_matches_separate_sequences(lens):
+    torch.manual_seed(1)
+    b, h, p, g, n = 1, 4, 8, 2, 16
+    L = sum(lens)
+    x = torch.randn(b, L, h, p, dtype=torch.float64)
+    dt = torch.randn(b, L, h, dtype=torch.float64) * 0.5
+    A = -torch.rand(h, dtype=torch.float64) * 2 - 0.1
+    B = torch.randn(b, L, g, n, dtype=torch.float64)
+    C = torch.randn(b, L, g, n, dtype=torch.float64)
+    D = torch.randn(h, dtype=torch.float64)
+    init = torch.randn(b, h, p, n, dtype=torch.float64)
+    sq = _seq_idx(lens)
+    y, fin = R.ssd_chunked_ref(x, dt, A, B, C, 32, D=D, initial_states=init, return_final_states=True, seq_idx=sq)
+    ys, fs = R.ssd_sequential_ref(x, dt, A, B, C, D=D, initial_states=init, return_final_states=True, seq_idx=sq)
+    torch.testing.assert_close(y, ys)
+    torch.testing.assert_close(fin, fs)
+    parts, s = [], 0
+    for i, m in enumerate(lens):
+        yi, fi = R.ssd_sequential_ref(x[:, s:s + m], dt[:, s:s + m], A, B[:, s:s + m], C[:, s:s + m], D=D,
+                                      initial_states=init if i == 0 else None, return_final_states=True)
+        parts.append(yi)
+        s += m
+    torch.testing.assert_close(y, torch.cat(parts, 1))
+    torch.testing.assert_close(fin, fi)
+
+
+def test_seq_idx_from_cu_seqlens():
+    from mamba_distributed_amd.models.mamba2 import seq_idx_from_cu_seqlens
+    sq = seq_idx_from_cu_seqlens(torch.tensor([0, 3, 4, 9]), 9)
+    assert sq.tolist() == [[0, 0, 0, 1, 2, 2, 2, 2, 2]] and sq.dtype == torch.int32
