@@ -185,9 +185,17 @@ __global__ __launch_bounds__(256) void ssd_fused_fwd_k(SSDArgs a) {
     pcum = cumbh[c * Q + (threadIdx.x & 63)];
     pdt = dtbh[c * Q + (threadIdx.x & 63)];
   };
+  // Y rows of one chunk, staged in Os by the wave that owns them (no block barrier needed)
+  auto store_y_rows = [&](int cc) {
+    const int row = 16 * w + (l >> 2), col = 16 * (l & 3);
+    if (row < min(Q, a.L - cc * Q)) {
+      bf16_t* yg = a.y + (int64_t)b * a.syb + (int64_t)(cc * Q + row) * a.syl + (int64_t)h * a.syh + col;
+      *reinterpret_cast<uint4*>(yg) = *reinterpret_cast<const uint4*>(Os + row * LD64 + col);
+      *reinterpret_cast<uint4*>(yg + 8) = *reinterpret_cast<const uint4*>(Os + row * LD64 + col + 8);
+    }
+  };
   prefetch(0);
   for (int c = 0; c < a.nc; ++c) {
-    const int valid = min(Q, a.L - c * Q);
     __syncthreads();  // chunk c-1 is fully consumed
     px.store(Xs, LD64);
     pb.store(Bs, LDN);
@@ -200,9 +208,10 @@ __global__ __launch_bounds__(256) void ssd_fused_fwd_k(SSDArgs a) {
 #pragma unroll
     for (int nt = 0; nt < NTS; ++nt) acc_to_lds(Ss, LDN, 16 * w, 16 * nt, st[nt]);
     __syncthreads();
-    if (c + 1 < a.nc) prefetch(c + 1);
-    const float cl = cumr[Q - 1];
-    // ---- save S_c for the backward (rows 16w.., one 16-B vector per lane per 64 columns)
+    // ---- global stores BEFORE the prefetch loads: vmcnt counts stores too and completes in order,
+    // so the wait for chunk c+1's operands at the next loop top must not also wait for stores issued
+    // at the end of this chunk.  Y rows of chunk c-1 (staged in Os by this same wave), then S_c.
+    if (c > 0) store_y_rows(c - 1);
     {
       bf16_t* sg = a.states + ((((int64_t)b * a.nc + c) * a.H + h) * P) * N;
 #pragma unroll
@@ -213,6 +222,8 @@ __global__ __launch_bounds__(256) void ssd_fused_fwd_k(SSDArgs a) {
             *reinterpret_cast<const uint4*>(Ss + row * LDN + col + 8);
       }
     }
+    if (c + 1 < a.nc) prefetch(c + 1);
+    const float cl = cumr[Q - 1];
     // ---- Y_off = e^{cum_i} C_i . S_c^T   (rows i of tile w, 4 p-tiles)
     f32x4 acc[4];
 #pragma unroll
@@ -268,14 +279,6 @@ __global__ __launch_bounds__(256) void ssd_fused_fwd_k(SSDArgs a) {
       for (int r = 0; r < 4; ++r)
         Os[(16 * w + 4 * lg + r) * LD64 + 16 * pt + li] = f2bf(acc[pt][r] + Dh * (float)xr[r]);
     }
-    {
-      const int row = 16 * w + (l >> 2), col = 16 * (l & 3);
-      if (row < valid) {
-        bf16_t* yg = a.y + (int64_t)b * a.syb + (int64_t)(c * Q + row) * a.syl + (int64_t)h * a.syh + col;
-        *reinterpret_cast<uint4*>(yg) = *reinterpret_cast<const uint4*>(Os + row * LD64 + col);
-        *reinterpret_cast<uint4*>(yg + 8) = *reinterpret_cast<const uint4*>(Os + row * LD64 + col + 8);
-      }
-    }
     // ---- S_{c+1} = e^{cl} S_c + (X o w)^T B
     const float decay = __expf(cl);
 #pragma unroll
@@ -292,6 +295,7 @@ __global__ __launch_bounds__(256) void ssd_fused_fwd_k(SSDArgs a) {
       for (int nt = 0; nt < NTS; ++nt) st[nt] = mfma16(A, frag_tr(Bs, LDN, 32 * ks, 16 * nt), st[nt]);
     }
   }
+  store_y_rows(a.nc - 1);
   if (a.final_state) {
 #pragma unroll
     for (int nt = 0; nt < NTS; ++nt)
@@ -348,9 +352,11 @@ __global__ __launch_bounds__(256) void ssd_dstate_bwd_k(SSDArgs a) {
     if (threadIdx.x < Q) er[threadIdx.x] = __expf(pe);
     const float decay = __expf(pl);
     __syncthreads();
-    store_tile<P, N>(a.dstates + ((((int64_t)b * a.nc + c) * a.H + h) * P) * N, N, Os, LDN, P);
+    // operands first (waits for the loads issued last chunk), then this chunk's stores, then the next
+    // loads: vmcnt completes in order, so stores issued before a wait would be waited for too
     py.store(Ys, LD64, er);
     pcs.store(Cs, LDN);
+    store_tile<P, N>(a.dstates + ((((int64_t)b * a.nc + c) * a.H + h) * P) * N, N, Os, LDN, P);
     if (c > 0) prefetch(c - 1);
     __syncthreads();
 #pragma unroll

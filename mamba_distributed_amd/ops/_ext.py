@@ -23,7 +23,8 @@ _LOADED = None  # None = not tried, False = failed, str = path
 _ERR = None
 
 _PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SO_PATH = os.path.join(_PKG_DIR, "_C.so")
+# MAMBA_AMD_SO: load another build of the extension (kernel A/B runs against a saved baseline .so)
+SO_PATH = os.environ.get("MAMBA_AMD_SO") or os.path.join(_PKG_DIR, "_C.so")
 
 
 def load() -> bool:

@@ -5,7 +5,8 @@ long-context configs (Mamba-2 2.8B at T=8192 and beyond) the SSD's linear recurr
 and cheap split: rank r holds tokens [r*L/cp, (r+1)*L/cp) of every sequence.
 
   conv1d   causal, width W: rank r needs the last W-1 *pre-conv* rows of rank r-1 (a halo of
-           (b, W-1, conv_dim) -- a few hundred KB); rank 0 pads with zeros.
+           (b, W-1, conv_dim) -- a few hundred KB), fed to the conv as its initial states; rank 0
+           uses zeros.
   SSD      linear in the entering state S_in:  y = y_0 + e^{cum_t} C_t . S_in,
            S_out = e^{cum_L} S_in + S_0  (y_0 / S_0 = the local scan from a zero state).
            Each rank runs the native SSD once from zero, all-gathers (S_0, cum_L) -- (b,h,p,n) fp32
@@ -42,9 +43,9 @@ def cp_causal_conv1d(xBC: torch.Tensor, weight: torch.Tensor, bias, cp_group, ac
         # rank 0 pads with zeros, but through the graph (0 * tails) so its backward runs the same
         # all-reduce as every other rank's
         halo = tails[(r - 1) * b: r * b] if r > 0 else tails[:b] * 0.0
-        xpad = torch.cat([halo, xBC], dim=1)
-        out = causal_conv1d_fn(xpad.transpose(1, 2), weight, bias, activation).transpose(1, 2)
-        return out[:, w - 1:]
+        # the halo enters as the conv's initial states (native conv1d_cl_var; no padded copy of xBC)
+        return causal_conv1d_fn(xBC.transpose(1, 2), weight, bias, activation,
+                                initial_states=halo.transpose(1, 2)).transpose(1, 2)
     return causal_conv1d_fn(xBC.transpose(1, 2), weight, bias, activation).transpose(1, 2)
 
 
