@@ -402,6 +402,20 @@ int pick_hg(int B, int nc, int H, int G) {
   return best;
 }
 
+// forward chunk-output kernel: up to 8 heads per workgroup (C.B^T amortised) while keeping >= 1024
+// workgroups (4 per CU at its ~57 KB of LDS... 2 resident + a second wave of them)
+int pick_hg_fwd(int B, int nc, int H, int G) {
+  const int hpg = H / G;
+  if (const char* e = std::getenv("MAMBA_AMD_SSD_HGF")) {
+    const int v = std::atoi(e);
+    if (v >= 1 && hpg % v == 0) return v;
+  }
+  int best = 1;
+  for (int d = 1; d <= 8 && d <= hpg; ++d)
+    if (hpg % d == 0 && (int64_t)B * nc * (H / d) >= 1024) best = d;
+  return best;
+}
+
 void ssd_common(mamba_amd::SSDArgs& a, const Tensor& x, const Tensor& dt, const Tensor& A, const Tensor& Bm,
                 const Tensor& Cm, int64_t chunk, bool softplus, double dt_min, double dt_max) {
   TORCH_CHECK(chunk == 64, "native SSD chunk must be 64");
@@ -421,6 +435,8 @@ void ssd_common(mamba_amd::SSDArgs& a, const Tensor& x, const Tensor& dt, const 
               Bm.stride(2) % 8 == 0 && Cm.stride(2) % 8 == 0, "B/C rows must be 16-B aligned");
   a.nc = (a.L + 63) / 64; a.Lp = a.nc * 64;
   a.HG = pick_hg(a.B, a.nc, a.H, a.G); a.nhg = a.H / a.HG;
+  a.HGf = pick_hg_fwd(a.B, a.nc, a.H, a.G); a.nhgf = a.H / a.HGf;
+  if (const char* e = std::getenv("MAMBA_AMD_SSD_ABLATE")) a.ablate = std::atoi(e);
   a.x = (const mamba_amd::bf16_t*)x.data_ptr(); a.sxb = x.stride(0); a.sxl = x.stride(1); a.sxh = x.stride(2);
   a.dt = dt.data_ptr(); a.dt_dtype = dcode(dt.scalar_type());
   a.sdtb = dt.stride(0); a.sdtl = dt.stride(1); a.sdth = dt.stride(2);
