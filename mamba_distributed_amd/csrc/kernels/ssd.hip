@@ -398,6 +398,7 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t Xs[Q * LD64];
   __shared__ __attribute__((aligned(16))) bf16_t dYs[Q * LD64];
   __shared__ __attribute__((aligned(16))) bf16_t Os[Q * LD64];
+  __shared__ __attribute__((aligned(16))) bf16_t MsT[Q * LD64];  // M^T [j][i] of the current head
   // per-head dt-gradient inputs, kept for all heads of the group so step (10) runs once at the end
   // with one wave per head instead of serialising wave 0 inside the head loop
   // Every cross-lane partial goes to a slot owned by ONE wave (plain read-modify-write in program
@@ -435,17 +436,29 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
   for (int v = threadIdx.x; v < 8 * 2 * Q; v += 512) (&ddw[0][0][0])[v] = 0.f;
   stage_tile<Q, N>(Cs, LDN, a.Cm + (int64_t)b * a.sCb + (int64_t)c * Q * a.sCl + (int64_t)g * a.sCg, a.sCl, valid);
   stage_tile<Q, N>(Bs, LDN, a.Bm + (int64_t)b * a.sBb + (int64_t)c * Q * a.sBl + (int64_t)g * a.sBg, a.sBl, valid);
+  // (1)(2) tile ownership: the 10 lower-triangular 16x16 tiles (I >= J) of M / dM go to the 8 waves
+  // (waves 0 and 1 take two diagonal tiles each) -- no tile is computed twice and the busiest wave has
+  // 2 tiles (a column-tile split gives 4:3:2:1).  M^T goes through LDS to the waves that need it in (3).
+  // Waves 2..7 also own one of the 6 all-zero upper tiles (zeroed in MsT once, written to part_dcb).
+  // wid:   0          1          2     3     4     5     6     7
+  // owns:  (0,0)(3,3) (1,1)(2,2) (1,0) (2,0) (3,0) (2,1) (3,1) (3,2);  zero tile of wid 2..7:
+  //                               (0,1) (0,2) (0,3) (1,2) (1,3) (2,3)      (nibble tables, no scratch)
+  const int own = wid < 2 ? 2 : 1;
+  const int tI[2] = {(0x33232110 >> (4 * wid)) & 15, wid == 0 ? 3 : 2};
+  const int tJ[2] = {(0x21100010 >> (4 * wid)) & 15, wid == 0 ? 3 : 2};
+  const int zI = (0x21100000 >> (4 * wid)) & 15, zJ = (0x33232100 >> (4 * wid)) & 15;
+  if (wid >= 2)
+    *reinterpret_cast<uint2*>(MsT + (16 * zJ + li) * LD64 + 16 * zI + 4 * lg) = make_uint2(0u, 0u);
   __syncthreads();
-  // CB tiles for the column tile w: rows i in tile I >= w
-  f32x4 cb[4], dcb[4], dBa[NTH], dCa[NTH];
+  f32x4 cbo[2], dcbo[2], dBa[NTH], dCa[NTH];  // C.B^T and the dCB accumulators of the owned tiles
 #pragma unroll
-  for (int I = 0; I < 4; ++I) {
-    cb[I] = zero4();
-    dcb[I] = zero4();
-    if (I >= w) {
+  for (int k = 0; k < 2; ++k) {
+    cbo[k] = zero4();
+    dcbo[k] = zero4();
+    if (k < own) {
 #pragma unroll
       for (int ks = 0; ks < N / 32; ++ks)
-        cb[I] = mfma16(frag_kc(Cs, LDN, 16 * I, 32 * ks), frag_kc(Bs, LDN, 16 * w, 32 * ks), cb[I]);
+        cbo[k] = mfma16(frag_kc(Cs, LDN, 16 * tI[k], 32 * ks), frag_kc(Bs, LDN, 16 * tJ[k], 32 * ks), cbo[k]);
     }
   }
 #pragma unroll
@@ -518,59 +531,45 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
     const float cl = cumr[Q - 1];
     const float Ah = a.a_log ? -__expf(a.A[h]) : a.A[h];
     const float Dh = a.D ? a.D[h] : 0.f;
-    const float dtj = dtr[hh & 7][jl], cumj = cumr[jl];
-    // ---- (1)(2) dM, M; half 0: dCB and the G row/col sums
-    f32x4 m[4];
-    float colG = 0.f;
+    // ---- (1)(2) dM, M of the owned tiles: dCB, the G row/col sums, M^T -> LDS
 #pragma unroll
-    for (int I = 0; I < 4; ++I) {
-      m[I] = zero4();
-      if (I >= w) {
+    for (int k = 0; k < 2; ++k) {
+      if (k < own) {
+        const int I = tI[k], jt = 16 * tJ[k] + li;
+        const float dtj = dtr[hh & 7][jt], cumj = cumr[jt];
         f32x4 dm = zero4();
 #pragma unroll
         for (int ks = 0; ks < P / 32; ++ks)
-          dm = mfma16(frag_kc(dYs, LD64, 16 * I, 32 * ks), frag_kc(Xs, LD64, 16 * w, 32 * ks), dm);
-        float gr[4];
+          dm = mfma16(frag_kc(dYs, LD64, 16 * I, 32 * ks), frag_kc(Xs, LD64, 16 * tJ[k], 32 * ks), dm);
+        float gr[4], mv[4], colG = 0.f;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int i = 16 * I + 4 * lg + r;
-          const float Lij = (jl <= i) ? __expf(cumr[i] - cumj) : 0.f;
+          const float Lij = (jt <= i) ? __expf(cumr[i] - cumj) : 0.f;
           const float dmv = dm[r] * dtj;
-          const float mv = cb[I][r] * Lij;
-          m[I][r] = mv;
-          dcb[I][r] += dmv * Lij;
-          gr[r] = dmv * mv;
+          mv[r] = cbo[k][r] * Lij;
+          dcbo[k][r] += dmv * Lij;
+          gr[r] = dmv * mv[r];
           colG += gr[r];
         }
-        if (half == 0) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float rs = row_sum16(gr[r]);
-            if (li == 0) dcw[hh & 7][wid][16 * I + 4 * lg + r] += rs;
-          }
+        for (int r = 0; r < 4; ++r) {
+          const float rs = row_sum16(gr[r]);
+          if (li == 0) dcw[hh & 7][wid][16 * I + 4 * lg + r] += rs;
         }
+        colG = rows_sum4(colG);
+        if (l < 16) dcw[hh & 7][wid][jt] -= colG;
+        *reinterpret_cast<uint2*>(MsT + jt * LD64 + 16 * I + 4 * lg) = make_uint2(pack2(mv[0], mv[1]), pack2(mv[2], mv[3]));
       }
     }
-    if (half == 0) {
-      colG = rows_sum4(colG);
-      if (l < 16) dcw[hh & 7][wid][jl] -= colG;
-    }
-    // ---- (3) dXdt = M^T dY, (4) BdS = B dS^T, (6) Yoff = C S^T  for this half's p-tiles
+    // ---- (4) BdS = B dS^T, (6) Yoff = C S^T for this half's p-tiles (independent of M: they fill the
+    // wait for the M^T barrier), then (3) dXdt = M^T dY
     f32x4 dxd[2], bds[2], yo[2];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       dxd[q] = zero4();
       bds[q] = zero4();
       yo[q] = zero4();
-    }
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      if (2 * ks + 1 >= w) {
-        const bf16x8 Af = acc_frag(m[2 * ks], m[2 * ks + 1]);
-#pragma unroll
-        for (int q = 0; q < 2; ++q)
-          dxd[q] = mfma16(Af, frag_tr_perm(dYs, LD64, 32 * ks, 16 * (2 * half + q)), dxd[q]);
-      }
     }
 #pragma unroll
     for (int ks = 0; ks < N / 32; ++ks) {
@@ -580,6 +579,16 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
       for (int q = 0; q < 2; ++q) {
         bds[q] = mfma16(Ab, frag_kc(dSs, LDN, 16 * (2 * half + q), 32 * ks), bds[q]);
         yo[q] = mfma16(Ac, frag_kc(Ss, LDN, 16 * (2 * half + q), 32 * ks), yo[q]);
+      }
+    }
+    __syncthreads();  // M^T complete
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      if (2 * ks + 1 >= w) {
+        const bf16x8 Af = frag_kc(MsT, LD64, 16 * w, 32 * ks);
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          dxd[q] = mfma16(Af, frag_tr(dYs, LD64, 32 * ks, 16 * (2 * half + q)), dxd[q]);
       }
     }
     // ---- (5) dX, ddt_direct, U, dD ; (6) dcum Yoff term   (rows j = i = 16w + 4lg + r)
@@ -664,14 +673,17 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
   }
   // ---- head-group partials
   const int64_t pbase = ((int64_t)b * a.nc + c) * a.nhg + hgi;
-  if (half == 0) {
 #pragma unroll
-    for (int I = 0; I < 4; ++I)
+  for (int k = 0; k < 2; ++k) {
+    if (k < own) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = 16 * I + 4 * lg + r;
-        a.part_dcb[(pbase * Q + i) * Q + jl] = dcb[I][r];
-      }
+      for (int r = 0; r < 4; ++r)
+        a.part_dcb[(pbase * Q + 16 * tI[k] + 4 * lg + r) * Q + 16 * tJ[k] + li] = dcbo[k][r];
+    }
+  }
+  if (wid >= 2) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) a.part_dcb[(pbase * Q + 16 * zI + 4 * lg + r) * Q + 16 * zJ + li] = 0.f;
   }
 #pragma unroll
   for (int nt = 0; nt < NTH; ++nt)

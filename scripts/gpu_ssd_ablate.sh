@@ -8,5 +8,5 @@ for m in ${ABL:-0 1 2 4}; do
   MAMBA_AMD_SSD_ABLATE=$m timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv \
     -d gpurun_out/abl/m$m -o run -- python3 scripts/kbench.py --only ssd --reps 10 > gpurun_out/abl/m$m.log 2>&1 || exit 1
   f=$(find gpurun_out/abl/m$m -name "*kernel_stats.csv" | head -1)
-  echo "== ablate $m"; python scripts/prof_summary.py "$f" 1 6 | grep ssd_
+  echo "== ablate $m"; python scripts/prof_summary.py "$f" 1 8 | grep -E "ssd_chunk_bwd|ssd_dstate|ssd_fused"
 done
