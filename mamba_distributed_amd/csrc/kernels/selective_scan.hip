@@ -14,6 +14,7 @@
 //  * deterministic everywhere: every partial has exactly one writer, reductions run in fixed order.
 #include "common.h"
 #include "selective_scan.h"
+#include <cstdlib>
 #include <type_traits>
 
 namespace mamba_amd {
@@ -250,6 +251,160 @@ __global__ __launch_bounds__(256) void selscan_fwd_k(SelScanArgs a) {
     store_items<VEC, T, SF_IT>(orow, tl, a.L, y);
   }
   if (a.last_state && lane < N) a.last_state[(int64_t)row * N + lane] = hc[lane];
+}
+
+typedef float ss_f2 __attribute__((ext_vector_type(2)));
+
+// ---- forward, wave-per-state-group form (bf16, N = 16, D % 64 == 0) ---------------------------
+// A workgroup owns 64 channels of one batch row; lane = channel, wave w owns states 4w .. 4w+3.  Time is
+// walked sequentially in 16-step tiles with the 4 states of a channel in registers (two float2 pairs),
+// so there is no scan at all, and B / C -- which do not depend on the channel -- are the same for every
+// lane of a wave: they come from SCALAR loads (SGPR operands of the packed math), so the step loop reads
+// nothing per lane but dt and dt*u (staged once per tile in LDS for the 4 waves).  Per step and lane:
+// 2 v_pk_mul (dt A), 4 exp, 2 v_pk_mul (dt u B), 2 v_pk_fma (h), 2 v_pk_fma (C h).  The 4 waves' partial
+// y meet in LDS at the end of the tile; (y + D u) silu(z) leaves as coalesced rows.
+constexpr int SG_T = 16, SG_D = 4;  // tile length, tiles of u / delta / z in flight
+__global__ __launch_bounds__(256) void selscan_fwd_sg_k(SelScanArgs a) {
+  constexpr int N = 16;
+  __shared__ __attribute__((aligned(16))) float dlS[64][SG_T + 4], duS[64][SG_T + 4];
+  __shared__ __attribute__((aligned(16))) float yS[4][64][SG_T + 4];
+  __shared__ __attribute__((aligned(16))) bf16_t uS[64][SG_T];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int wgs_per_b = a.D / 64;
+  const int b = blockIdx.x / wgs_per_b, d0 = (blockIdx.x % wgs_per_b) * 64;
+  const int g = d0 / (a.D / a.G);
+  const int d = d0 + lane;  // step loop: this lane's channel
+  // staging / epilogue role: channel sr = tid >> 2, 4 steps at 4 * (tid & 3)
+  const int sr = threadIdx.x >> 2, sc = (threadIdx.x & 3) * 4;
+  const bf16_t* urow = ((const bf16_t*)a.u_) + (int64_t)b * a.sub + (int64_t)(d0 + sr) * a.sud;
+  const bf16_t* drow = ((const bf16_t*)a.delta_) + (int64_t)b * a.sdb + (int64_t)(d0 + sr) * a.sdd;
+  const bf16_t* zrow = a.z_ ? ((const bf16_t*)a.z_) + (int64_t)b * a.szb + (int64_t)(d0 + sr) * a.szd : nullptr;
+  bf16_t* orow = ((bf16_t*)a.out_) + (int64_t)b * a.sob + (int64_t)(d0 + sr) * a.sod;
+  const float sbias = a.delta_bias ? a.delta_bias[d0 + sr] : 0.f;
+  const float sD = a.D_ ? a.D_[d0 + sr] : 0.f;
+  const bf16_t* Bw = ((const bf16_t*)a.Bm_) + (int64_t)b * a.sBb + (int64_t)g * a.sBg + (int64_t)(4 * w) * a.sBn;
+  const bf16_t* Cw = ((const bf16_t*)a.Cm_) + (int64_t)b * a.sCb + (int64_t)g * a.sCg + (int64_t)(4 * w) * a.sCn;
+  ss_f2 A2[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) A2[p] = ss_f2{a.A[d * N + 4 * w + 2 * p], a.A[d * N + 4 * w + 2 * p + 1]} * kLog2e;
+  ss_f2 h[2] = {ss_f2{0.f, 0.f}, ss_f2{0.f, 0.f}};
+  const int nck = (a.L + SB_T - 1) / SB_T;
+  const int ntile = (a.L + SG_T - 1) / SG_T;
+  // SG_D-deep ring of this thread's u / delta / z pieces (8 B each): each tile's data was requested
+  // SG_D tiles earlier, so the short tiles never wait for HBM
+  struct Ring { uint2 u, dl, z; };
+  Ring ring[SG_D];
+  auto fetch = [&](Ring& r, int tile) {  // clamped to L - 4 (L % 8 == 0): always legal
+    const int t = min(tile * SG_T + sc, a.L - 4);
+    r.u = *reinterpret_cast<const uint2*>(urow + t);
+    r.dl = *reinterpret_cast<const uint2*>(drow + t);
+    r.z = zrow ? *reinterpret_cast<const uint2*>(zrow + t) : make_uint2(0u, 0u);
+  };
+  // B / C rows (this wave's 4 states x 16 steps = 64 dwords) of the NEXT tile in flight during the
+  // current one, one dword per lane (lane = 16 n + 8 [C] + j), moved to SGPRs with v_readlane
+  const int bl_n = lane >> 4, bl_m = (lane >> 3) & 1, bl_j = lane & 7;
+  const bf16_t* blrow = (bl_m ? Cw + (int64_t)bl_n * a.sCn : Bw + (int64_t)bl_n * a.sBn) + 2 * bl_j;
+  uint32_t bc = 0u;
+  auto fetch_bc = [&](int tile) { bc = *reinterpret_cast<const uint32_t*>(blrow + min(tile * SG_T, a.L - SG_T)); };
+#pragma unroll
+  for (int k = 0; k < SG_D; ++k) fetch(ring[k], k);
+  fetch_bc(0);
+  auto do_tile = [&](Ring& r, int tile) {
+    const int t0 = tile * SG_T;
+    __syncthreads();  // the previous tile's readers are done
+    {
+      const float u[4] = {__uint_as_float(r.u.x << 16), __uint_as_float(r.u.x & 0xffff0000u),
+                          __uint_as_float(r.u.y << 16), __uint_as_float(r.u.y & 0xffff0000u)};
+      const float raw[4] = {__uint_as_float(r.dl.x << 16), __uint_as_float(r.dl.x & 0xffff0000u),
+                            __uint_as_float(r.dl.y << 16), __uint_as_float(r.dl.y & 0xffff0000u)};
+      float dl[4], du[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float v = raw[i] + sbias;
+        dl[i] = (t0 + sc + i < a.L) ? (a.softplus ? softplus_fast(v) : v) : 0.f;
+        du[i] = dl[i] * u[i];
+      }
+      *reinterpret_cast<float4*>(&dlS[sr][sc]) = make_float4(dl[0], dl[1], dl[2], dl[3]);
+      *reinterpret_cast<float4*>(&duS[sr][sc]) = make_float4(du[0], du[1], du[2], du[3]);
+      *reinterpret_cast<uint2*>(&uS[sr][sc]) = r.u;
+    }
+    const uint2 zc = r.z;
+    uint32_t Bq[4][SG_T / 2], Cq[4][SG_T / 2];
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int j = 0; j < SG_T / 2; ++j) {
+        Bq[n][j] = __builtin_amdgcn_readlane(bc, 16 * n + j);
+        Cq[n][j] = __builtin_amdgcn_readlane(bc, 16 * n + 8 + j);
+      }
+    __syncthreads();
+    fetch(r, min(tile + SG_D, ntile - 1));
+    fetch_bc(min(tile + 1, ntile - 1));
+    if (a.carries && t0 % SB_T == 0)
+      *reinterpret_cast<float4*>(a.carries + (((int64_t)b * a.D + d) * nck + t0 / SB_T) * N + 4 * w) =
+          make_float4(h[0].x, h[0].y, h[1].x, h[1].y);
+#pragma unroll
+    for (int t4 = 0; t4 < SG_T; t4 += 4) {
+      const float4 dl4 = *reinterpret_cast<const float4*>(&dlS[lane][t4]);
+      const float4 du4 = *reinterpret_cast<const float4*>(&duS[lane][t4]);
+      const float dlv[4] = {dl4.x, dl4.y, dl4.z, dl4.w}, duv[4] = {du4.x, du4.y, du4.z, du4.w};
+      float yv[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int t = t4 + k;
+        const int j = t >> 1;
+        const bool hi = t & 1;
+        ss_f2 y2 = ss_f2{0.f, 0.f};
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const uint32_t b0 = Bq[2 * p][j], b1 = Bq[2 * p + 1][j], c0 = Cq[2 * p][j], c1 = Cq[2 * p + 1][j];
+          const ss_f2 Bp = ss_f2{__uint_as_float(hi ? (b0 & 0xffff0000u) : (b0 << 16)),
+                                 __uint_as_float(hi ? (b1 & 0xffff0000u) : (b1 << 16))};
+          const ss_f2 Cp = ss_f2{__uint_as_float(hi ? (c0 & 0xffff0000u) : (c0 << 16)),
+                                 __uint_as_float(hi ? (c1 & 0xffff0000u) : (c1 << 16))};
+          const ss_f2 e = A2[p] * dlv[k];
+          const ss_f2 av = ss_f2{__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
+          h[p] = __builtin_elementwise_fma(av, h[p], Bp * duv[k]);
+          y2 = __builtin_elementwise_fma(Cp, h[p], y2);
+        }
+        yv[k] = y2.x + y2.y;
+      }
+      *reinterpret_cast<float4*>(&yS[w][lane][t4]) = make_float4(yv[0], yv[1], yv[2], yv[3]);
+    }
+    __syncthreads();  // all 4 waves' partial y of the tile are in LDS
+    if (t0 + sc < a.L) {
+      float y[4];
+      const float4 y0 = *reinterpret_cast<const float4*>(&yS[0][sr][sc]);
+      const float4 y1 = *reinterpret_cast<const float4*>(&yS[1][sr][sc]);
+      const float4 y2 = *reinterpret_cast<const float4*>(&yS[2][sr][sc]);
+      const float4 y3 = *reinterpret_cast<const float4*>(&yS[3][sr][sc]);
+      y[0] = (y0.x + y1.x) + (y2.x + y3.x);
+      y[1] = (y0.y + y1.y) + (y2.y + y3.y);
+      y[2] = (y0.z + y1.z) + (y2.z + y3.z);
+      y[3] = (y0.w + y1.w) + (y2.w + y3.w);
+      float u[4];
+      ld4<bf16_t>(&uS[sr][sc], u);
+      const float z[4] = {__uint_as_float(zc.x << 16), __uint_as_float(zc.x & 0xffff0000u),
+                          __uint_as_float(zc.y << 16), __uint_as_float(zc.y & 0xffff0000u)};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        y[i] = fmaf(sD, u[i], y[i]);
+        if (zrow) y[i] *= siluf_(z[i]);
+      }
+      st4<bf16_t>(orow + t0 + sc, y);
+    }
+  };
+  int tile = 0;
+  for (; tile + SG_D <= ntile; tile += SG_D) {
+#pragma unroll
+    for (int k = 0; k < SG_D; ++k) do_tile(ring[k], tile + k);
+  }
+#pragma unroll
+  for (int k = 0; k < SG_D; ++k)
+    if (tile + k < ntile) do_tile(ring[k], tile + k);
+  if (a.last_state)
+    *reinterpret_cast<float4*>(a.last_state + ((int64_t)b * a.D + d) * N + 4 * w) =
+        make_float4(h[0].x, h[0].y, h[1].x, h[1].y);
 }
 
 // ============================== backward =======================================================
@@ -944,6 +1099,15 @@ hipError_t launch_selscan_fwd(const SelScanArgs& a, hipStream_t st) {
   const int64_t rows = (int64_t)a.B * a.D;
   dim3 grid((unsigned)((rows + 3) / 4)), block(256);
   const bool v = a.dtype == kBF16 && a.vec && a.vecbc && (!a.z_ || a.vecz) && a.L % SF_IT == 0;
+  // sequential-time walk (wave per state group, lane per channel) when the batch has the channels to fill
+  // the GPU (>= 2048 wavefronts); MAMBA_AMD_SELSCAN_LC=0 forces the time-parallel kernel (A/B, tests).
+  // Measured at B=32, D=1536, L=1024, N=16 on MI355X: 290 us vs 345 us.
+  const char* lce = std::getenv("MAMBA_AMD_SELSCAN_LC");
+  if (v && (!lce || std::atoi(lce) != 0) && a.N == 16 && a.D % 64 == 0 && (a.D / a.G) % 64 == 0 &&
+      (int64_t)a.B * a.D / 16 >= 2048) {
+    hipLaunchKernelGGL(selscan_fwd_sg_k, dim3((unsigned)(a.B * (a.D / 64))), dim3(256), 0, st, a);
+    return hipGetLastError();
+  }
   if (v) SS_DISPATCH(hipLaunchKernelGGL((selscan_fwd_k<TT, NN, true>), grid, block, 0, st, a));
   else SS_DISPATCH(hipLaunchKernelGGL((selscan_fwd_k<TT, NN, false>), grid, block, 0, st, a));
   return hipGetLastError();

@@ -121,12 +121,15 @@ def main():
         res["ce_fwd_inplace_grad"] = (t, 2 * logits.numel() * 2)
     if "selscan" in only:
         d, n = 1536, 16
-        u = torch.randn(d, B, L, device=dev).to(torch.bfloat16).permute(1, 0, 2)
-        delta = (torch.randn(d, B, L, device=dev) * 0.5 - 1).to(torch.bfloat16).permute(1, 0, 2)
+        # the Mamba-1 layer's layouts: u / delta / z channel-major per batch row (b, d, l), B / C (b, 1, n, l)
+        # (the previous (d, b, l)-permuted views put consecutive channels 64 KB apart, an HBM stride
+        # the model never produces)
+        xz = torch.randn(B, 2 * d, L, device=dev).to(torch.bfloat16)
+        u, z = xz[:, :d], xz[:, d:]
+        delta = (torch.randn(B, d, L, device=dev) * 0.5 - 1).to(torch.bfloat16)
         A = -torch.rand(d, n, device=dev) * 4
-        Bm = torch.randn(n, B, L, device=dev).to(torch.bfloat16).permute(1, 0, 2).unsqueeze(1)
-        Cm = torch.randn(n, B, L, device=dev).to(torch.bfloat16).permute(1, 0, 2).unsqueeze(1)
-        z = torch.randn(d, B, L, device=dev).to(torch.bfloat16).permute(1, 0, 2)
+        Bm = torch.randn(B, 1, n, L, device=dev).to(torch.bfloat16)
+        Cm = torch.randn(B, 1, n, L, device=dev).to(torch.bfloat16)
         D = torch.randn(d, device=dev)
         db = torch.randn(d, device=dev)
         out, carries, last = ops.selscan_fwd(u, delta, A, Bm, Cm, D, z, db, True)

@@ -769,3 +769,32 @@ def test_ssd_walk_matches_sequential_kernels(cuda, monkeypatch, b, L, H):
         outs.append([y, fin] + [t.grad for t in xs])
     for nm, a_, b_ in zip(["y", "final", "dx", "ddt", "dB", "dC", "dinit"], *outs):
         assert rel(a_, b_) < 1e-2, (nm, rel(a_, b_))
+
+
+@pytest.mark.parametrize("L,with_z", [(256, True), (1008, False)])
+def test_selective_scan_channel_walk(cuda, monkeypatch, L, with_z):
+    """Forward at a channel count that selects the sequential-time walk (B * D / 16 >= 2048):
+    against the fp32 reference and bitwise-stable vs the time-parallel kernel's saved carries (the
+    backward consumes them), including a partial last 32-step tile (L = 1008) and the last state."""
+    from mamba_distributed_amd.ops.selective_scan import selective_scan_fn
+    torch.manual_seed(6)
+    b, d, n = 8, 4096, 16
+    u = torch.randn(b, d, L, device=cuda).to(torch.bfloat16)
+    delta = (torch.randn(b, d, L, device=cuda) * 0.5 - 1).to(torch.bfloat16)
+    A = -torch.rand(d, n, device=cuda) * 4 - 0.1
+    Bm = torch.randn(b, 1, n, L, device=cuda).to(torch.bfloat16)
+    Cm = torch.randn(b, 1, n, L, device=cuda).to(torch.bfloat16)
+    D = torch.randn(d, device=cuda)
+    z = torch.randn(b, d, L, device=cuda).to(torch.bfloat16) if with_z else None
+    db = torch.randn(d, device=cuda) * 0.3
+    ops = torch.ops.mamba_amd
+    outs = {}
+    for lc in ("1", "0"):
+        monkeypatch.setenv("MAMBA_AMD_SELSCAN_LC", lc)
+        outs[lc] = ops.selscan_fwd(u, delta, A, Bm, Cm, D, z, db, True)
+    y_ref = R.selective_scan_ref(u, delta, A, Bm, Cm, D, z=z, delta_bias=db, delta_softplus=True)
+    assert rel(outs["1"][0], y_ref) < 2e-2
+    for i in range(3):  # out, carries, last state
+        assert rel(outs["1"][i], outs["0"][i]) < 1e-2, i
+    y = selective_scan_fn(u, delta, A, Bm, Cm, D, z=z, delta_bias=db, delta_softplus=True)
+    assert rel(y, y_ref) < 2e-2
