@@ -80,6 +80,7 @@ class _CausalConv1dVarFn(torch.autograd.Function):
         ctx.silu, ctx.wshape, ctx.params = silu, weight.shape, (weight, bias)
         ctx.has_init, ctx.init_dtype = initial_states is not None, getattr(initial_states, "dtype", None)
         ctx.ret_final = return_final
+        ctx.set_materialize_grads(False)
         if not return_final:
             ctx.mark_non_differentiable(fin)
         return out.transpose(1, 2), fin
@@ -87,6 +88,8 @@ class _CausalConv1dVarFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout, dfin):
         xt, w2, bias, seq_idx, init = ctx.saved_tensors
+        if dout is None:
+            dout = torch.zeros_like(xt).transpose(1, 2)
         dx, dw, db, dinit = _ext.ops().conv1d_cl_var_bwd(xt, w2, bias, dout.transpose(1, 2), ctx.silu, seq_idx,
                                                          init, dfin if ctx.ret_final else None, None)
         pw, pb = ctx.params

@@ -47,6 +47,7 @@ class _SSDFn(torch.autograd.Function):
         ctx.flags = (dt_softplus, dt_min, dt_max)
         ctx.return_final = return_final_states
         ctx.params = (A, D, dt_bias)
+        ctx.set_materialize_grads(False)
         if return_final_states:
             return y, final
         return y
@@ -56,6 +57,8 @@ class _SSDFn(torch.autograd.Function):
         x, dt, A, B, C, D, dt_bias, init, cum, dtp, states = ctx.saved_tensors
         dfinal = rest[0] if ctx.return_final and len(rest) else None
         softplus, dt_min, dt_max = ctx.flags
+        if dy is None:
+            dy = torch.zeros_like(x)
         g = _ext.ops().ssd_bwd(dy.contiguous(), x, dt, A, B, C, D, dt_bias, init, cum, dtp, states,
                                dfinal, NATIVE_CHUNK, softplus, dt_min, dt_max, None, None, None, None)
         dx, ddt, dA, dB, dC, dD, ddt_bias, dinit = g
@@ -126,6 +129,9 @@ class _Mamba2InnerFn(torch.autograd.Function):
         ctx.wshape = conv_w.shape
         ctx.params = (conv_w, conv_b, dt_bias, A, D, norm_w)
         ctx.ret_final = return_final_states
+        # unused outputs (final when not requested) must not get materialised zero gradients: that was a
+        # 25 MB fill per layer per micro-step at the 280M shape
+        ctx.set_materialize_grads(False)
         if not return_final_states:
             ctx.mark_non_differentiable(final)
         return yn.view(b, l, di), final
@@ -134,6 +140,9 @@ class _Mamba2InnerFn(torch.autograd.Function):
     def backward(ctx, dyn, dfinal):
         (zxbcdt, w2, conv_b, dt_bias, A, D, norm_w, xBC_c, y, rstd, cum, dtp, states, init,
          seq_idx) = ctx.saved_tensors
+        if dyn is None:
+            dyn = torch.zeros(zxbcdt.shape[0], zxbcdt.shape[1], dt_bias.shape[0] * ctx.meta[1],
+                              device=zxbcdt.device, dtype=zxbcdt.dtype)
         eps, headdim, ngroups, d_state, dt_min, dt_max, nbg, a_log = ctx.meta
         ops = _ext.ops()
         b, l, dproj = zxbcdt.shape
