@@ -63,6 +63,24 @@ def _wgrad_native(p, dy2: torch.Tensor, x2: torch.Tensor):
     return dw
 
 
+def _native_dgrad_ok(dy2: torch.Tensor, w: torch.Tensor) -> bool:
+    """Opt-in (MAMBA_AMD_NATIVE_DGRAD=1): the input gradient dX = dY W on the native pipelined engine for
+    short contractions (K = out_features <= 1024, the out_proj of the d_model=768 models).  In isolation it
+    is 3% faster than the tuned hipBLASLt solution (91.6-94 vs 94-97 us, profiles/r2_v3_gemm_pipe_bench.log)
+    but the whole 280M step is 1% slower with it (276.6k vs 279.3k tok/s, interleaved A/B,
+    profiles/r2_v5_ab_native_dgrad.txt: its 128 KB-LDS workgroups crowd the overlapped micro-batch's
+    kernels), so hipBLASLt stays the default."""
+    import os
+    return (os.environ.get("MAMBA_AMD_NATIVE_DGRAD", "0") == "1" and dy2.dtype == torch.bfloat16
+            and w.dtype == torch.bfloat16 and dy2.is_cuda and w.is_contiguous() and w.shape[0] <= 1024
+            and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0 and dy2.shape[0] >= 4096)
+
+
+def _dgrad_native(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """dX (T, in) = dY (T, out) . W (out, in): A k-contiguous, B (k rows, n contiguous), bf16 epilogue."""
+    return _ext.ops().gp_mm(dy2, w, None, 0, 1, 0, 1, 256)
+
+
 class _ProjFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, cd):
@@ -83,7 +101,9 @@ class _ProjFn(torch.autograd.Function):
             dy2 = dy2.to(w.dtype)
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
-        dx = torch.mm(dy2, w) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = _dgrad_native(dy2, w) if _native_dgrad_ok(dy2, w) else torch.mm(dy2, w)
         dw = None
         if ctx.needs_input_grad[1]:
             p = ctx.param
