@@ -144,7 +144,9 @@ def _ssd_inputs(cuda, b, L, H, G, N, seed=0, strided=True):
     return x.contiguous() if not strided else x, dt, A, Bm, Cm, D, dt_bias
 
 
-@pytest.mark.parametrize("b,L,H,G,N", [(2, 256, 4, 1, 128), (1, 200, 8, 2, 64), (2, 70, 6, 1, 128)])
+@pytest.mark.parametrize("b,L,H,G,N", [(2, 256, 4, 1, 128), (1, 200, 8, 2, 64), (2, 70, 6, 1, 128),
+                                       (4, 1024, 24, 1, 128),   # the 280M headline shape (16 chunks, 24 heads)
+                                       (1, 8192, 8, 1, 128)])   # the 2.8B long-sequence shape (128 chunks)
 def test_ssd_fwd_bwd(cuda, b, L, H, G, N):
     from mamba_distributed_amd.ops.ssd import mamba_chunk_scan_combined
     x, dt, A, Bm, Cm, D, dt_bias = _ssd_inputs(cuda, b, L, H, G, N)
@@ -278,6 +280,36 @@ def test_model_native_vs_reference(cuda, layer):
     m = LMHeadModel(cfg, device=cuda)
     x = torch.randint(0, 1024, (2, 192), device=cuda)
     y = torch.randint(0, 1024, (2, 192), device=cuda)
+
+    def lossgrad(force_ref):
+        if force_ref:
+            os.environ["MAMBA_AMD_FORCE_REFERENCE"] = "1"
+        try:
+            m.zero_grad(set_to_none=True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                _, loss = m(x, y)
+            loss.backward()
+            return loss.item(), {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+        finally:
+            os.environ.pop("MAMBA_AMD_FORCE_REFERENCE", None)
+
+    ln, gn = lossgrad(False)
+    lr, gr = lossgrad(True)
+    assert abs(ln - lr) < 1e-2 * abs(lr), (ln, lr)
+    bad = {n: rel(gn[n], gr[n]) for n in gr if rel(gn[n], gr[n]) > 5e-2}
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("layer", ["Mamba1", "Mamba2"])
+def test_model_native_vs_reference_headline_width(cuda, layer):
+    """The 280M configs' layer width and sequence length (d_model 768, T=1024, 16 SSD chunks, 24 heads)
+    through 2 layers: loss and every parameter gradient, native kernels vs the fp32 reference ops."""
+    from mamba_distributed_amd import LMHeadModel, MambaConfig
+    torch.manual_seed(0)
+    cfg = MambaConfig(d_model=768, n_layer=2, vocab_size=4096, ssm_cfg={"layer": layer})
+    m = LMHeadModel(cfg, device=cuda)
+    x = torch.randint(0, 4096, (2, 1024), device=cuda)
+    y = torch.randint(0, 4096, (2, 1024), device=cuda)
 
     def lossgrad(force_ref):
         if force_ref:
