@@ -155,7 +155,7 @@ __global__ __launch_bounds__(256) void ssd_fused_fwd_k(SSDArgs a) {
   __shared__ __attribute__((aligned(16))) float cumr[Q], dtr[Q], wjr[Q];  // wjr = e^{cl-cum_j} dt_j
   const int h = blockIdx.x, b = blockIdx.y;
   const int g = h / (a.H / a.G);
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;  // wave-uniform: scalar branches
   const int li = l & 15, lg = l >> 4;
   const float* cumbh = a.cum + ((int64_t)b * a.H + h) * a.Lp;
   const float* dtbh = a.dtp + ((int64_t)b * a.H + h) * a.Lp;
@@ -320,7 +320,7 @@ __global__ __launch_bounds__(256) void ssd_dstate_bwd_k(SSDArgs a) {
   __shared__ float er[Q];
   const int h = blockIdx.x, b = blockIdx.y;
   const int g = h / (a.H / a.G);
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;  // wave-uniform: scalar branches
   const float* cumbh = a.cum + ((int64_t)b * a.H + h) * a.Lp;
   const bf16_t* yg = a.dy + (int64_t)b * a.sdyb + (int64_t)h * a.sdyh;
   const bf16_t* cg = a.Cm + (int64_t)b * a.sCb + (int64_t)g * a.sCg;
@@ -409,7 +409,7 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
   __shared__ float redw[8][8];     // [head][wave]        dD
   const int c = blockIdx.x, hgi = blockIdx.y, b = blockIdx.z;
   const int h0 = hgi * a.HG, g = h0 / (a.H / a.G);
-  const int wid = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;  // wave-uniform: scalar branches
   const int w = wid & 3, half = wid >> 2;
   const int li = l & 15, lg = l >> 4;
   const int valid = min(Q, a.L - c * Q);
@@ -705,7 +705,7 @@ __global__ __launch_bounds__(256) void ssd_dbc_bwd_k(SSDArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t Os[Q * LDN];
   __shared__ __attribute__((aligned(16))) bf16_t dCBs[Q * LD64];
   const int c = blockIdx.x, g = blockIdx.y, b = blockIdx.z;
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;  // wave-uniform: scalar branches
   const int valid = min(Q, a.L - c * Q);
   const int hpg = a.H / a.G;
   const int hg0 = g * hpg / a.HG, hg1 = (g + 1) * hpg / a.HG;
@@ -781,7 +781,7 @@ __global__ __launch_bounds__(256) void ssd_walk_k(SSDArgs a) {
   const int lid = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x));  // neighbours share an L2
   const int nb = lid % nblk, h = (lid / nblk) % a.H, b = lid / (nblk * a.H);
   const int g = h / (a.H / a.G);
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, li = l & 15, lg = l >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63, li = l & 15, lg = l >> 4;
   const int n0 = 64 * nb;
   const float* __restrict__ cumbh = a.cum + ((int64_t)b * a.H + h) * a.Lp;
   const float* __restrict__ dtbh = a.dtp + ((int64_t)b * a.H + h) * a.Lp;
@@ -925,7 +925,7 @@ __global__ __launch_bounds__(256) void ssd_chunk_fwd_k(SSDArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t Ys[Q * LD64];  // y of the previous head, [i][p]
   const int c = blockIdx.x, hgi = blockIdx.y, b = blockIdx.z;
   const int h0 = hgi * a.HGf, g = h0 / (a.H / a.G);
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, li = l & 15, lg = l >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63, li = l & 15, lg = l >> 4;
   const int valid = min(Q, a.L - c * Q);
   stage_tile<Q, N>(Cs, LDN, a.Cm + (int64_t)b * a.sCb + (int64_t)c * Q * a.sCl + (int64_t)g * a.sCg, a.sCl, valid);
   stage_tile<Q, N>(Bs, LDN, a.Bm + (int64_t)b * a.sBb + (int64_t)c * Q * a.sBl + (int64_t)g * a.sBg, a.sBl, valid);
