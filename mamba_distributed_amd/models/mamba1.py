@@ -92,10 +92,54 @@ class _InProjCMFn(torch.autograd.Function):
 
 
 def _wgrad_native(p, dY, X, dy_cm, x_cm):
-    """Weight gradient of a channel-major projection on the native wgrad GEMM (csrc/kernels/gemm.hip,
-    CM / CMB variants): fp32, added in place into ``p.grad`` on the no-sync micro-steps (side stream,
-    ops/grad_accum.py), otherwise returned through grad_accum.defer.  Returns (handled, dw);
-    handled is False when the layout is not supported and the caller must fall back."""
+    """Weight gradient of a channel-major projection.  Default: ``_wgrad_native_cm`` (gemm_wgrad_cm,
+    reduced every micro-step).  MAMBA_AMD_M1_DEFER_WGRAD=1: dW (P, Q) = sum over tokens of dY x X on the native
+    pipelined GEMM engine (csrc/kernels/gemm_pipe.hip; k-contiguous / k-row operand layouts) with fp32
+    split-K slabs that persist across the micro-steps of an optimizer step (ops/grad_accum.deferred):
+    no-sync micro-steps add their slabs on the side stream and return nothing, the sync micro-step
+    reduces once.  Returns (handled, dw); handled is False when the layout is not supported."""
+    ops = _ext.ops()
+    P = dY.shape[0] if dy_cm else dY.shape[1]
+    Q = X.shape[0] if x_cm else X.shape[1]
+    T = dY.shape[1] if dy_cm else dY.shape[0]
+    ok = (dY.dtype == torch.bfloat16 and X.dtype == torch.bfloat16 and dY.stride(1) == 1 and X.stride(1) == 1
+          and dY.stride(0) % 8 == 0 and X.stride(0) % 8 == 0 and T % 8 == 0 and Q % 4 == 0
+          and dY.data_ptr() % 16 == 0 and X.data_ptr() % 16 == 0 and (X.shape[0] if x_cm else T) % 8 == 0
+          and (dY.shape[0] if dy_cm else T) % 8 == 0)
+    if not ok or os.environ.get("MAMBA_AMD_M1_DEFER_WGRAD", "0") != "1":
+        return _wgrad_native_cm(p, dY, X, dy_cm, x_cm)
+    la, lb = (0 if dy_cm else 1), (0 if x_cm else 1)
+    S = ops.gp_splits(P, Q, T)
+    d = grad_accum.deferred(p, "wgrad_cm", (S, P, Q), dY.device)
+    if d is None:  # outside an accumulation scope: transient slabs, reduce now
+        part = ops.gp_mm(dY, X, None, la, lb, 1, S, 256)
+        dw = torch.empty(P, Q, device=dY.device, dtype=torch.float32)
+        ops.gp_reduce(part, dw, False)
+        return True, grad_accum.defer(p, dw.to(p.dtype))
+    buf, mode = d
+    slab_mode = 1 if mode in (1, 3) else 2  # store / add
+    if mode <= 2:
+        side = grad_accum.side_stream(dY.device)
+        if side is None:
+            ops.gp_mm(dY, X, buf, la, lb, slab_mode, S, 256)
+        else:
+            side.wait_stream(torch.cuda.current_stream(dY.device))
+            with torch.cuda.stream(side):
+                ops.gp_mm(dY, X, buf, la, lb, slab_mode, S, 256)
+            dY.record_stream(side)
+            X.record_stream(side)
+        return True, None
+    ops.gp_mm(dY, X, buf, la, lb, slab_mode, S, 256)
+    dw = torch.empty(P, Q, device=dY.device, dtype=torch.float32)
+    ops.gp_reduce(buf, dw, False)
+    return True, grad_accum.defer(p, dw.to(p.dtype))
+
+
+def _wgrad_native_cm(p, dY, X, dy_cm, x_cm):
+    """Default Mamba-1 weight gradient: gemm_wgrad_cm, reduced every micro-step (added in place into
+    ``p.grad`` on the no-sync micro-steps).  The deferred-slab alternative measured 0.7% slower on the
+    whole Mamba-1 280M step (180.0k vs 181.2k tok/s, profiles/r2_v5_ab_m1_defer_wgrad.txt): the skinny
+    x_proj / dt_proj products (Q = 48, P = 80) suit gemm_wgrad_cm's tiles better than the 256x256 engine."""
     M = dY.shape[1] if dy_cm else dY.shape[0]
     ok = (dY.dtype == torch.bfloat16 and X.dtype == torch.bfloat16 and dY.stride(1) == 1 and X.stride(1) == 1
           and M % 64 == 0 and dY.stride(0) % 8 == 0 and X.stride(0) % 8 == 0 and dY.shape[0] % 8 == 0
