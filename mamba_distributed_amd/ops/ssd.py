@@ -82,9 +82,13 @@ def mamba_chunk_scan_combined(x, dt, A, B, C, chunk_size=256, D=None, z=None, dt
     upstream, with unchanged gradients).  ``initial_states`` belong to the row's first sequence."""
     # native kernels are bf16 (the training/serving dtype); fp32 activations (e.g. the reference's
     # fp32 HellaSwag eval) take the fp32 reference path
-    if x.dtype == torch.bfloat16 and _ext.use_native(x) and z is None and (D is None or D.dim() == 1):
+    if x.dtype == torch.bfloat16 and _ext.use_native(x) and (D is None or D.dim() == 1):
         out = _SSDFn.apply(x, dt, A, B, C, D, dt_bias, initial_states, dt_softplus,
                            float(dt_limit[0]), float(dt_limit[1]), return_final_states, seq_idx)
+        if z is not None:  # upstream's gate y * silu(z) (elementwise, fp32 math, autograd through both)
+            y, fin = out if return_final_states else (out, None)
+            y = (y.float() * F.silu(z.float())).to(y.dtype)
+            return (y, fin) if return_final_states else y
         return out
     return ssd_chunked_ref(x, dt, A, B, C, chunk_size, D=D, z=z, dt_bias=dt_bias,
                            dt_softplus=dt_softplus, dt_limit=dt_limit, initial_states=initial_states,

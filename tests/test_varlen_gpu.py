@@ -140,3 +140,19 @@ def test_packed_two_sequence_batch_matches_separate(cuda):
         gs.append(ui.grad)
     assert rel(yp, torch.cat(ys, 1)) < 1e-2
     assert rel(up.grad, torch.cat(gs, 1)) < 2e-2
+
+
+def test_chunk_scan_combined_with_z_native(cuda):
+    """mamba_chunk_scan_combined(z=...) runs the native SSD (plus the elementwise gate), fwd and bwd vs fp32."""
+    from mamba_distributed_amd.ops.ssd import mamba_chunk_scan_combined
+    b, L, H = 2, 200, 8
+    x, dt, A, Bm, Cm, D, dt_bias = _ssd_inputs(cuda, b, L, H, 1, 128, seed=31)
+    z = torch.randn(b, L, H, 64, device=cuda).to(torch.bfloat16)
+
+    def f(x, dt, Bm, Cm, z):
+        return mamba_chunk_scan_combined(x, dt, A, Bm, Cm, 64, D=D, z=z, dt_bias=dt_bias, dt_softplus=True)
+
+    on, orf, gn, gr = run_both(f, f, [x, dt, Bm, Cm, z])
+    assert rel(on, orf) < 2e-2
+    for nm, a, b_ in zip(["x", "dt", "B", "C", "z"], gn, gr):
+        assert rel(a, b_) < 3e-2, (nm, rel(a, b_))
