@@ -77,7 +77,7 @@ def main():
     from mamba_distributed_amd.data.loader import SyntheticTokens
     from mamba_distributed_amd.ops import grad_accum
     from mamba_distributed_amd.parallel import ddp as ddp_mod
-    from mamba_distributed_amd.parallel.microbatch import resolve_overlap, run_micro_batches
+    from mamba_distributed_amd.parallel.microbatch import auto_defer_reduce, resolve_overlap, run_micro_batches
     from mamba_distributed_amd.parallel.dist import all_reduce_avg, all_reduce_max, barrier, destroy, init_distributed
 
     info = init_distributed("auto")
@@ -116,7 +116,7 @@ def main():
 
     def step():
         ddp_mod.zero_grad(dmodel, opt)
-        with grad_accum.accumulation_scope():
+        with grad_accum.accumulation_scope(defer_reduce=auto_defer_reduce(cfg)):
             # micro-batch k+1's forward runs on a second stream beside micro-batch k's backward
             loss_acc = run_micro_batches(dmodel, loader.next_batch, accum, compute_loss,
                                          overlap=overlap)

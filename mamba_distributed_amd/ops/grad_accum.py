@@ -16,7 +16,8 @@ projection gradients.  Inside an ``accumulation_scope`` on the no-sync micro-ste
     A_log / D / dt_bias) or as K-split fp32 slabs (projection weights) are NOT reduced on the no-sync
     micro-steps at all: the kernels add into persistent per-parameter buffers (``deferred``) and the
     column sum / slab sum runs once, on the sync micro-step, whose autograd return then carries the
-    whole step's gradient (set MAMBA_AMD_DEFER_REDUCE=0 to reduce on every micro-step instead).
+    whole step's gradient.  ``accumulation_scope(defer_reduce=...)`` picks this per model
+    (parallel/microbatch.py::auto_defer_reduce); MAMBA_AMD_DEFER_REDUCE=0 / 1 forces it off / on.
 
 The last micro-step (the one that triggers DDP's bucketed all-reduce) and anything outside a scope
 use the normal autograd path, so DDP's gradient hooks fire exactly as usual.  The scope also caches
@@ -33,6 +34,7 @@ import torch
 
 _scope_depth = 0
 _direct = False
+_defer_scope = True   # deferred reductions requested by the outermost accumulation_scope
 _side = {}            # device index -> side stream for in-place weight-gradient GEMMs
 _side_dirty = set()   # devices whose side stream has work the main stream has not waited for
 _pending: List[Tuple[torch.Tensor, torch.Tensor]] = []
@@ -42,9 +44,12 @@ _bufs: Dict[Tuple[int, str], list] = {}  # (id(param), tag) -> [param, fp32 buff
 
 
 @contextlib.contextmanager
-def accumulation_scope():
-    """Wrap the micro-batch loop of ONE optimizer step (no parameter updates inside)."""
-    global _scope_depth, _direct
+def accumulation_scope(defer_reduce: bool = True):
+    """Wrap the micro-batch loop of ONE optimizer step (no parameter updates inside).
+    ``defer_reduce``: keep per-parameter partial buffers across the micro-steps (``deferred``)."""
+    global _scope_depth, _direct, _defer_scope
+    if _scope_depth == 0:
+        _defer_scope = bool(defer_reduce)
     _scope_depth += 1
     try:
         yield
@@ -102,8 +107,10 @@ def deferred(param, tag: str, shape, device):
     (sync micro-step).  A second call in the same sync micro-step starts over (3) and its gradient is
     added by autograd as usual."""
     import os
-    if (_scope_depth == 0 or not isinstance(param, torch.Tensor) or not param.requires_grad
-            or os.environ.get("MAMBA_AMD_DEFER_REDUCE", "1") == "0"):
+    if _scope_depth == 0 or not isinstance(param, torch.Tensor) or not param.requires_grad:
+        return None
+    env = os.environ.get("MAMBA_AMD_DEFER_REDUCE", "")
+    if env == "0" or (env != "1" and not _defer_scope):
         return None
     key = (id(param), tag)
     shape = tuple(int(v) for v in shape)

@@ -57,6 +57,15 @@ def auto_overlap(cfg) -> bool:
     return getattr(cfg, "d_model", 0) <= 1024
 
 
+def auto_defer_reduce(cfg) -> bool:
+    """Default for the deferred partial reductions (ops/grad_accum.py::deferred), by model width.
+    Measured on one MI355X (interleaved runs): Mamba-2 280M 272k -> 283k tok/s with deferral, but
+    Mamba-2 1.4B (d_model 2048, overlap off) 88k -> 41k: there the deferred projection slabs are
+    full-size K-split GEMMs on the weight-gradient side stream, and next to the main stream's
+    chip-filling GEMMs they serialise.  So: on for d_model <= 1024 (same crossover as overlap)."""
+    return getattr(cfg, "d_model", 0) <= 1024
+
+
 def resolve_overlap(mode, cfg) -> bool:
     """``mode``: "auto" (auto_overlap), "on"/"off", or a bool."""
     if isinstance(mode, bool):

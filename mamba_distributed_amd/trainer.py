@@ -37,7 +37,7 @@ from .parallel.api import clip_grad_norm_ as par_clip_grad_norm_
 from .parallel.api import full_state_dict, parallelize, sync_tp_grads
 from .parallel.dist import all_gather_object, all_reduce_avg, barrier, destroy, init_distributed
 from .parallel.groups import init_parallel_groups
-from .parallel.microbatch import resolve_overlap, run_micro_batches
+from .parallel.microbatch import auto_defer_reduce, resolve_overlap, run_micro_batches
 from .utils.checkpoint import latest_checkpoint, load_checkpoint, rng_state, save_checkpoint, set_rng_state
 from .utils.lr import get_lr
 
@@ -268,7 +268,7 @@ class Trainer:
         # not under TP/CP, whose per-layer collectives must be issued on one stream per communicator
         overlap = (resolve_overlap(self.a.overlap_microbatches, self.raw_model.config) and self.device_type == "cuda"
                    and not self.parallel)
-        with grad_accum.accumulation_scope():  # weights are frozen until optimizer.step()
+        with grad_accum.accumulation_scope(defer_reduce=auto_defer_reduce(self.raw_model.config)):  # weights are frozen until optimizer.step()
             loss_accum = run_micro_batches(self.model, lambda: self._batch(self.train_loader), self.grad_accum_steps,
                                            compute_loss, overlap=overlap)
         all_reduce_avg(loss_accum)

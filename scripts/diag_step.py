@@ -19,18 +19,20 @@ def main():
     from mamba_distributed_amd.ops import grad_accum
     from mamba_distributed_amd.parallel import ddp as ddp_mod
     from mamba_distributed_amd.parallel.dist import init_distributed
-    from mamba_distributed_amd.parallel.microbatch import resolve_overlap, run_micro_batches
+    from mamba_distributed_amd.parallel.microbatch import auto_defer_reduce, resolve_overlap, run_micro_batches
     from mamba_distributed_amd.utils.gemm_tuning import enable_tuned_gemms
     info = init_distributed()
     dev = info.device
     enable_tuned_gemms()
     torch.manual_seed(1337)
-    cfg = preset("mamba2-280m")
+    model_name = sys.argv[1] if len(sys.argv) > 1 else "mamba2-280m"
+    cfg = preset(model_name)
     model = LMHeadModel(cfg, device=dev)
     dmodel = ddp_mod.wrap_data_parallel(model, info, "native", 100.0, "fp32")
     opt = model.configure_optimizers(0.1, 6e-4, "cuda", False)
     loader = SyntheticTokens(32, 1024, cfg.vocab_size, 0, 1, device=dev)
     overlap = resolve_overlap("auto", cfg)
+    print("overlap", overlap, flush=True)
     accum = 16
 
     def compute_loss(x, y):
@@ -48,8 +50,11 @@ def main():
     def step():
         mark("start")
         ddp_mod.zero_grad(dmodel, opt)
-        with grad_accum.accumulation_scope():
-            loss_acc = run_micro_batches(dmodel, loader.next_batch, accum, compute_loss, overlap=overlap)
+        mark("zero_grad")
+        with grad_accum.accumulation_scope(defer_reduce=auto_defer_reduce(cfg)):
+            loss_acc = run_micro_batches(dmodel, loader.next_batch, 1, compute_loss, overlap=False)
+            mark("micro-batch 0")
+            loss_acc = run_micro_batches(dmodel, loader.next_batch, accum - 1, compute_loss, overlap=overlap)
             mark("micro-batches enqueued")
         mark("scope exited")
         norm = ddp_mod.clip_grad_norm_(dmodel, 1.0)
