@@ -76,3 +76,30 @@ def test_overlap_policy_by_width():
     assert resolve_overlap("off", preset("mamba2-280m")) is False
     assert resolve_overlap("on", preset("mamba2-1.4b")) is True
     assert resolve_overlap(True, None) is True
+
+
+def test_defer_reduce_policy_by_width(monkeypatch):
+    """auto_defer_reduce: on for d_model <= 1024; accumulation_scope(defer_reduce=...) gates
+    grad_accum.deferred, and MAMBA_AMD_DEFER_REDUCE=0/1 overrides it."""
+    import torch
+    from mamba_distributed_amd import preset
+    from mamba_distributed_amd.ops import grad_accum
+    from mamba_distributed_amd.parallel.microbatch import auto_defer_reduce
+    assert auto_defer_reduce(preset("mamba2-280m")) is True
+    assert auto_defer_reduce(preset("mamba2-1.4b")) is False
+    p = torch.nn.Parameter(torch.zeros(4))
+    monkeypatch.delenv("MAMBA_AMD_DEFER_REDUCE", raising=False)
+    try:
+        assert grad_accum.deferred(p, "t", (2, 4), p.device) is None  # outside a scope
+        with grad_accum.accumulation_scope(defer_reduce=False):
+            assert grad_accum.deferred(p, "t", (2, 4), p.device) is None
+            monkeypatch.setenv("MAMBA_AMD_DEFER_REDUCE", "1")
+            assert grad_accum.deferred(p, "t", (2, 4), p.device) is not None
+        monkeypatch.delenv("MAMBA_AMD_DEFER_REDUCE")
+        with grad_accum.accumulation_scope(defer_reduce=True):
+            buf, mode = grad_accum.deferred(p, "t", (2, 4), p.device)
+            assert buf.shape == (2, 4) and mode == 3  # sync micro-step (not direct): store + reduce
+            monkeypatch.setenv("MAMBA_AMD_DEFER_REDUCE", "0")
+            assert grad_accum.deferred(p, "t", (2, 4), p.device) is None
+    finally:
+        grad_accum.release_buffers()
