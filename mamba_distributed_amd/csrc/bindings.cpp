@@ -554,7 +554,6 @@ void selscan_common(mamba_amd::SelScanArgs& a, const Tensor& u, const Tensor& de
   TORCH_CHECK(a.N == 16 || a.N == 8 || a.N == 4, "native selective scan supports d_state 4/8/16");
   TORCH_CHECK(a.D % a.G == 0 && Bm.size(3) == a.L && Cm.sizes() == Bm.sizes(), "B/C shape");
   a.dtype = dcode(u.scalar_type());
-  a.Kc = mamba_amd::selscan_bwd_kc();
   a.softplus = softplus;
   auto v8 = [&](const Tensor& t, int64_t s0, int64_t s1) {
     return a.dtype == mamba_amd::kBF16 && (uintptr_t)t.data_ptr() % 16 == 0 && s0 % 8 == 0 && s1 % 8 == 0;
@@ -585,9 +584,12 @@ std::tuple<Tensor, Tensor, Tensor> selscan_fwd(Tensor u, Tensor delta, Tensor A,
   a.A = Af.data_ptr<float>(); a.D_ = fptr(Df); a.delta_bias = fptr(bf);
   auto out = at::empty({a.D, a.B, a.L}, u.options()).permute({1, 0, 2});
   a.out_ = out.data_ptr(); a.sob = out.stride(0); a.sod = out.stride(1);
-  const int nt = mamba_amd::selscan_ntiles(a.L);
+  a.carry_t = mamba_amd::selscan_carry_t(a);
+  a.nct = (a.L + a.carry_t - 1) / a.carry_t;
   auto fo = u.options().dtype(at::kFloat);
-  auto carries = at::empty({a.B, a.D, nt, a.N}, fo);
+  // (B, D, nct, N) view; 16-step carries are laid out (B, nct, D, N) (kernels: carry_index)
+  auto carries = a.carry_t == mamba_amd::kSelScanCarryTile ? at::empty({a.B, a.D, a.nct, a.N}, fo)
+                                                           : at::empty({a.B, a.nct, a.D, a.N}, fo).permute({0, 2, 1, 3});
   auto last = at::empty({a.B, a.D, a.N}, fo);
   a.carries = carries.data_ptr<float>(); a.last_state = last.data_ptr<float>();
   HIPCHK(mamba_amd::launch_selscan_fwd(a, cur_stream()));
@@ -605,7 +607,15 @@ std::vector<Tensor> selscan_bwd_impl(Tensor dout, Tensor u, Tensor delta, Tensor
   selscan_common(a, u, delta, A, Bm, Cm, zz, softplus);
   if (dout.stride(2) != 1 || dout.scalar_type() != u.scalar_type()) dout = dout.to(u.scalar_type()).contiguous();
   TORCH_CHECK(dout.sizes() == u.sizes(), "dout shape");
-  TORCH_CHECK(carries.is_contiguous() && carries.size(2) == mamba_amd::selscan_ntiles(a.L), "carries");
+  // the carry granularity is the forward's choice: 16 steps (wave-per-state-group kernels) or 512
+  a.nct = carries.size(2);
+  a.carry_t = a.nct == (a.L + mamba_amd::kSelScanCarrySG - 1) / mamba_amd::kSelScanCarrySG
+                  ? mamba_amd::kSelScanCarrySG : mamba_amd::kSelScanCarryTile;
+  TORCH_CHECK(carries.dim() == 4 && carries.size(0) == a.B && carries.size(1) == a.D && carries.size(3) == a.N &&
+              a.nct == (a.L + a.carry_t - 1) / a.carry_t, "carries shape");
+  TORCH_CHECK(a.carry_t == mamba_amd::kSelScanCarryTile ? carries.is_contiguous()
+                                                        : carries.permute({0, 2, 1, 3}).is_contiguous(),
+              "carries layout (selscan_fwd's output)");
   Tensor Af = f32c(A), Df = f32c_opt(D), bf = f32c_opt(delta_bias);
   a.A = Af.data_ptr<float>(); a.D_ = fptr(Df); a.delta_bias = fptr(bf);
   a.carries = carries.data_ptr<float>();
@@ -629,6 +639,7 @@ std::vector<Tensor> selscan_bwd_impl(Tensor dout, Tensor u, Tensor delta, Tensor
   a.dB_ = dB.data_ptr(); a.sdBb = dB.stride(0); a.sdBg = dB.stride(1); a.sdBn = dB.stride(2);
   a.dC_ = dC.data_ptr(); a.sdCb = dC.stride(0); a.sdCg = dC.stride(1); a.sdCn = dC.stride(2);
   auto fo = u.options().dtype(at::kFloat);
+  a.Kc = mamba_amd::selscan_bwd_kc(a);
   const int ndg = (a.D + a.Kc - 1) / a.Kc;
   auto part_bc = at::empty({2, a.B, ndg, a.N, a.L}, fo);
   a.part_dB = part_bc[0].data_ptr<float>(); a.part_dC = part_bc[1].data_ptr<float>();

@@ -4,6 +4,10 @@
 
 namespace mamba_amd {
 
+// saved-state (carry) granularities: every 16 steps for the wave-per-state-group kernels, else every
+// backward tile of the time-parallel kernels
+constexpr int kSelScanCarrySG = 16, kSelScanCarryTile = 512;
+
 struct SelScanArgs {
   int B, D, L, N, G, Kc;  // Kc = channels per workgroup (<= 64)
   int dtype;              // dtype of u / delta / z / B / C / out (kBF16 or kF32)
@@ -16,7 +20,8 @@ struct SelScanArgs {
   const float* D_; const float* delta_bias;
   const void* z_; int64_t szb, szd;
   void* out_; int64_t sob, sod;
-  float* carries;                                   // (B, D, ntiles, N) state at each tile start
+  float* carries;                                   // (B, D, nct, N) state at every carry_t-th step
+  int carry_t, nct;                                 // steps between saved states, nct = ceil(L / carry_t)
   float* last_state;                                // (B, D, N) or null
   // backward
   const void* dout_; int64_t sgb, sgd;
@@ -45,8 +50,10 @@ struct SSMUpdateArgs {
 
 hipError_t launch_selscan_fwd(const SelScanArgs& a, hipStream_t st);
 hipError_t launch_selscan_bwd(const SelScanArgs& a, hipStream_t st);
-int selscan_ntiles(int L);
-int selscan_bwd_kc();  // channels per backward workgroup (SelScanArgs::Kc)
+// carry granularity the forward will use for these args (16 with the wave-per-state-group kernels, else 512)
+int selscan_carry_t(const SelScanArgs& a);
+// channels per backward workgroup (SelScanArgs::Kc; sizes the dB / dC partials); needs carry_t set
+int selscan_bwd_kc(const SelScanArgs& a);
 hipError_t launch_ssm_update(const SSMUpdateArgs& a, hipStream_t st);
 
 }  // namespace mamba_amd

@@ -25,6 +25,14 @@ constexpr int SB_IT = 8, SB_T = 64 * SB_IT;   // backward tiles; also the saved-
 constexpr int SB_W = 4;                       // waves per backward workgroup
 constexpr int SB_KC = 32;                     // channels per backward workgroup (3 rounds of 2 WGs/CU at 280M)
 static_assert(SF_T % SB_T == 0, "forward tiles must hold whole backward tiles");
+static_assert(SB_T == kSelScanCarryTile && SB_T % kSelScanCarrySG == 0, "carry granularities");
+
+// saved states: (B, D, nct, N) for 512-step carries; (B, nct, D, N) for 16-step ones, so that one tile's
+// states of a 64-channel workgroup are one contiguous 4 KB block (coalesced stores and loads)
+__device__ __forceinline__ int64_t carry_index(const SelScanArgs& a, int b, int d, int j) {
+  return a.carry_t == kSelScanCarryTile ? (((int64_t)b * a.D + d) * a.nct + j) * a.N
+                                        : (((int64_t)b * a.nct + j) * a.D + d) * a.N;
+}
 
 // ---- item I/O: IT consecutive steps of one (b, d) row (16-B vectors when aligned) -------------
 // VEC: every row segment is a whole number of 16-B vectors inside [0, L) or entirely outside
@@ -288,7 +296,6 @@ __global__ __launch_bounds__(256) void selscan_fwd_sg_k(SelScanArgs a) {
 #pragma unroll
   for (int p = 0; p < 2; ++p) A2[p] = ss_f2{a.A[d * N + 4 * w + 2 * p], a.A[d * N + 4 * w + 2 * p + 1]} * kLog2e;
   ss_f2 h[2] = {ss_f2{0.f, 0.f}, ss_f2{0.f, 0.f}};
-  const int nck = (a.L + SB_T - 1) / SB_T;
   const int ntile = (a.L + SG_T - 1) / SG_T;
   // SG_D-deep ring of this thread's u / delta / z pieces (8 B each): each tile's data was requested
   // SG_D tiles earlier, so the short tiles never wait for HBM
@@ -340,8 +347,8 @@ __global__ __launch_bounds__(256) void selscan_fwd_sg_k(SelScanArgs a) {
     __syncthreads();
     fetch(r, min(tile + SG_D, ntile - 1));
     fetch_bc(min(tile + 1, ntile - 1));
-    if (a.carries && t0 % SB_T == 0)
-      *reinterpret_cast<float4*>(a.carries + (((int64_t)b * a.D + d) * nck + t0 / SB_T) * N + 4 * w) =
+    if (a.carries && t0 % a.carry_t == 0)
+      *reinterpret_cast<float4*>(a.carries + carry_index(a, b, d, t0 / a.carry_t) + 4 * w) =
           make_float4(h[0].x, h[0].y, h[1].x, h[1].y);
 #pragma unroll
     for (int t4 = 0; t4 < SG_T; t4 += 4) {
@@ -473,7 +480,7 @@ __global__ __launch_bounds__(256) void selscan_bwd_k(SelScanArgs a) {
           if (a.z_) nz = *reinterpret_cast<const uint2*>(((const bf16_t*)a.z_) + (int64_t)b * a.szb + (int64_t)d * a.szd + tl);
         }
         if (NW == 4 && k < nch)
-          nh = *reinterpret_cast<const float4*>(a.carries + (((int64_t)b * a.D + d0 + k) * ntl + tile) * N + w * NW);
+          nh = *reinterpret_cast<const float4*>(a.carries + carry_index(a, b, d0 + k, tile * (SB_T / a.carry_t)) + w * NW);
       }
     };
     if (has_states) fetch(0);
@@ -546,7 +553,7 @@ __global__ __launch_bounds__(256) void selscan_bwd_k(SelScanArgs a) {
           }
           const float prod = ca;  // the lane's decay product also seeds the adjoint composition
           scan_prefix(ca, cb);
-          const float hc0 = (VEC && NW == 4) ? hcv[0] : a.carries[(((int64_t)b * a.D + d) * ntl + tile) * N + n];
+          const float hc0 = (VEC && NW == 4) ? hcv[0] : a.carries[carry_index(a, b, d, tile * (SB_T / a.carry_t)) + n];
           if constexpr (VEC && NW == 4) {  // rotate like the accumulators: the live one is slot 0
             const float t0_ = hcv[0];
             hcv[0] = hcv[1]; hcv[1] = hcv[2]; hcv[2] = hcv[3]; hcv[3] = t0_;
@@ -834,7 +841,7 @@ __global__ __launch_bounds__(256) void selscan_bwd_fast_k(SelScanArgs a) {
           ng = *reinterpret_cast<const uint4*>(gb + (int64_t)d * a.sgd + tl);
           if (zb) nz = *reinterpret_cast<const uint4*>(zb + (int64_t)d * a.szd + tl);
         }
-        const float* cp = a.carries + (((int64_t)b * a.D + d) * ntl + tile) * N + w * NW;
+        const float* cp = a.carries + carry_index(a, b, d, tile * (SB_T / a.carry_t)) + w * NW;
 #pragma unroll
         for (int nn = 0; nn < NW; ++nn) {
           nh[nn] = cp[nn];
@@ -1060,6 +1067,261 @@ __global__ __launch_bounds__(256) void selscan_bwd_fast_k(SelScanArgs a) {
   }
 }
 
+// ---- backward, wave-per-state-group form (bf16, N = 16, D % 64 == 0, L % 16 == 0) -------------
+// The mirror of selscan_fwd_sg_k: a workgroup owns 64 channels of one batch row, lane = channel, wave w
+// owns states 4w .. 4w+3 (two float2 pairs), and time is walked BACKWARDS in 16-step tiles, one step after
+// the other -- no scans.  The forward saved the state at every tile start (carry_t = 16), so per tile a
+// wave
+//   * replays the tile forward from its saved state, keeping h_t (4 states x 16 steps = 64 VGPRs);
+//   * runs the adjoint lam_t = dy_t C_t + x_t, x_{t-1} = a_t lam_t backwards with packed f32 math; B / C do
+//     not depend on the channel, so they are SGPR operands (one dword per lane + v_readlane, as forward);
+//   * keeps dA[d, n] = sum_t dt lam a h_{t-1} in the lane (one (d, n) per lane and register);
+//   * reduces dB[t, n] = sum_d lam dt u and dC[t, n] = sum_d dy h over the 64 lanes with a register
+//     butterfly every 4 steps (v_permlane32_swap / v_permlane16_swap halves, then DPP row rotations):
+//     one partial per 64-channel group, summed in fixed order by selscan_reduce_bc_k;
+//   * meets the other 3 waves in LDS for the sums over states (lam B, A lam a h, C h), and the tile is
+//     finished (du, ddelta, dz, dD, ddelta_bias) by all 256 threads: channel tid / 4, steps 2 (tid % 4)
+//     and 2 (tid % 4) + 1 of each half -- the same threads that staged those steps.
+// Per lane and step: 2 x (pk_mul, 2 exp, pk_mul, pk_fma) replay + 2 x (pk_mul, 2 exp, 11 pk ops) adjoint.
+// Deterministic: every partial has one writer and every sum a fixed order.
+constexpr int SGB_T = kSelScanCarrySG;  // backward tile = forward carry granularity
+static_assert(SGB_T == SG_T, "the forward writes a carry at every one of its tiles");
+
+// v_permlane32_swap / v_permlane16_swap: x <- [x_lo, y_lo], y <- [x_hi, y_hi] (32-lane halves), and
+// x <- [x_r0, y_r0, x_r2, y_r2], y <- [x_r1, y_r1, x_r3, y_r3] (16-lane rows).  Inline asm: the compiler's
+// builtins for these return the first result twice (ROCm 7.2 clang: `v_add x, x` after the swap).  The
+// s_nop covers a VALU / swap write -> swap read (2 wait states, as the compiler places between swaps).
+__device__ __forceinline__ void permlane32_swap(float& x, float& y) {
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+}
+__device__ __forceinline__ void permlane16_swap(float& x, float& y) {
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+}
+// sum over the 64 lanes of 8 values per lane; lane l returns the total of value (l >> 3) & 7
+__device__ __forceinline__ float lane_sum8(const float (&v)[8]) {
+  const int lane = threadIdx.x & 63;
+  float w4[4], w2[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // xor 32: lanes 0-31 keep value i, lanes 32-63 value i + 4
+    float x = v[i], y = v[i + 4];
+    permlane32_swap(x, y);
+    w4[i] = x + y;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {  // xor 16: even rows keep i, odd rows i + 2
+    float x = w4[i], y = w4[i + 2];
+    permlane16_swap(x, y);
+    w2[i] = x + y;
+  }
+  // xor 8 (row_ror:8): bit 3 clear keeps value 0, set keeps value 1
+  const float p = w2[0] + dppf<0x128>(0.f, w2[0]);
+  const float q = w2[1] + dppf<0x128>(0.f, w2[1]);
+  float z = (lane & 8) ? q : p;
+  // the remaining 8 lanes of each half row hold the same value: half-row mirror, then the quad
+  z += dppf<0x141>(0.f, z);
+  z += dppf<0xB1>(0.f, z);  // quad_perm [1,0,3,2]
+  z += dppf<0x4E>(0.f, z);  // quad_perm [2,3,0,1]
+  return z;
+}
+
+__global__ __launch_bounds__(256) void selscan_bwd_sg_k(SelScanArgs a) {
+  constexpr int N = 16, T = SGB_T, TH = SGB_T / 2;
+  // per step and channel: dt, dt u, dout silu(z) (adjoint) and u, softplus', dout silu'(z) (finish)
+  __shared__ float dlS[T][65], duS[T][65], dyS[T][65], uS[T][65], sdS[T][65], gzS[T][65];
+  __shared__ float sS[4][3][T][65];  // per wave: sum_n lam B, A lam a h, C h
+  __shared__ __attribute__((aligned(16))) float BCs[4][T][8];  // per wave and step: B of its 4 states, C
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int wgs_per_b = a.D / 64;
+  const int b = blockIdx.x / wgs_per_b, dg = blockIdx.x % wgs_per_b, d0 = dg * 64;
+  const int g = d0 / (a.D / a.G);
+  const int d = d0 + lane;
+  // staging / finishing role: channel sr, steps 2 sp, 2 sp + 1 of each half tile.  Rows are addressed
+  // as a uniform base (SGPRs) plus a 32-bit per-thread offset (host: every row offset < 2^31).
+  const int sr = threadIdx.x >> 2, sp = threadIdx.x & 3;
+  const bf16_t* ub = (const bf16_t*)a.u_ + (int64_t)b * a.sub + (int64_t)d0 * a.sud;
+  const bf16_t* db = (const bf16_t*)a.delta_ + (int64_t)b * a.sdb + (int64_t)d0 * a.sdd;
+  const bf16_t* gb = (const bf16_t*)a.dout_ + (int64_t)b * a.sgb + (int64_t)d0 * a.sgd;
+  const bf16_t* zb = a.z_ ? (const bf16_t*)a.z_ + (int64_t)b * a.szb + (int64_t)d0 * a.szd : nullptr;
+  bf16_t* dub = (bf16_t*)a.du_ + (int64_t)b * a.sdub + (int64_t)d0 * a.sdud;
+  bf16_t* ddb = (bf16_t*)a.ddelta_ + (int64_t)b * a.sddb + (int64_t)d0 * a.sddd;
+  bf16_t* dzb = (a.z_ && a.dz_) ? (bf16_t*)a.dz_ + (int64_t)b * a.sdzb + (int64_t)d0 * a.sdzd : nullptr;
+  const int ou = sr * (int)a.sud + 2 * sp, od = sr * (int)a.sdd + 2 * sp, og = sr * (int)a.sgd + 2 * sp,
+            oz = sr * (int)a.szd + 2 * sp;
+  const float sbias = a.delta_bias ? a.delta_bias[d0 + sr] : 0.f;
+  const float sD = a.D_ ? a.D_[d0 + sr] : 0.f;
+  ss_f2 A2[2], An[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    An[p] = ss_f2{a.A[d * N + 4 * w + 2 * p], a.A[d * N + 4 * w + 2 * p + 1]};
+    A2[p] = An[p] * kLog2e;
+  }
+  const int ntile = a.L / T;
+  const int ndg = a.D / 64;
+  // next tile's inputs, in flight during the current one: this thread's u / delta / dout / z dwords
+  // (2 steps of each half), the wave's B / C dword (lane = 16 n + 8 [C] + j) and the lane's saved state
+  uint32_t nu[2], nr[2], ng[2], nz[2];
+  uint32_t nbc = 0u;
+  float4 nh;
+  const bf16_t* Bw = ((const bf16_t*)a.Bm_) + (int64_t)b * a.sBb + (int64_t)g * a.sBg + (int64_t)(4 * w) * a.sBn;
+  const bf16_t* Cw = ((const bf16_t*)a.Cm_) + (int64_t)b * a.sCb + (int64_t)g * a.sCg + (int64_t)(4 * w) * a.sCn;
+  const int bl_n = lane >> 4, bl_m = (lane >> 3) & 1, bl_j = lane & 7;
+  const int obc = bl_n * (int)(bl_m ? a.sCn : a.sBn) + 2 * bl_j;
+  const float* cb = a.carries + carry_index(a, b, d0, 0) + 4 * w;  // (B, nct, D, N)
+  const int oc = lane * N, ocj = a.D * N;
+  auto fetch = [&](int tile) {
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const int t = tile * T + TH * hf;
+      nu[hf] = *reinterpret_cast<const uint32_t*>(ub + t + ou);
+      nr[hf] = *reinterpret_cast<const uint32_t*>(db + t + od);
+      ng[hf] = *reinterpret_cast<const uint32_t*>(gb + t + og);
+      nz[hf] = zb ? *reinterpret_cast<const uint32_t*>(zb + t + oz) : 0u;
+    }
+    if (bl_m) nbc = *reinterpret_cast<const uint32_t*>(Cw + tile * T + obc);
+    else nbc = *reinterpret_cast<const uint32_t*>(Bw + tile * T + obc);
+    nh = *reinterpret_cast<const float4*>(cb + tile * ocj + oc);
+  };
+  ss_f2 x[2] = {ss_f2{0.f, 0.f}, ss_f2{0.f, 0.f}};  // adjoint carried into the step after the tile
+  ss_f2 dA[2] = {ss_f2{0.f, 0.f}, ss_f2{0.f, 0.f}};
+  float dDp = 0.f, dbp = 0.f;
+  // this lane's dB / dC totals (lane_sum8): state 4 w + ((lane >> 3) & 3), step t2 + (lane >> 5)
+  float* pdB = a.part_dB + (((int64_t)b * ndg + dg) * N + 4 * w) * a.L;
+  float* pdC = a.part_dC + (((int64_t)b * ndg + dg) * N + 4 * w) * a.L;
+  const int opd = ((lane >> 3) & 3) * a.L + (lane >> 5);
+  fetch(ntile - 1);
+  for (int tile = ntile - 1; tile >= 0; --tile) {
+    const int t0 = tile * T;
+    __syncthreads();  // the previous tile's readers of the staged rows are done
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        auto upk = [&](uint32_t q) { return __uint_as_float(e ? (q & 0xffff0000u) : (q << 16)); };
+        const float u = upk(nu[hf]), v = upk(nr[hf]) + sbias, go = upk(ng[hf]), zz = upk(nz[hf]);
+        const float dl = a.softplus ? softplus_fast(v) : v;
+        const float sg = sigmoid_fast(zz);
+        const int tl = TH * hf + 2 * sp + e;
+        dlS[tl][sr] = dl;
+        duS[tl][sr] = dl * u;
+        dyS[tl][sr] = zb ? go * (zz * sg) : go;
+        uS[tl][sr] = u;
+        sdS[tl][sr] = a.softplus ? sigmoid_fast(v) : 1.f;
+        gzS[tl][sr] = zb ? go * sg * (1.f + zz * (1.f - sg)) : 0.f;
+      }
+    }
+    // B / C are the same for every lane: broadcast LDS reads in the step loops
+    BCs[w][2 * bl_j][4 * bl_m + bl_n] = __uint_as_float(nbc << 16);
+    BCs[w][2 * bl_j + 1][4 * bl_m + bl_n] = __uint_as_float(nbc & 0xffff0000u);
+    const ss_f2 hst[2] = {ss_f2{nh.x, nh.y}, ss_f2{nh.z, nh.w}};
+    __syncthreads();
+    if (tile > 0) fetch(tile - 1);
+    auto ldB = [&](int t, ss_f2 (&o)[2]) {
+      const float4 q = *reinterpret_cast<const float4*>(&BCs[w][t][0]);
+      o[0] = ss_f2{q.x, q.y};
+      o[1] = ss_f2{q.z, q.w};
+    };
+    auto ldC = [&](int t, ss_f2 (&o)[2]) {
+      const float4 q = *reinterpret_cast<const float4*>(&BCs[w][t][4]);
+      o[0] = ss_f2{q.x, q.y};
+      o[1] = ss_f2{q.z, q.w};
+    };
+    // replay the tile from its saved state, keeping h_t of every step
+    ss_f2 hs[T][2];
+    {
+      ss_f2 h[2] = {hst[0], hst[1]};
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        const float dl = dlS[t][lane], du = duS[t][lane];
+        ss_f2 Bv[2];
+        ldB(t, Bv);
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const ss_f2 e = A2[p] * dl;
+          const ss_f2 av = ss_f2{__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
+          h[p] = __builtin_elementwise_fma(av, h[p], Bv[p] * du);
+          hs[t][p] = h[p];
+        }
+      }
+    }
+    // re-read dt / B / C from LDS and recompute exp(dt A) below rather than keep the replay's values
+    // live across the tile (register pressure)
+    asm volatile("" ::: "memory");
+    // the adjoint, backwards, two steps at a time (one lane butterfly per two steps for dB and dC)
+#pragma unroll
+    for (int t2 = T - 2; t2 >= 0; t2 -= 2) {
+      float cB[8], cC[8];  // value 4 k + n_local for step t2 + k
+#pragma unroll
+      for (int k = 1; k >= 0; --k) {
+        const int t = t2 + k;
+        const float dl = dlS[t][lane], du = duS[t][lane], dy = dyS[t][lane];
+        ss_f2 s1 = ss_f2{0.f, 0.f}, s2 = s1, yy = s1;
+        ss_f2 Bv[2], Cv[2];
+        ldB(t, Bv);
+        ldC(t, Cv);
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const ss_f2 e = A2[p] * dl;
+          const ss_f2 av = ss_f2{__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
+          const ss_f2 Bp = Bv[p], Cp = Cv[p];
+          const ss_f2 lam = __builtin_elementwise_fma(Cp, ss_f2{dy, dy}, x[p]);
+          const ss_f2 hp = t > 0 ? hs[t > 0 ? t - 1 : 0][p] : hst[p];
+          const ss_f2 t1 = lam * (av * hp);  // lam a_t h_{t-1}
+          const ss_f2 cb = lam * du, cc = hs[t][p] * dy;
+          cB[4 * k + 2 * p] = cb.x; cB[4 * k + 2 * p + 1] = cb.y;
+          cC[4 * k + 2 * p] = cc.x; cC[4 * k + 2 * p + 1] = cc.y;
+          s1 = __builtin_elementwise_fma(lam, Bp, s1);
+          s2 = __builtin_elementwise_fma(An[p], t1, s2);
+          yy = __builtin_elementwise_fma(Cp, hs[t][p], yy);
+          dA[p] = __builtin_elementwise_fma(t1, ss_f2{dl, dl}, dA[p]);
+          x[p] = av * lam;
+        }
+        sS[w][0][t][lane] = s1.x + s1.y;
+        sS[w][1][t][lane] = s2.x + s2.y;
+        sS[w][2][t][lane] = yy.x + yy.y;
+      }
+      const float rb = lane_sum8(cB), rc = lane_sum8(cC);
+      if ((lane & 7) == 0) {
+        pdB[t0 + t2 + opd] = rb;
+        pdC[t0 + t2 + opd] = rc;
+      }
+    }
+    __syncthreads();  // the 4 waves' sums over states of the tile are in LDS
+    // finish: this thread's 2 steps of each half (the ones it staged)
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      float o_du[2], o_dd[2], o_dz[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int tl = TH * hf + 2 * sp + e;
+        const float S1 = (sS[0][0][tl][sr] + sS[1][0][tl][sr]) + (sS[2][0][tl][sr] + sS[3][0][tl][sr]);
+        const float S2 = (sS[0][1][tl][sr] + sS[1][1][tl][sr]) + (sS[2][1][tl][sr] + sS[3][1][tl][sr]);
+        const float Y = (sS[0][2][tl][sr] + sS[1][2][tl][sr]) + (sS[2][2][tl][sr] + sS[3][2][tl][sr]);
+        const float dl = dlS[tl][sr], dy = dyS[tl][sr], u = uS[tl][sr];
+        o_du[e] = fmaf(dl, S1, sD * dy);
+        o_dd[e] = fmaf(u, S1, S2) * sdS[tl][sr];
+        o_dz[e] = gzS[tl][sr] * fmaf(sD, u, Y);
+        dDp = fmaf(dy, u, dDp);
+        dbp += o_dd[e];
+      }
+      const int t = t0 + TH * hf;
+      *reinterpret_cast<unsigned*>(dub + t + sr * (int)a.sdud + 2 * sp) = pack2(o_du[0], o_du[1]);
+      *reinterpret_cast<unsigned*>(ddb + t + sr * (int)a.sddd + 2 * sp) = pack2(o_dd[0], o_dd[1]);
+      if (dzb) *reinterpret_cast<unsigned*>(dzb + t + sr * (int)a.sdzd + 2 * sp) = pack2(o_dz[0], o_dz[1]);
+    }
+  }
+  *reinterpret_cast<float4*>(a.part_dA + ((int64_t)b * a.D + d) * N + 4 * w) =
+      make_float4(dA[0].x, dA[0].y, dA[1].x, dA[1].y);
+  // dD / ddelta_bias: the 4 threads of a channel are one quad
+  dDp += dppf<0xB1>(0.f, dDp);
+  dDp += dppf<0x4E>(0.f, dDp);
+  dbp += dppf<0xB1>(0.f, dbp);
+  dbp += dppf<0x4E>(0.f, dbp);
+  if (sp == 0) {
+    a.part_dD[(int64_t)b * a.D + d0 + sr] = dDp;
+    a.part_dbias[(int64_t)b * a.D + d0 + sr] = dbp;
+  }
+}
+
 // dB[b,g,n,t] = sum over the channel groups that belong to group g
 template <typename T>
 __global__ void selscan_reduce_bc_k(SelScanArgs a) {
@@ -1095,38 +1357,67 @@ __global__ void selscan_reduce_bc_k(SelScanArgs a) {
     else return hipErrorInvalidValue;                                               \
   } while (0)
 
+static bool env_off(const char* name) {
+  const char* e = std::getenv(name);
+  return e && std::atoi(e) == 0;
+}
+// the wave-per-state-group kernels: bf16 rows, 64-channel workgroups inside one B/C group
+static bool sg_shape_ok(const SelScanArgs& a) {
+  return a.dtype == kBF16 && a.vec && a.vecbc && (!a.z_ || a.vecz) && a.N == 16 && a.D % 64 == 0 &&
+         (a.D / a.G) % 64 == 0;
+}
+// sequential-time forward walk when the batch has the channels to fill the GPU (>= 2048 wavefronts);
+// MAMBA_AMD_SELSCAN_LC=0 forces the time-parallel kernel (A/B, tests).
+// Measured at B=32, D=1536, L=1024, N=16 on MI355X: 290 us vs 345 us.
+static bool use_fwd_sg(const SelScanArgs& a) {
+  return sg_shape_ok(a) && a.L % SF_IT == 0 && !env_off("MAMBA_AMD_SELSCAN_LC") && (int64_t)a.B * a.D / 16 >= 2048;
+}
+// sequential-time backward: needs the forward's 16-step carries; MAMBA_AMD_SELSCAN_BWD_SG=0 keeps the
+// time-parallel backward (and 512-step carries)
+int selscan_carry_t(const SelScanArgs& a) {
+  return (use_fwd_sg(a) && a.L % SGB_T == 0 && !env_off("MAMBA_AMD_SELSCAN_BWD_SG")) ? SGB_T : SB_T;
+}
+static bool use_bwd_sg(const SelScanArgs& a) {
+  // 32-bit in-kernel offsets: 64 rows of every (b, d, l) tensor, 64 carry rows
+  const int64_t lim = (int64_t)1 << 24;
+  const bool off32 = a.sud < lim && a.sdd < lim && a.sgd < lim && (!a.z_ || a.szd < lim) && a.sdud < lim &&
+                     a.sddd < lim && (!a.dz_ || a.sdzd < lim) && a.sBn < lim && a.sCn < lim && a.L < lim;
+  return a.carry_t == SGB_T && sg_shape_ok(a) && a.vecg && a.L % SGB_T == 0 && a.nct == a.L / SGB_T && off32;
+}
+int selscan_bwd_kc(const SelScanArgs& a) { return use_bwd_sg(a) ? 64 : SB_KC; }
+
 hipError_t launch_selscan_fwd(const SelScanArgs& a, hipStream_t st) {
   const int64_t rows = (int64_t)a.B * a.D;
   dim3 grid((unsigned)((rows + 3) / 4)), block(256);
-  const bool v = a.dtype == kBF16 && a.vec && a.vecbc && (!a.z_ || a.vecz) && a.L % SF_IT == 0;
-  // sequential-time walk (wave per state group, lane per channel) when the batch has the channels to fill
-  // the GPU (>= 2048 wavefronts); MAMBA_AMD_SELSCAN_LC=0 forces the time-parallel kernel (A/B, tests).
-  // Measured at B=32, D=1536, L=1024, N=16 on MI355X: 290 us vs 345 us.
-  const char* lce = std::getenv("MAMBA_AMD_SELSCAN_LC");
-  if (v && (!lce || std::atoi(lce) != 0) && a.N == 16 && a.D % 64 == 0 && (a.D / a.G) % 64 == 0 &&
-      (int64_t)a.B * a.D / 16 >= 2048) {
+  if (a.carries && a.nct != (a.L + a.carry_t - 1) / a.carry_t) return hipErrorInvalidValue;
+  if (use_fwd_sg(a)) {
     hipLaunchKernelGGL(selscan_fwd_sg_k, dim3((unsigned)(a.B * (a.D / 64))), dim3(256), 0, st, a);
     return hipGetLastError();
   }
+  if (a.carry_t != SB_T) return hipErrorInvalidValue;  // the time-parallel forward saves per 512-step tile
+  const bool v = a.dtype == kBF16 && a.vec && a.vecbc && (!a.z_ || a.vecz) && a.L % SF_IT == 0;
   if (v) SS_DISPATCH(hipLaunchKernelGGL((selscan_fwd_k<TT, NN, true>), grid, block, 0, st, a));
   else SS_DISPATCH(hipLaunchKernelGGL((selscan_fwd_k<TT, NN, false>), grid, block, 0, st, a));
   return hipGetLastError();
 }
 
-int selscan_ntiles(int L) { return (L + SB_T - 1) / SB_T; }
-int selscan_bwd_kc() { return SB_KC; }
-
 hipError_t launch_selscan_bwd(const SelScanArgs& a, hipStream_t st) {
-  if (a.Kc != SB_KC) return hipErrorInvalidValue;
-  dim3 grid((a.D + SB_KC - 1) / SB_KC, a.B), block(64 * SB_W);
-  const bool v = a.dtype == kBF16 && a.vec && a.vecbc && a.vecg && (!a.z_ || a.vecz) && a.L % 8 == 0;
-  if (v) {
-    if (a.N == 16) hipLaunchKernelGGL(selscan_bwd_fast_k<16>, grid, block, 0, st, a);
-    else if (a.N == 8) hipLaunchKernelGGL(selscan_bwd_fast_k<8>, grid, block, 0, st, a);
-    else if (a.N == 4) hipLaunchKernelGGL(selscan_bwd_fast_k<4>, grid, block, 0, st, a);
-    else return hipErrorInvalidValue;
+  if (a.Kc != selscan_bwd_kc(a) || (a.carry_t != SGB_T && a.carry_t != SB_T) ||
+      a.nct != (a.L + a.carry_t - 1) / a.carry_t)
+    return hipErrorInvalidValue;
+  if (use_bwd_sg(a)) {
+    hipLaunchKernelGGL(selscan_bwd_sg_k, dim3((unsigned)(a.B * (a.D / 64))), dim3(256), 0, st, a);
   } else {
-    SS_DISPATCH(hipLaunchKernelGGL((selscan_bwd_k<TT, NN, false>), grid, block, 0, st, a));
+    dim3 grid((a.D + SB_KC - 1) / SB_KC, a.B), block(64 * SB_W);
+    const bool v = a.dtype == kBF16 && a.vec && a.vecbc && a.vecg && (!a.z_ || a.vecz) && a.L % 8 == 0;
+    if (v) {
+      if (a.N == 16) hipLaunchKernelGGL(selscan_bwd_fast_k<16>, grid, block, 0, st, a);
+      else if (a.N == 8) hipLaunchKernelGGL(selscan_bwd_fast_k<8>, grid, block, 0, st, a);
+      else if (a.N == 4) hipLaunchKernelGGL(selscan_bwd_fast_k<4>, grid, block, 0, st, a);
+      else return hipErrorInvalidValue;
+    } else {
+      SS_DISPATCH(hipLaunchKernelGGL((selscan_bwd_k<TT, NN, false>), grid, block, 0, st, a));
+    }
   }
   MAMBA_HIP_CHECK(hipGetLastError());
   const int64_t total = (int64_t)a.B * a.G * a.N * a.L;

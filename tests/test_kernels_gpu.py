@@ -826,10 +826,49 @@ def test_selective_scan_channel_walk(cuda, monkeypatch, L, with_z):
         outs[lc] = ops.selscan_fwd(u, delta, A, Bm, Cm, D, z, db, True)
     y_ref = R.selective_scan_ref(u, delta, A, Bm, Cm, D, z=z, delta_bias=db, delta_softplus=True)
     assert rel(outs["1"][0], y_ref) < 2e-2
-    for i in range(3):  # out, carries, last state
-        assert rel(outs["1"][i], outs["0"][i]) < 1e-2, i
+    # out and last state; carries: the walk saves every 16 steps (for the sequential backward), the
+    # time-parallel kernel every 512
+    assert rel(outs["1"][0], outs["0"][0]) < 1e-2
+    assert rel(outs["1"][2], outs["0"][2]) < 1e-2
+    assert outs["1"][1].shape[2] == (L + 15) // 16 and outs["0"][1].shape[2] == (L + 511) // 512
+    assert rel(outs["1"][1][:, :, ::32], outs["0"][1]) < 1e-2
     y = selective_scan_fn(u, delta, A, Bm, Cm, D, z=z, delta_bias=db, delta_softplus=True)
     assert rel(y, y_ref) < 2e-2
+
+
+@pytest.mark.parametrize("b,d,L,G,with_z", [(32, 1536, 256, 1, True), (16, 2048, 160, 2, False)])
+def test_selective_scan_sequential_backward(cuda, monkeypatch, b, d, L, G, with_z):
+    """The sequential-time backward (selscan_bwd_sg_k, 16-step carries, lane-butterfly dB/dC) at the
+    Mamba-1 280M channel count: every gradient vs the fp32 reference and vs the time-parallel backward."""
+    from mamba_distributed_amd.ops.selective_scan import selective_scan_fn
+    torch.manual_seed(8)
+    n = 16
+    u = torch.randn(b, d, L, device=cuda).to(torch.bfloat16)
+    delta = (torch.randn(b, d, L, device=cuda) * 0.5 - 1).to(torch.bfloat16)
+    A = -torch.rand(d, n, device=cuda) * 4 - 0.1
+    Bm = torch.randn(b, G, n, L, device=cuda).to(torch.bfloat16)
+    Cm = torch.randn(b, G, n, L, device=cuda).to(torch.bfloat16)
+    D = torch.randn(d, device=cuda)
+    z = torch.randn(b, d, L, device=cuda).to(torch.bfloat16) if with_z else None
+    db = torch.randn(d, device=cuda) * 0.3
+    ops = torch.ops.mamba_amd
+    assert ops.selscan_fwd(u, delta, A, Bm, Cm, D, z, db, True)[1].shape[2] == L // 16  # 16-step carries
+
+    def f(u, delta, A, Bm, Cm, D, z, db):
+        return selective_scan_fn(u, delta, A, Bm, Cm, D, z=z, delta_bias=db, delta_softplus=True)
+
+    ins = [u, delta, A, Bm, Cm, D, z, db]
+    on, orf, gn, gr = run_both(f, f, ins)
+    assert rel(on, orf) < 2e-2, rel(on, orf)
+    names = ["u", "delta", "A", "B", "C", "D", "z", "db"]
+    for nm, a_, b_ in zip(names, gn, gr):
+        if b_ is not None:
+            assert rel(a_, b_) < 3e-2, (nm, rel(a_, b_))
+    monkeypatch.setenv("MAMBA_AMD_SELSCAN_BWD_SG", "0")  # time-parallel backward, 512-step carries
+    _, _, gp, _ = run_both(f, f, ins)
+    for nm, a_, b_ in zip(names, gn, gp):
+        if b_ is not None:
+            assert rel(a_, b_) < 1e-2, (nm, rel(a_, b_))
 
 
 def test_mamba1_deferred_wgrad_matches_default(cuda, monkeypatch):
