@@ -864,6 +864,18 @@ def test_selective_scan_sequential_backward(cuda, monkeypatch, b, d, L, G, with_
     for nm, a_, b_ in zip(names, gn, gr):
         if b_ is not None:
             assert rel(a_, b_) < 3e-2, (nm, rel(a_, b_))
+    # 16-step carries consumed by the time-parallel backward (a dout that is not 16-B aligned keeps the
+    # sequential kernel out): same gradients
+    out, carries, _ = ops.selscan_fwd(u, delta, A, Bm, Cm, D, z, db, True)
+    go = torch.randn_like(out)
+    ref_g = ops.selscan_bwd(go, u, delta, A, Bm, Cm, D, z, db, carries, True)
+    buf = torch.empty(go.numel() + 1, device=cuda, dtype=go.dtype)
+    go_mis = buf[1:].view(go.shape)
+    go_mis.copy_(go)
+    mis_g = ops.selscan_bwd(go_mis, u, delta, A, Bm, Cm, D, z, db, carries, True)
+    for nm, a_, b_ in zip(["du", "ddelta", "dA", "dB", "dC", "dD", "dz", "dbias"], mis_g, ref_g):
+        if b_.numel():
+            assert rel(a_, b_) < 1e-2, (nm, rel(a_, b_))
     monkeypatch.setenv("MAMBA_AMD_SELSCAN_BWD_SG", "0")  # time-parallel backward, 512-step carries
     _, _, gp, _ = run_both(f, f, ins)
     for nm, a_, b_ in zip(names, gn, gp):
