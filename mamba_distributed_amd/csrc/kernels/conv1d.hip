@@ -15,6 +15,7 @@
 //   4 waves (4 time tiles) summed through LDS -> one partial row per block -> fixed-order sum.
 #include "common.h"
 #include "launchers.h"
+#include <cstdlib>
 #include <type_traits>
 
 namespace mamba_amd {
@@ -384,26 +385,50 @@ __device__ __forceinline__ void unpack8(const uint4 v, f2v (&o)[4]) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) o[q] = f2v{__uint_as_float(u[q] << 16), __uint_as_float(u[q] & 0xffff0000u)};
 }
+// CV channels of one row as CV/2 packed pairs: CV = 8 -> one 16-B load, CV = 4 -> one 8-B load
+template <int CV> struct RowV;
+template <> struct RowV<8> {
+  uint4 v;
+  __device__ __forceinline__ void load(const bf16_t* p) { v = *reinterpret_cast<const uint4*>(p); }
+  __device__ __forceinline__ void zero() { v = make_uint4(0, 0, 0, 0); }
+  __device__ __forceinline__ void unpack(f2v (&o)[4]) const { unpack8(v, o); }
+};
+template <> struct RowV<4> {
+  uint2 v;
+  __device__ __forceinline__ void load(const bf16_t* p) { v = *reinterpret_cast<const uint2*>(p); }
+  __device__ __forceinline__ void zero() { v = make_uint2(0, 0); }
+  __device__ __forceinline__ void unpack(f2v (&o)[2]) const {
+    o[0] = f2v{__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u)};
+    o[1] = f2v{__uint_as_float(v.y << 16), __uint_as_float(v.y & 0xffff0000u)};
+  }
+};
 __device__ __forceinline__ unsigned pack2(const f2v v) {
   return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf2v));
 }
 __device__ __forceinline__ uint4 pack8(const f2v (&o)[4]) {
   return make_uint4(pack2(o[0]), pack2(o[1]), pack2(o[2]), pack2(o[3]));
 }
+__device__ __forceinline__ void store_row(bf16_t* p, const f2v (&o)[4]) { *reinterpret_cast<uint4*>(p) = pack8(o); }
+__device__ __forceinline__ void store_row(bf16_t* p, const f2v (&o)[2]) {
+  *reinterpret_cast<uint2*>(p) = make_uint2(pack2(o[0]), pack2(o[1]));
+}
 
-template <int W, int TT>
+// CV = channels per lane (8: 16-B rows, 4: 8-B rows -- half the registers, twice the waves in flight and
+// no idle lanes when C % 512 != 0, e.g. the 280M conv width 1792)
+template <int W, int TT, int CV>
 __global__ __launch_bounds__(256) void conv_cl_fwd_bf16_k(const bf16_t* __restrict__ x, int64_t sxb, int64_t sxl,
                                                           const float* __restrict__ w, const float* __restrict__ bias,
                                                           bf16_t* __restrict__ out, int64_t sob, int64_t sol, int L,
                                                           int C, bool silu) {
+  constexpr int NQ = CV / 2;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c = (blockIdx.x * 64 + lane) * 8;
+  const int c = (blockIdx.x * 64 + lane) * CV;
   const int t0 = (blockIdx.y * 4 + wave) * TT;
   const int b = blockIdx.z;
   if (c >= C || t0 >= L) return;
-  f2v wk[W][4], bs[4];
+  f2v wk[W][NQ], bs[NQ];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < NQ; ++q) {
 #pragma unroll
     for (int k = 0; k < W; ++k) wk[k][q] = f2v{w[(c + 2 * q) * W + k], w[(c + 2 * q + 1) * W + k]};
     bs[q] = bias ? f2v{bias[c + 2 * q], bias[c + 2 * q + 1]} : f2v{0.f, 0.f};
@@ -411,58 +436,68 @@ __global__ __launch_bounds__(256) void conv_cl_fwd_bf16_k(const bf16_t* __restri
   const bf16_t* xb = x + b * sxb + c;
   bf16_t* ob = out + b * sob + c;
   const int tend = min(t0 + TT, L);
-  auto ldrow = [&](int t) -> uint4 {
-    return (t >= 0 && t < tend) ? *reinterpret_cast<const uint4*>(xb + t * sxl) : make_uint4(0, 0, 0, 0);
+  auto ldrow = [&](int t) {
+    RowV<CV> r;
+    if (t >= 0 && t < tend) r.load(xb + t * sxl);
+    else r.zero();
+    return r;
   };
-  f2v xr[W][4];
+  f2v xr[W][NQ];
 #pragma unroll
-  for (int k = 0; k < W - 1; ++k) unpack8(ldrow(t0 - (W - 1) + k), xr[k]);
+  for (int k = 0; k < W - 1; ++k) ldrow(t0 - (W - 1) + k).unpack(xr[k]);
   const int nsteps = tend - t0;
-  for (int i0 = 0; i0 < nsteps; i0 += W) {
-    uint4 rx[W];
+  // each group of W rows is requested one group ahead (two groups of loads in flight per wave)
+  RowV<CV> rx[W];
 #pragma unroll
-    for (int u = 0; u < W; ++u) rx[u] = ldrow(t0 + i0 + u);
+  for (int u = 0; u < W; ++u) rx[u] = ldrow(t0 + u);
+  for (int i0 = 0; i0 < nsteps; i0 += W) {
+    RowV<CV> nx[W];
+#pragma unroll
+    for (int u = 0; u < W; ++u) nx[u] = ldrow(t0 + i0 + W + u);
 #pragma unroll
     for (int u = 0; u < W; ++u) {
       const int i = i0 + u;
       if (i < nsteps) {
         const int sl = (u + W - 1) % W;
-        unpack8(rx[u], xr[sl]);
-        f2v o[4];
+        rx[u].unpack(xr[sl]);
+        f2v o[NQ];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < NQ; ++q) {
           f2v a = bs[q];
 #pragma unroll
           for (int k = 0; k < W; ++k) a += wk[k][q] * xr[(u + k) % W][q];
           if (silu) a = a * f2v{sigmoidf_(a.x), sigmoidf_(a.y)};
           o[q] = a;
         }
-        *reinterpret_cast<uint4*>(ob + (t0 + i) * sol) = pack8(o);
+        store_row(ob + (t0 + i) * sol, o);
       }
     }
+#pragma unroll
+    for (int u = 0; u < W; ++u) rx[u] = nx[u];
   }
 }
 
-template <int W, int TT>
+template <int W, int TT, int CV>
 __global__ __launch_bounds__(256) void conv_cl_bwd_bf16_k(const bf16_t* __restrict__ x, int64_t sxb, int64_t sxl,
                                                           const float* __restrict__ w, const float* __restrict__ bias,
                                                           const bf16_t* __restrict__ dout, int64_t sgb, int64_t sgl,
                                                           bf16_t* __restrict__ dx, int64_t sdb, int64_t sdl,
                                                           float* __restrict__ part, bool pacc, int L, int C, bool silu) {
-  __shared__ float red[4][64 * 8 * (W + 1)];
+  constexpr int NQ = CV / 2;
+  __shared__ float red[4][64 * CV * (W + 1)];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c = (blockIdx.x * 64 + lane) * 8;
+  const int c = (blockIdx.x * 64 + lane) * CV;
   const int t0 = (blockIdx.y * 4 + wave) * TT;
   const int b = blockIdx.z;
-  f2v acc[W + 1][4];
+  f2v acc[W + 1][NQ];
 #pragma unroll
   for (int k = 0; k < W + 1; ++k)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) acc[k][q] = f2v{0.f, 0.f};
+    for (int q = 0; q < NQ; ++q) acc[k][q] = f2v{0.f, 0.f};
   if (c < C && t0 < L) {
-    f2v wk[W][4], bs[4];
+    f2v wk[W][NQ], bs[NQ];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < NQ; ++q) {
 #pragma unroll
       for (int k = 0; k < W; ++k) wk[k][q] = f2v{w[(c + 2 * q) * W + k], w[(c + 2 * q + 1) * W + k]};
       bs[q] = bias ? f2v{bias[c + 2 * q], bias[c + 2 * q + 1]} : f2v{0.f, 0.f};
@@ -473,33 +508,43 @@ __global__ __launch_bounds__(256) void conv_cl_bwd_bf16_k(const bf16_t* __restri
     const int tend = min(t0 + TT, L);
     const int nsteps = tend + W - 1 - t0;  // main steps t = t0 .. t0+nsteps-1
     const int tlim = min(L, t0 + nsteps);
-    auto ldrow = [&](const bf16_t* base, int64_t stride, int t) -> uint4 {
-      return (t >= 0 && t < tlim) ? *reinterpret_cast<const uint4*>(base + t * stride) : make_uint4(0, 0, 0, 0);
+    auto ldrow = [&](const bf16_t* base, int64_t stride, int t) {
+      RowV<CV> r;
+      if (t >= 0 && t < tlim) r.load(base + t * stride);
+      else r.zero();
+      return r;
     };
-    f2v xr[W][4], dp[W][4];
+    f2v xr[W][NQ], dp[W][NQ];
 #pragma unroll
     for (int k = 0; k < W; ++k) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) dp[k][q] = f2v{0.f, 0.f};
-      if (k < W - 1) unpack8(ldrow(xb, sxl, t0 - (W - 1) + k), xr[k]);
+      for (int q = 0; q < NQ; ++q) dp[k][q] = f2v{0.f, 0.f};
+      if (k < W - 1) ldrow(xb, sxl, t0 - (W - 1) + k).unpack(xr[k]);
+    }
+    // each group of W rows of x and dout is requested one group ahead (two groups in flight per wave)
+    RowV<CV> rx[W], rg[W];
+#pragma unroll
+    for (int u = 0; u < W; ++u) {
+      rx[u] = ldrow(xb, sxl, t0 + u);
+      rg[u] = ldrow(gb, sgl, t0 + u);
     }
     for (int i0 = 0; i0 < nsteps; i0 += W) {
-      uint4 rx[W], rg[W];
+      RowV<CV> nx[W], ng[W];
 #pragma unroll
       for (int u = 0; u < W; ++u) {
-        rx[u] = ldrow(xb, sxl, t0 + i0 + u);
-        rg[u] = ldrow(gb, sgl, t0 + i0 + u);
+        nx[u] = ldrow(xb, sxl, t0 + i0 + W + u);
+        ng[u] = ldrow(gb, sgl, t0 + i0 + W + u);
       }
 #pragma unroll
       for (int u = 0; u < W; ++u) {
         const int i = i0 + u, t = t0 + i;
         if (i < nsteps) {
           const int sl = (u + W - 1) % W;  // slot of step t (compile-time after unrolling)
-          unpack8(rx[u], xr[sl]);
-          f2v g[4];
-          unpack8(rg[u], g);
+          rx[u].unpack(xr[sl]);
+          f2v g[NQ];
+          rg[u].unpack(g);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
+          for (int q = 0; q < NQ; ++q) {
             f2v a = bs[q];
 #pragma unroll
             for (int k = 0; k < W; ++k) a += wk[k][q] * xr[(u + k) % W][q];
@@ -513,38 +558,43 @@ __global__ __launch_bounds__(256) void conv_cl_bwd_bf16_k(const bf16_t* __restri
           }
           if (t < tend) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < NQ; ++q) {
 #pragma unroll
               for (int k = 0; k < W; ++k) acc[k][q] += dp[sl][q] * xr[(u + k) % W][q];
               acc[W][q] += dp[sl][q];
             }
           }
           if (i >= W - 1) {  // dx[s], s = t-(W-1) >= t0
-            f2v o[4];
+            f2v o[NQ];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < NQ; ++q) {
               f2v v = f2v{0.f, 0.f};
 #pragma unroll
               for (int m = 0; m < W; ++m) v += wk[W - 1 - m][q] * dp[(u + m) % W][q];
               o[q] = v;
             }
-            *reinterpret_cast<uint4*>(db_ + (t - (W - 1)) * sdl) = pack8(o);
+            store_row(db_ + (t - (W - 1)) * sdl, o);
           }
         }
+      }
+#pragma unroll
+      for (int u = 0; u < W; ++u) {
+        rx[u] = nx[u];
+        rg[u] = ng[u];
       }
     }
   }
 #pragma unroll
   for (int k = 0; k < W + 1; ++k)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      red[wave][(lane * 8 + 2 * q) * (W + 1) + k] = acc[k][q].x;
-      red[wave][(lane * 8 + 2 * q + 1) * (W + 1) + k] = acc[k][q].y;
+    for (int q = 0; q < NQ; ++q) {
+      red[wave][(lane * CV + 2 * q) * (W + 1) + k] = acc[k][q].x;
+      red[wave][(lane * CV + 2 * q + 1) * (W + 1) + k] = acc[k][q].y;
     }
   __syncthreads();
   const int64_t prow = (int64_t)blockIdx.z * gridDim.y + blockIdx.y;
-  for (int i = threadIdx.x; i < 64 * 8 * (W + 1); i += 256) {
-    const int ch = blockIdx.x * 512 + i / (W + 1);
+  for (int i = threadIdx.x; i < 64 * CV * (W + 1); i += 256) {
+    const int ch = blockIdx.x * 64 * CV + i / (W + 1);
     if (ch < C) {
       float* pp = part + prow * (int64_t)C * (W + 1) + (int64_t)ch * (W + 1) + i % (W + 1);
       const float v = red[0][i] + red[1][i] + red[2][i] + red[3][i];
@@ -781,6 +831,15 @@ hipError_t launch_conv_cf_bwd(const void* x, int dt, int64_t sxb, int64_t sxd, c
   return hipErrorInvalidValue;
 }
 
+// channels per lane of the bf16 channel-last kernels: 4 (8-B rows) unless MAMBA_AMD_CONV_CV=8
+static int conv_cl_cv(int C) {
+  static const int cv = [] {
+    const char* e = std::getenv("MAMBA_AMD_CONV_CV");
+    return (e && std::atoi(e) == 8) ? 8 : 4;
+  }();
+  return (C % 4 == 0) ? cv : 8;
+}
+
 template <typename T>
 static hipError_t cl_fwd(const T* x, int64_t sxb, int64_t sxl, const float* w, const float* bias, T* out,
                          int64_t sob, int64_t sol, int Bn, int L, int C, int Wd, bool silu, hipStream_t st) {
@@ -789,9 +848,15 @@ static hipError_t cl_fwd(const T* x, int64_t sxb, int64_t sxl, const float* w, c
   if constexpr (std::is_same<T, bf16_t>::value) {
     if (vec) {
       constexpr int TF = 32;
-      dim3 g2((C + 511) / 512, (L + 4 * TF - 1) / (4 * TF), Bn);
-      W_SWITCH(Wd, hipLaunchKernelGGL((conv_cl_fwd_bf16_k<WW, TF>), g2, dim3(256), 0, st, x, sxb, sxl, w, bias, out,
-                                      sob, sol, L, C, silu));
+      if (conv_cl_cv(C) == 4) {
+        dim3 g2((C + 255) / 256, (L + 4 * TF - 1) / (4 * TF), Bn);
+        W_SWITCH(Wd, hipLaunchKernelGGL((conv_cl_fwd_bf16_k<WW, TF, 4>), g2, dim3(256), 0, st, x, sxb, sxl, w, bias,
+                                        out, sob, sol, L, C, silu));
+      } else {
+        dim3 g2((C + 511) / 512, (L + 4 * TF - 1) / (4 * TF), Bn);
+        W_SWITCH(Wd, hipLaunchKernelGGL((conv_cl_fwd_bf16_k<WW, TF, 8>), g2, dim3(256), 0, st, x, sxb, sxl, w, bias,
+                                        out, sob, sol, L, C, silu));
+      }
       return hipGetLastError();
     }
   }
@@ -827,8 +892,14 @@ static hipError_t cl_bwd(const T* x, int64_t sxb, int64_t sxl, const float* w, c
   dim3 grid((C + 511) / 512, (L + 4 * CLB_T - 1) / (4 * CLB_T), Bn), block(256);
   if constexpr (std::is_same<T, bf16_t>::value) {
     if (vec) {
-      W_SWITCH(Wd, hipLaunchKernelGGL((conv_cl_bwd_bf16_k<WW, CLB_T>), grid, block, 0, st, x, sxb, sxl, w, bias, g,
-                                      sgb, sgl, dx, sdb, sdl, part, pacc, L, C, silu));
+      if (conv_cl_cv(C) == 4) {
+        dim3 g4((C + 255) / 256, grid.y, grid.z);
+        W_SWITCH(Wd, hipLaunchKernelGGL((conv_cl_bwd_bf16_k<WW, CLB_T, 4>), g4, block, 0, st, x, sxb, sxl, w, bias,
+                                        g, sgb, sgl, dx, sdb, sdl, part, pacc, L, C, silu));
+      } else {
+        W_SWITCH(Wd, hipLaunchKernelGGL((conv_cl_bwd_bf16_k<WW, CLB_T, 8>), grid, block, 0, st, x, sxb, sxl, w, bias,
+                                        g, sgb, sgl, dx, sdb, sdl, part, pacc, L, C, silu));
+      }
       MAMBA_HIP_CHECK(hipGetLastError());
       return dw ? launch_colsum(part, conv_cl_bwd_partial_rows(Bn, L), C * (Wd + 1), dw, st) : hipSuccess;
     }

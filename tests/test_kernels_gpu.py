@@ -88,11 +88,12 @@ def test_gated_rmsnorm(cuda, nbg, D, G):
 
 
 @pytest.mark.parametrize("layout", ["cf", "cl"])
-@pytest.mark.parametrize("L", [1024, 77])
-def test_conv1d(cuda, layout, L):
+@pytest.mark.parametrize("L,d", [(1024, 384), (77, 384), (300, 1800)])
+def test_conv1d(cuda, layout, L, d):
+    """d = 1800: a channel-last width that is not a multiple of the 256 channels of a workgroup."""
     from mamba_distributed_amd.ops.conv1d import causal_conv1d_fn
     torch.manual_seed(2)
-    b, d, W = 3, 384, 4
+    b, W = 3, 4
     if layout == "cf":
         base = torch.randn(b, 2 * d, L, device=cuda, dtype=torch.bfloat16)   # x = first half of channels
     else:
