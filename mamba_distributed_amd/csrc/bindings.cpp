@@ -445,6 +445,45 @@ void ssd_common(mamba_amd::SSDArgs& a, const Tensor& x, const Tensor& dt, const 
   a.softplus = softplus; a.dt_min = (float)dt_min; a.dt_max = (float)dt_max;
 }
 
+// fp32 sequential SSD forward (evaluation in fp32): x (b,l,h,64), dt (b,l,h), B/C (b,l,g,n) fp32
+std::tuple<Tensor, Tensor> ssd_fwd_f32(Tensor x, Tensor dt, Tensor A, Tensor Bm, Tensor Cm, optional<Tensor> D,
+                                       optional<Tensor> dt_bias, optional<Tensor> init, bool softplus,
+                                       double dt_min, double dt_max, bool want_final) {
+  check_cuda(x, "x");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto f32 = [](const Tensor& t) { return t.scalar_type() == at::kFloat; };
+  TORCH_CHECK(f32(x) && f32(dt) && f32(Bm) && f32(Cm), "ssd_fwd_f32: fp32 operands");
+  TORCH_CHECK(x.dim() == 4 && x.size(3) == 64 && x.stride(3) == 1, "x must be (b,l,h,64), unit p");
+  TORCH_CHECK(Bm.dim() == 4 && Cm.sizes() == Bm.sizes() && Bm.stride(3) == 1 && Cm.stride(3) == 1, "B/C (b,l,g,n)");
+  mamba_amd::SSDF32Args a{};
+  a.B = x.size(0); a.L = x.size(1); a.H = x.size(2); a.G = Bm.size(2); a.N = Bm.size(3);
+  TORCH_CHECK(a.N == 64 || a.N == 128, "d_state 64 or 128");
+  TORCH_CHECK(a.H % a.G == 0 && Bm.size(0) == a.B && Bm.size(1) == a.L, "B/C shape");
+  TORCH_CHECK(dt.dim() == 3 && dt.size(0) == a.B && dt.size(1) == a.L && dt.size(2) == a.H, "dt shape");
+  Tensor Af = f32c(A), Df = f32c_opt(D), bf = f32c_opt(dt_bias);
+  TORCH_CHECK(Af.numel() == a.H && (!Df.defined() || Df.numel() == a.H), "A / D per head");
+  a.x = x.data_ptr<float>(); a.sxb = x.stride(0); a.sxl = x.stride(1); a.sxh = x.stride(2);
+  a.dt = dt.data_ptr<float>(); a.sdtb = dt.stride(0); a.sdtl = dt.stride(1); a.sdth = dt.stride(2);
+  a.A = Af.data_ptr<float>(); a.D = fptr(Df); a.dt_bias = fptr(bf);
+  a.Bm = Bm.data_ptr<float>(); a.sBb = Bm.stride(0); a.sBl = Bm.stride(1); a.sBg = Bm.stride(2);
+  a.Cm = Cm.data_ptr<float>(); a.sCb = Cm.stride(0); a.sCl = Cm.stride(1); a.sCg = Cm.stride(2);
+  Tensor initc;
+  if (init.has_value() && init->defined()) {
+    initc = init->to(at::kFloat).contiguous();
+    TORCH_CHECK(initc.numel() == (int64_t)a.B * a.H * 64 * a.N, "initial states (b,h,p,n)");
+    a.init = initc.data_ptr<float>();
+  }
+  auto y = at::empty({a.B, a.L, a.H, 64}, x.options());
+  a.y = y.data_ptr<float>(); a.syb = y.stride(0); a.syl = y.stride(1); a.syh = y.stride(2);
+  Tensor fin = want_final ? at::empty({a.B, a.H, 64, a.N}, x.options()) : at::empty({0}, x.options());
+  a.final_state = want_final ? fin.data_ptr<float>() : nullptr;
+  a.softplus = softplus;
+  a.clamp = !(dt_min == 0.0 && std::isinf(dt_max));
+  a.dt_min = (float)dt_min; a.dt_max = (float)dt_max;
+  HIPCHK(mamba_amd::launch_ssd_fwd_f32(a, cur_stream()));
+  return {y, fin};
+}
+
 std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> ssd_fwd(Tensor x, Tensor dt, Tensor A, Tensor Bm, Tensor Cm,
                                                            optional<Tensor> D, optional<Tensor> dt_bias,
                                                            optional<Tensor> init, int64_t chunk, bool softplus,
@@ -958,6 +997,8 @@ TORCH_LIBRARY(mamba_amd, m) {
         "Tensor? initial_states, Tensor? dfinal, Tensor(a!)? dx_out, Tensor(z!)? part_buf=None, int part_mode=0) "
         "-> (Tensor, Tensor, Tensor, Tensor)");
   m.def("conv1d_update(Tensor x, Tensor(a!) conv_state, Tensor weight, Tensor? bias, bool silu) -> Tensor");
+  m.def("ssd_fwd_f32(Tensor x, Tensor dt, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? dt_bias, Tensor? init, "
+        "bool softplus, float dt_min, float dt_max, bool want_final) -> (Tensor, Tensor)");
   m.def("ssd_fwd(Tensor x, Tensor dt, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? dt_bias, Tensor? init, "
         "int chunk, bool softplus, float dt_min, float dt_max, bool A_is_log=False, Tensor? seq_idx=None) "
         "-> (Tensor, Tensor, Tensor, Tensor, Tensor)");
@@ -1011,6 +1052,7 @@ TORCH_LIBRARY_IMPL(mamba_amd, CUDA, m) {
   m.impl("conv1d_cl_var_fwd", &conv1d_cl_var_fwd);
   m.impl("conv1d_cl_var_bwd", &conv1d_cl_var_bwd);
   m.impl("ssd_fwd", &ssd_fwd);
+  m.impl("ssd_fwd_f32", &ssd_fwd_f32);
   m.impl("ssd_bwd", &ssd_bwd);
   m.impl("selscan_fwd", &selscan_fwd);
   m.impl("selscan_bwd", &selscan_bwd);

@@ -41,6 +41,22 @@ struct SSDArgs {
   float* part_dA; float* part_dD; float* part_dbias;  // (b, nc, h)
 };
 
+// fp32 sequential SSD forward (evaluation in fp32, e.g. the reference's HellaSwag protocol); P = 64,
+// N = 64 / 128, no varlen.  Outputs y (b, l, h, p) and optionally the final state (b, h, p, n).
+struct SSDF32Args {
+  int B, L, H, G, N;
+  const float* x; int64_t sxb, sxl, sxh;       // unit p
+  const float* dt; int64_t sdtb, sdtl, sdth;   // raw dt
+  const float* A; const float* D; const float* dt_bias;
+  const float* Bm; int64_t sBb, sBl, sBg;      // unit n
+  const float* Cm; int64_t sCb, sCl, sCg;
+  const float* init;                           // (B, H, 64, N) contiguous or null
+  float* y; int64_t syb, syl, syh;             // unit p
+  float* final_state;                          // (B, H, 64, N) contiguous or null
+  bool softplus, clamp; float dt_min, dt_max;
+};
+hipError_t launch_ssd_fwd_f32(const SSDF32Args& a, hipStream_t st);
+
 hipError_t launch_ssd_fwd(const SSDArgs& a, hipStream_t st);
 hipError_t launch_ssd_bwd(const SSDArgs& a, hipStream_t st);
 

@@ -1048,6 +1048,67 @@ static void launch_walk(const SSDArgs& a, int depth, hipStream_t st) {
     else return hipErrorInvalidValue;                           \
   } while (0)
 
+// ============================== fp32 sequential forward (evaluation) =========================
+// The reference evaluates HellaSwag in fp32 (eval.py); the MFMA kernels above are bf16.  This path keeps
+// every operand fp32 and runs the recurrence itself, step by step (S_t = e^{dt A} S_{t-1} + dt x_t B_t^T,
+// y_t = S_t C_t + D x_t): one 256-thread workgroup per (b, h), thread = (row p = tid / 4, a quarter of
+// the N states), 16 steps of B / C / x / dt staged in LDS at a time, y summed over the quad by DPP.
+// Not a training path (no backward); throughput is irrelevant next to the eval's GEMMs.
+template <int N>
+__global__ __launch_bounds__(256) void ssd_fwd_f32_k(SSDF32Args a) {
+  constexpr int NS = N / 4, TS = 16;
+  __shared__ float Bs[TS][N], Cs[TS][N], Xs[TS][P], dts[TS];
+  const int h = blockIdx.x, b = blockIdx.y, g = h / (a.H / a.G);
+  const int p = threadIdx.x >> 2, nq = threadIdx.x & 3;
+  const float Ah = a.A[h], Dh = a.D ? a.D[h] : 0.f, bias = a.dt_bias ? a.dt_bias[h] : 0.f;
+  const int64_t srow = (((int64_t)b * a.H + h) * P + p) * N + nq * NS;
+  float S[NS];
+#pragma unroll
+  for (int j = 0; j < NS; ++j) S[j] = a.init ? a.init[srow + j] : 0.f;
+  for (int t0 = 0; t0 < a.L; t0 += TS) {
+    const int nt = min(TS, a.L - t0);
+    __syncthreads();  // the previous block of steps is consumed
+    for (int i = threadIdx.x; i < nt * N; i += 256) {
+      const int tt = i / N, n = i % N;
+      Bs[tt][n] = a.Bm[(int64_t)b * a.sBb + (int64_t)(t0 + tt) * a.sBl + (int64_t)g * a.sBg + n];
+      Cs[tt][n] = a.Cm[(int64_t)b * a.sCb + (int64_t)(t0 + tt) * a.sCl + (int64_t)g * a.sCg + n];
+    }
+    for (int i = threadIdx.x; i < nt * P; i += 256) {
+      const int tt = i / P, pp = i % P;
+      Xs[tt][pp] = a.x[(int64_t)b * a.sxb + (int64_t)(t0 + tt) * a.sxl + (int64_t)h * a.sxh + pp];
+    }
+    if (threadIdx.x < nt) {
+      float v = a.dt[(int64_t)b * a.sdtb + (int64_t)(t0 + threadIdx.x) * a.sdtl + (int64_t)h * a.sdth] + bias;
+      if (a.softplus) v = v > 20.f ? v : log1pf(expf(v));  // torch.nn.functional.softplus (threshold 20)
+      if (a.clamp) v = fminf(fmaxf(v, a.dt_min), a.dt_max);
+      dts[threadIdx.x] = v;
+    }
+    __syncthreads();
+    for (int tt = 0; tt < nt; ++tt) {
+      const float d = dts[tt], dA = expf(d * Ah), xv = Xs[tt][p], dx = d * xv;
+      float yp = 0.f;
+#pragma unroll
+      for (int j = 0; j < NS; ++j) {
+        S[j] = fmaf(dA, S[j], dx * Bs[tt][nq * NS + j]);
+        yp = fmaf(S[j], Cs[tt][nq * NS + j], yp);
+      }
+      yp += __shfl_xor(yp, 1, 4);
+      yp += __shfl_xor(yp, 2, 4);
+      if (nq == 0) a.y[(int64_t)b * a.syb + (int64_t)(t0 + tt) * a.syl + (int64_t)h * a.syh + p] = fmaf(Dh, xv, yp);
+    }
+  }
+  if (a.final_state) {
+#pragma unroll
+    for (int j = 0; j < NS; ++j) a.final_state[srow + j] = S[j];
+  }
+}
+
+hipError_t launch_ssd_fwd_f32(const SSDF32Args& a, hipStream_t st) {
+  if (a.H % a.G != 0 || (a.N != 64 && a.N != 128)) return hipErrorInvalidValue;
+  N_SWITCH(a.N, hipLaunchKernelGGL(ssd_fwd_f32_k<NN>, dim3(a.H, a.B), dim3(256), 0, st, a));
+  return hipGetLastError();
+}
+
 hipError_t launch_ssd_fwd(const SSDArgs& a, hipStream_t st) {
   const int64_t waves = (int64_t)a.B * a.H * a.nc;
   hipLaunchKernelGGL(ssd_cumsum_k, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, a);

@@ -71,6 +71,19 @@ class _SSDFn(torch.autograd.Function):
                 None, None, None, None, None)
 
 
+def _f32_eval_ok(x, dt, B, C, D, init, seq_idx) -> bool:
+    """fp32 SSD forward on the native sequential kernel: fp32 operands, no autograd, headdim 64,
+    d_state 64/128, per-head D, no packed sequences."""
+    if x.dtype != torch.float32 or B.dtype != torch.float32 or C.dtype != torch.float32:
+        return False
+    if not _ext.use_native(x) or seq_idx is not None or x.shape[-1] != 64 or B.shape[-1] not in (64, 128):
+        return False
+    if D is not None and D.dim() != 1:
+        return False
+    ts = [t for t in (x, dt, B, C, D, init) if t is not None]
+    return not (torch.is_grad_enabled() and any(t.requires_grad for t in ts))
+
+
 def mamba_chunk_scan_combined(x, dt, A, B, C, chunk_size=256, D=None, z=None, dt_bias=None,
                               initial_states=None, seq_idx=None, dt_softplus=False,
                               dt_limit=(0.0, _INF), return_final_states=False):
@@ -80,8 +93,17 @@ def mamba_chunk_scan_combined(x, dt, A, B, C, chunk_size=256, D=None, z=None, dt
     restarts at every change (native: the in-chunk cumsum gets a -256 offset at each sequence
     start, so every decay factor across the boundary is exactly 0 in fp32 -- the same masks as
     upstream, with unchanged gradients).  ``initial_states`` belong to the row's first sequence."""
-    # native kernels are bf16 (the training/serving dtype); fp32 activations (e.g. the reference's
-    # fp32 HellaSwag eval) take the fp32 reference path
+    # native MFMA kernels are bf16 (the training/serving dtype); fp32 activations without autograd (the
+    # reference's fp32 HellaSwag eval) run the native fp32 sequential forward
+    if _f32_eval_ok(x, dt, B, C, D, initial_states, seq_idx):
+        x, B, C = (t if t.stride(-1) == 1 else t.contiguous() for t in (x, B, C))
+        y, fin = _ext.ops().ssd_fwd_f32(x, dt.float(), A, B, C, D, dt_bias,
+                                        None if initial_states is None else initial_states.float(),
+                                        dt_softplus, float(dt_limit[0]), float(dt_limit[1]), return_final_states)
+        if z is not None:
+            y = y * F.silu(z.float())
+        y = y.to(x.dtype)
+        return (y, fin) if return_final_states else y
     if x.dtype == torch.bfloat16 and _ext.use_native(x) and (D is None or D.dim() == 1):
         out = _SSDFn.apply(x, dt, A, B, C, D, dt_bias, initial_states, dt_softplus,
                            float(dt_limit[0]), float(dt_limit[1]), return_final_states, seq_idx)
@@ -198,7 +220,9 @@ class _Mamba2InnerFn(torch.autograd.Function):
 
 def mamba2_inner_ref(zxbcdt, conv_w, conv_b, dt_bias, A, D, norm_w, eps, headdim, ngroups, d_state,
                      dt_limit=(0.0, _INF), norm_before_gate=False, chunk_size=64, initial_states=None,
-                     seq_idx=None, return_final_states=False):
+                     seq_idx=None, return_final_states=False, native_ssd=False):
+    """The composed reference (PyTorch ops); ``native_ssd``: the SSD step through
+    ``mamba_chunk_scan_combined`` (fp32 inference -> the native fp32 forward)."""
     b, l, dproj = zxbcdt.shape
     H = dt_bias.shape[0]
     di = H * headdim
@@ -208,10 +232,11 @@ def mamba2_inner_ref(zxbcdt, conv_w, conv_b, dt_bias, A, D, norm_w, eps, headdim
     xBC = causal_conv1d_ref(xBC.transpose(1, 2), conv_w.reshape(conv_dim, -1), conv_b, "silu",
                             seq_idx=seq_idx).transpose(1, 2)
     x, Bm, Cm = torch.split(xBC, [di, gn, gn], dim=-1)
-    y = ssd_chunked_ref(x.unflatten(-1, (H, headdim)), dt, A, Bm.unflatten(-1, (ngroups, d_state)),
-                        Cm.unflatten(-1, (ngroups, d_state)), chunk_size, D=D, dt_bias=dt_bias,
-                        dt_softplus=True, dt_limit=dt_limit, initial_states=initial_states,
-                        return_final_states=return_final_states, seq_idx=seq_idx)
+    ssd = mamba_chunk_scan_combined if native_ssd else ssd_chunked_ref
+    y = ssd(x.unflatten(-1, (H, headdim)), dt, A, Bm.unflatten(-1, (ngroups, d_state)),
+            Cm.unflatten(-1, (ngroups, d_state)), chunk_size, D=D, dt_bias=dt_bias,
+            dt_softplus=True, dt_limit=dt_limit, initial_states=initial_states,
+            return_final_states=return_final_states, seq_idx=seq_idx)
     y, final = y if return_final_states else (y, None)
     y = gated_rms_norm_ref(y.flatten(-2), z, norm_w, eps, di // ngroups, norm_before_gate)
     return (y, final) if return_final_states else y
@@ -240,7 +265,7 @@ def mamba2_inner_fn(zxbcdt, conv_w, conv_b, dt_bias, A, D, norm_w, eps, headdim,
         A = -torch.exp(A.float())
     return mamba2_inner_ref(zxbcdt, conv_w, conv_b, dt_bias, A, D, norm_w, eps, headdim, ngroups,
                             d_state, dt_limit, norm_before_gate, ref_chunk_size, initial_states,
-                            seq_idx, return_final_states)
+                            seq_idx, return_final_states, native_ssd=True)
 
 
 def mamba_split_conv1d_scan_combined(zxbcdt, conv1d_weight, conv1d_bias, dt_bias, A, D, chunk_size,

@@ -908,3 +908,60 @@ def test_mamba1_deferred_wgrad_matches_default(cuda, monkeypatch):
         grads[v] = {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
     for n in grads["0"]:
         assert rel(grads["1"][n], grads["0"][n]) < 1e-2, n
+
+
+@pytest.mark.parametrize("b,L,H,G,N,with_init", [(2, 200, 8, 1, 128, True), (1, 64, 4, 2, 64, False),
+                                                 (3, 1030, 24, 1, 128, False)])
+def test_ssd_fp32_native_forward(cuda, b, L, H, G, N, with_init):
+    """fp32 inference (the reference's fp32 HellaSwag protocol) runs the native fp32 sequential SSD
+    forward: y and the final state vs the fp32 chunked reference, incl. z gate and dt limits."""
+    from mamba_distributed_amd.ops.ssd import mamba_chunk_scan_combined
+    g = torch.Generator(device=cuda).manual_seed(40)
+    x = torch.randn(b, L, H, 64, generator=g, device=cuda)
+    dt = torch.randn(b, L, H, generator=g, device=cuda) * 0.5 - 1
+    A = -torch.rand(H, generator=g, device=cuda) * 4 - 0.2
+    Bm = torch.randn(b, L, G, N, generator=g, device=cuda) * 0.5
+    Cm = torch.randn(b, L, G, N, generator=g, device=cuda) * 0.5
+    D = torch.randn(H, generator=g, device=cuda)
+    dtb = torch.randn(H, generator=g, device=cuda) * 0.3
+    z = torch.randn(b, L, H, 64, generator=g, device=cuda)
+    init = torch.randn(b, H, 64, N, generator=g, device=cuda) * 0.3 if with_init else None
+    ops = torch.ops.mamba_amd
+    kw = dict(D=D, z=z, dt_bias=dtb, initial_states=init, dt_softplus=True, dt_limit=(0.01, 3.0),
+              return_final_states=True)
+    with torch.no_grad():
+        y, fin = mamba_chunk_scan_combined(x, dt, A, Bm, Cm, 64, **kw)
+        y2, fin2 = R.ssd_chunked_ref(x.double(), dt.double(), A.double(), Bm.double(), Cm.double(), 64,
+                                     D=D.double(), z=z.double(), dt_bias=dtb.double(),
+                                     initial_states=None if init is None else init.double(), dt_softplus=True,
+                                     dt_limit=(0.01, 3.0), return_final_states=True)
+        yn, finn = ops.ssd_fwd_f32(x, dt, A, Bm, Cm, D, dtb, init, True, 0.01, 3.0, True)
+    assert y.dtype == torch.float32
+    assert rel(y, y2) < 1e-4, rel(y, y2)
+    assert rel(fin, fin2) < 1e-4, rel(fin, fin2)
+    assert rel(yn * torch.nn.functional.silu(z), y) < 1e-6
+
+
+def test_mamba2_layer_fp32_eval_uses_native_ssd(cuda, monkeypatch):
+    """Mamba-2 layer in fp32 under no_grad: the SSD step runs ssd_fwd_f32 (native) and matches the
+    all-reference forward."""
+    from mamba_distributed_amd.models.mamba2 import Mamba2
+    from mamba_distributed_amd.ops import ssd as ssd_mod
+    torch.manual_seed(9)
+    layer = Mamba2(256, d_state=128, headdim=64, device=cuda).float().eval()
+    u = torch.randn(2, 150, 256, device=cuda)
+    used = []
+    orig = ssd_mod._f32_eval_ok
+
+    def spy(*a, **k):
+        r = orig(*a, **k)
+        used.append(r)
+        return r
+    monkeypatch.setattr(ssd_mod, "_f32_eval_ok", spy)
+    with torch.no_grad():
+        y = layer(u)
+    assert used and all(used)
+    monkeypatch.setenv("MAMBA_AMD_FORCE_REFERENCE", "1")
+    with torch.no_grad():
+        yr = layer(u)
+    assert rel(y, yr) < 1e-4, rel(y, yr)
