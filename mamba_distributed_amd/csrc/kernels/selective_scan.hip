@@ -1087,41 +1087,48 @@ __global__ __launch_bounds__(256) void selscan_bwd_fast_k(SelScanArgs a) {
 constexpr int SGB_T = kSelScanCarrySG;  // backward tile = forward carry granularity
 static_assert(SGB_T == SG_T, "the forward writes a carry at every one of its tiles");
 
-// v_permlane32_swap / v_permlane16_swap: x <- [x_lo, y_lo], y <- [x_hi, y_hi] (32-lane halves), and
-// x <- [x_r0, y_r0, x_r2, y_r2], y <- [x_r1, y_r1, x_r3, y_r3] (16-lane rows).  Inline asm: the compiler's
-// builtins for these return the first result twice (ROCm 7.2 clang: `v_add x, x` after the swap).  The
-// s_nop covers a VALU / swap write -> swap read (2 wait states, as the compiler places between swaps).
-__device__ __forceinline__ void permlane32_swap(float& x, float& y) {
-  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(x), "+v"(y));
-}
-__device__ __forceinline__ void permlane16_swap(float& x, float& y) {
-  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
-}
-// sum over the 64 lanes of 8 values per lane; lane l returns the total of value (l >> 3) & 7
-__device__ __forceinline__ float lane_sum8(const float (&v)[8]) {
+// v_permlane32_swap / v_permlane16_swap (inline asm: the clang builtins of this ROCm return the first
+// result twice, `v_add x, x` after the swap): x <- [x_lo, y_lo], y <- [x_hi, y_hi] (32-lane halves) and
+// x <- [x_r0, y_r0, x_r2, y_r2], y <- [x_r1, y_r1, x_r3, y_r3] (16-lane rows).  The s_nop covers a VALU
+// write -> swap read (2 wait states, as the compiler places between swaps).
+// sums over the 64 lanes of two sets of 8 values per lane (dB and dC of two steps); lane l returns the
+// totals of value (l >> 3) & 7 of each set.  The independent swaps of a stage share one asm block, so only
+// its first instruction needs the wait states after the VALU writes of its inputs.
+__device__ __forceinline__ void lane_sum8x2(const float (&u)[8], const float (&v)[8], float& ru, float& rv) {
   const int lane = threadIdx.x & 63;
-  float w4[4], w2[2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {  // xor 32: lanes 0-31 keep value i, lanes 32-63 value i + 4
-    float x = v[i], y = v[i + 4];
-    permlane32_swap(x, y);
-    w4[i] = x + y;
-  }
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {  // xor 16: even rows keep i, odd rows i + 2
-    float x = w4[i], y = w4[i + 2];
-    permlane16_swap(x, y);
-    w2[i] = x + y;
-  }
-  // xor 8 (row_ror:8): bit 3 clear keeps value 0, set keeps value 1
-  const float p = w2[0] + dppf<0x128>(0.f, w2[0]);
-  const float q = w2[1] + dppf<0x128>(0.f, w2[1]);
-  float z = (lane & 8) ? q : p;
-  // the remaining 8 lanes of each half row hold the same value: half-row mirror, then the quad
-  z += dppf<0x141>(0.f, z);
-  z += dppf<0xB1>(0.f, z);  // quad_perm [1,0,3,2]
-  z += dppf<0x4E>(0.f, z);  // quad_perm [2,3,0,1]
-  return z;
+  float a0 = u[0], a1 = u[1], a2 = u[2], a3 = u[3], b0 = u[4], b1 = u[5], b2 = u[6], b3 = u[7];
+  float c0 = v[0], c1 = v[1], c2 = v[2], c3 = v[3], d0 = v[4], d1 = v[5], d2 = v[6], d3 = v[7];
+  // xor 32: lanes 0-31 keep value i, lanes 32-63 value i + 4
+  asm volatile("s_nop 1\n\t"
+               "v_permlane32_swap_b32 %0, %4\n\tv_permlane32_swap_b32 %1, %5\n\t"
+               "v_permlane32_swap_b32 %2, %6\n\tv_permlane32_swap_b32 %3, %7\n\t"
+               "v_permlane32_swap_b32 %8, %12\n\tv_permlane32_swap_b32 %9, %13\n\t"
+               "v_permlane32_swap_b32 %10, %14\n\tv_permlane32_swap_b32 %11, %15"
+               : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3),
+                 "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3));
+  float e0 = a0 + b0, e1 = a1 + b1, e2 = a2 + b2, e3 = a3 + b3;
+  float f0 = c0 + d0, f1 = c1 + d1, f2 = c2 + d2, f3 = c3 + d3;
+  // xor 16: even rows keep i, odd rows i + 2
+  asm volatile("s_nop 1\n\t"
+               "v_permlane16_swap_b32 %0, %2\n\tv_permlane16_swap_b32 %1, %3\n\t"
+               "v_permlane16_swap_b32 %4, %6\n\tv_permlane16_swap_b32 %5, %7"
+               : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3), "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3));
+  const float g0 = e0 + e2, g1 = e1 + e3, h0 = f0 + f2, h1 = f1 + f3;
+  // xor 8 (row_ror:8): bit 3 clear keeps value 0, set keeps value 1; then the remaining 8 lanes of each
+  // half row hold the same value: half-row mirror, then the quad
+  const bool hi = lane & 8;
+  const float pu0 = g0 + dppf<0x128>(0.f, g0), pu1 = g1 + dppf<0x128>(0.f, g1);  // DPP on every lane,
+  const float pv0 = h0 + dppf<0x128>(0.f, h0), pv1 = h1 + dppf<0x128>(0.f, h1);  // then the select
+  float zu = hi ? pu1 : pu0;
+  float zv = hi ? pv1 : pv0;
+  zu += dppf<0x141>(0.f, zu);
+  zv += dppf<0x141>(0.f, zv);
+  zu += dppf<0xB1>(0.f, zu);  // quad_perm [1,0,3,2]
+  zv += dppf<0xB1>(0.f, zv);
+  zu += dppf<0x4E>(0.f, zu);  // quad_perm [2,3,0,1]
+  zv += dppf<0x4E>(0.f, zv);
+  ru = zu;
+  rv = zv;
 }
 
 __global__ __launch_bounds__(256) void selscan_bwd_sg_k(SelScanArgs a) {
@@ -1279,7 +1286,8 @@ __global__ __launch_bounds__(256) void selscan_bwd_sg_k(SelScanArgs a) {
         sS[w][1][t][lane] = s2.x + s2.y;
         sS[w][2][t][lane] = yy.x + yy.y;
       }
-      const float rb = lane_sum8(cB), rc = lane_sum8(cC);
+      float rb, rc;
+      lane_sum8x2(cB, cC, rb, rc);
       if ((lane & 7) == 0) {
         pdB[t0 + t2 + opd] = rb;
         pdC[t0 + t2 + opd] = rc;
