@@ -886,6 +886,26 @@ Tensor gp_mm(Tensor A, Tensor B, optional<Tensor> out, int64_t la, int64_t lb, i
 int64_t gp_splits(int64_t M, int64_t N, int64_t K) { return mamba_amd::gemm_pipe_splits((int)M, (int)N, (int)K); }
 void gp_set_ablate(int64_t bits) { mamba_amd::gemm_pipe_set_ablate((int)bits); }
 
+// A HIP stream whose kernels may only be dispatched to the CUs set in `mask` (32 CUs per word, the
+// runtime's logical CU order; hipExtStreamCreateWithCUMask).  Returned as the raw hipStream_t so Python
+// wraps it in torch.cuda.ExternalStream.  Used to partition the CUs between the compute-bound
+// weight-gradient / micro-batch streams and the memory-bound backward (utils/cu_mask.py).  The stream
+// lives for the process (never destroyed: torch may still hold events recorded on it at exit).
+int64_t cu_masked_stream(int64_t device, std::vector<int64_t> mask) {
+  TORCH_CHECK(!mask.empty() && mask.size() <= 64, "cu_masked_stream: 1..64 mask words");
+  std::vector<uint32_t> words(mask.size());
+  bool any = false;
+  for (size_t i = 0; i < mask.size(); ++i) {
+    words[i] = (uint32_t)(mask[i] & 0xffffffffLL);
+    any = any || words[i] != 0u;
+  }
+  TORCH_CHECK(any, "cu_masked_stream: empty CU mask");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(at::Device(at::kCUDA, (c10::DeviceIndex)device));
+  hipStream_t s = nullptr;
+  HIPCHK(hipExtStreamCreateWithCUMask(&s, (uint32_t)words.size(), words.data()));
+  return reinterpret_cast<int64_t>(s);
+}
+
 // out (+)= sum over the leading dim of part (S, ...) in fixed order; out fp32 contiguous, numel(out) = numel(part[0])
 void gp_reduce(Tensor part, Tensor out, bool accumulate) {
   check_cuda(part, "part");
@@ -1021,6 +1041,7 @@ TORCH_LIBRARY(mamba_amd, m) {
   m.def("gp_splits(int M, int N, int K) -> int", &gp_splits);
   m.def("part_rows(str kind, int a, int b=0) -> int", &part_rows);
   m.def("gp_set_ablate(int bits) -> ()", &gp_set_ablate);
+  m.def("cu_masked_stream(int device, int[] mask) -> int", &cu_masked_stream);
   m.def("gp_reduce(Tensor part, Tensor(a!) out, bool accumulate=False) -> ()");
   m.def("gemm_skinny(Tensor A, Tensor B, Tensor(a!)? out=None, bool accumulate=False) -> Tensor");
   m.def("ssm_state_update(Tensor(a!) state, Tensor x, Tensor dt, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? z, "

@@ -120,12 +120,16 @@ struct GemmPipeArgs {
 // four LDS-DMAs or an MFMA waiting on a fragment read issued fewer than 16 MFMAs earlier.
 // (A persistent variant that streams the next output tile's K-tiles behind this one's was measured slower:
 // the dynamic buffer parity and tile bookkeeping cost more in the K-loop than the hidden epilogue gained.)
-template <int LA, int LB, int MI, int EPI, int ABL = 0, int WN = 4>
+template <int LA, int LB, int MI, int EPI, int ABL = 0, int WN = 4, int NJ_ = 0>
 __global__ __launch_bounds__(128 * WN) void gemm_pipe_k(GemmPipeArgs a) {
   // WN = 4: 8 waves as 2 x 4, each (BM/2) x 64; WN = 2: 4 waves as 2 x 2, each (BM/2) x 128 (one wave per
-  // SIMD, accumulators in AGPRs, 1/3 fewer fragment bytes per MFMA)
+  // SIMD, accumulators in AGPRs, 1/3 fewer fragment bytes per MFMA).
+  // NJ_ = 3 (KC.KC only): BN = 192, each wave (BM/2) x 48 -- for N = 768 outputs (the d_model side of the
+  // 280M projections) 4 column tiles instead of 3, so M = 32768 makes 512 tiles = exactly 2 rounds of
+  // 256 CUs, where 256-wide tiles make 384 = 1.5 rounds (the second half-empty)
+  static_assert(NJ_ == 0 || (NJ_ == 3 && LB == 0 && WN == 4), "BN = 192 is a KC-operand, 8-wave tile");
   constexpr int NT = 128 * WN;
-  constexpr int NJ = 16 / WN;                 // 16-col tiles per wave (BN = 256)
+  constexpr int NJ = NJ_ ? NJ_ : 16 / WN;     // 16-col tiles per wave (BN = 256, or 192)
   constexpr int BM = 32 * MI, BN = 16 * NJ * WN;
   constexpr int SA = BM * 128, SB = BN * 128;  // bytes per K-tile image
   constexpr int SS = SA + SB;
@@ -377,11 +381,14 @@ hipError_t launch_gemm_pipe(int la, int lb, const void* A, int64_t lda, const vo
   a.M = M; a.N = N; a.K = K; a.splits = splits;
   a.ablate = g_gp_ablate;
   a.kslice = ((K + splits - 1) / splits + GP_BK - 1) / GP_BK * GP_BK;
+  // tile code `bm`: 256 -> 256 x 256, 128 -> 128 x 256, 192 -> 256 x 192 (KC.KC), 1256 -> 256 x 256 on 4 waves
   const int BM = bm == 128 ? 128 : 256;
+  const int BN = bm == 192 ? 192 : 256;
+  if (bm == 192 && !(la == 0 && lb == 0)) return hipErrorInvalidValue;
   // 256 x 256 on 4 waves of 128 x 128 (one wave per SIMD, AGPR accumulators): measured 16-27 % slower than
   // the 8-wave tile under hipcc's schedule (profiles/r2_v3_gemm_pipe_bench.log); kept for A/B
   const bool w4 = bm == 1256;
-  const int ntiles = ((M + BM - 1) / BM) * ((N + 255) / 256) * splits;
+  const int ntiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN) * splits;
   const int nwg = ntiles;
 #define GP_LAUNCH(LA_, LB_, MI_, EPI_)                                                                 \
   if (w4 && LA_ == 0 && LB_ == 0)                                                                      \
@@ -394,10 +401,16 @@ hipError_t launch_gemm_pipe(int la, int lb, const void* A, int64_t lda, const vo
     case 1: GP_LAUNCH(LA_, LB_, MI_, 1); break; \
     default: GP_LAUNCH(LA_, LB_, MI_, 2); break; \
   }
-  if (a.ablate && la == 0 && lb == 0 && BM == 256 && epi == 0) {
+  if (a.ablate && la == 0 && lb == 0 && BM == 256 && BN == 256 && epi == 0) {
 #define GP_ABL(B_) case B_: hipLaunchKernelGGL((gemm_pipe_k<0, 0, 8, 0, B_>), dim3(nwg), dim3(GP_NT), 0, st, a); break;
     switch (a.ablate) { GP_ABL(1) GP_ABL(2) GP_ABL(4) GP_ABL(8) GP_ABL(5) GP_ABL(6) GP_ABL(14) default: break; }
 #undef GP_ABL
+  } else if (la == 0 && lb == 0 && BN == 192) {
+    switch (epi) {
+      case 0: hipLaunchKernelGGL((gemm_pipe_k<0, 0, 8, 0, 0, 4, 3>), dim3(nwg), dim3(GP_NT), 0, st, a); break;
+      case 1: hipLaunchKernelGGL((gemm_pipe_k<0, 0, 8, 1, 0, 4, 3>), dim3(nwg), dim3(GP_NT), 0, st, a); break;
+      default: hipLaunchKernelGGL((gemm_pipe_k<0, 0, 8, 2, 0, 4, 3>), dim3(nwg), dim3(GP_NT), 0, st, a); break;
+    }
   } else if (la == 0 && lb == 0) {
     if (BM == 256) { GP_EPI(0, 0, 8) } else { GP_EPI(0, 0, 4) }
   } else if (la == 0 && lb == 1) {

@@ -3,9 +3,10 @@
 Parameter names, shapes and init follow upstream ``mamba_ssm/modules/mamba2.py::Mamba2``
  so checkpoints interchange.  Training forward:
 
-    zxbcdt = in_proj(u)                      hipBLASLt, (b, l, 2di + 2GN + H), token-major
+    zxbcdt = in_proj(u)                      hipBLASLt fwd / dgrad, native wgrad; token-major
     y      = mamba2_inner_fn(zxbcdt, ...)    HIP: conv1d(xBC)+SiLU -> SSD -> gated RMSNorm
-    out    = out_proj(y)                     hipBLASLt
+    out    = out_proj(y)                     hipBLASLt fwd / dgrad, native wgrad
+(projection routing: ops/linear.py)
 
 The conv, SSD and norm kernels read their operands straight out of the strided zxbcdt buffer
 and the backward writes d(zxbcdt) as one buffer (ops/ssd.py).

@@ -82,7 +82,9 @@ def side_stream(device: torch.device):
     idx = device.index if device.index is not None else torch.cuda.current_device()
     s = _side.get(idx)
     if s is None:
-        s = torch.cuda.Stream(device=idx)
+        from ..utils.cu_mask import env_eighths, masked_stream
+        k = env_eighths("MAMBA_AMD_SIDE_CUS")  # optional CU partition (utils/cu_mask.py)
+        s = masked_stream(idx, k) if k else torch.cuda.Stream(device=idx)
         _side[idx] = s
     _side_dirty.add(idx)
     return s
@@ -147,6 +149,20 @@ def cached_cast(w: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
         return ent[1]
     t = w.to(dtype)
     _wcache[key] = (w, t)  # holding w keeps id(w) unique for the scope's lifetime
+    return t
+
+
+def cached_transpose(w: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    """``w.to(dtype).t().contiguous()`` (the input-gradient GEMM's k-contiguous B operand), reused across
+    the micro-steps of the current scope like ``cached_cast``."""
+    if _scope_depth == 0:
+        return w.to(dtype).t().contiguous()
+    key = (id(w), dtype, "t")
+    ent = _wcache.get(key)
+    if ent is not None and ent[0] is w:
+        return ent[1]
+    t = cached_cast(w, dtype).t().contiguous()
+    _wcache[key] = (w, t)
     return t
 
 

@@ -1,7 +1,8 @@
 """Bias-free projection (nn.Linear without bias) with a native weight-gradient GEMM.
 
-Forward and input-gradient GEMMs are plain GEMMs (no fusion) and run on whichever of hipBLASLt (pinned
-TunableOp table) and the native engine is faster for the shape (``utils/gemm_tuning``).  The weight
+Forward and input-gradient GEMMs are plain GEMMs (no fusion) on hipBLASLt with the pinned TunableOp table
+(``utils/gemm_tuning``), measured faster at these shapes than the native engine, whose 256 x 192 tile for the
+d_model-wide outputs stays available as an opt-in (``_narrow_native``).  The weight
 gradient dW = dY^T X reduces over all B*T tokens into a small output (3352 x 768 for in_proj), where the
 library leaves most CUs idle: the native engine (csrc/kernels/gemm_pipe.hip, ``gp_mm`` with both operands
 token-major) splits the tokens into S K-slices written as fp32 slabs.  Inside an accumulation scope the
@@ -81,12 +82,34 @@ def _dgrad_native(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return _ext.ops().gp_mm(dy2, w, None, 0, 1, 0, 1, 256)
 
 
+def _narrow_native() -> bool:
+    """MAMBA_AMD_NATIVE_NARROW=1 (opt-in; default off): GEMMs whose OUTPUT is d_model <= 1024 wide -- the out_proj
+    forward and the in_proj input gradient of the 280M models -- on the native engine's 256 x 192 tile
+    (gemm_pipe.hip, tile code 192): N = 768 makes 4 column tiles, so 32768 rows are 512 tiles = exactly two
+    rounds of 256 CUs, where 256-wide tiles (ours or the library's) leave the second round half empty.  The
+    input gradient reads W^T as a k-contiguous operand, transposed once per optimizer step
+    (grad_accum.cached_transpose).  Measured on one MI355X (profiles/r2_v7_narrow_tile_ab.txt): the out_proj
+    forward 71.4 us against hipBLASLt's 69.5 (256 x 256: 79.7), the in_proj input gradient 203 against 167,
+    whole 280M step -2.2 % (277.5k vs 283.6k tok/s, interleaved), so the library stays the default."""
+    import os
+    return os.environ.get("MAMBA_AMD_NATIVE_NARROW", "0") == "1"
+
+
+def _narrow_ok(a: torch.Tensor, n_out: int, k: int) -> bool:
+    return (a.is_cuda and a.dtype == torch.bfloat16 and a.dim() == 2 and a.stride(-1) == 1
+            and a.stride(0) % 8 == 0 and a.data_ptr() % 16 == 0 and a.shape[0] >= 8192
+            and 384 <= n_out <= 1024 and n_out % 8 == 0 and k % 8 == 0 and _narrow_native())
+
+
 class _ProjFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, cd):
         x2 = x.reshape(-1, x.shape[-1]).to(cd)
         w = grad_accum.cached_cast(weight, cd)
-        y = F.linear(x2, w)
+        if _narrow_ok(x2, w.shape[0], w.shape[1]) and w.is_contiguous():
+            y = _ext.ops().gp_mm(x2, w, None, 0, 0, 0, 1, 192)
+        else:
+            y = F.linear(x2, w)
         ctx.save_for_backward(x2, w)
         ctx.param = weight
         ctx.wdtype = weight.dtype
@@ -103,7 +126,12 @@ class _ProjFn(torch.autograd.Function):
             dy2 = dy2.contiguous()
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = _dgrad_native(dy2, w) if _native_dgrad_ok(dy2, w) else torch.mm(dy2, w)
+            if _narrow_ok(dy2, w.shape[1], w.shape[0]):
+                dx = _ext.ops().gp_mm(dy2, grad_accum.cached_transpose(ctx.param, w.dtype), None, 0, 0, 0, 1, 192)
+            elif _native_dgrad_ok(dy2, w):
+                dx = _dgrad_native(dy2, w)
+            else:
+                dx = torch.mm(dy2, w)
         dw = None
         if ctx.needs_input_grad[1]:
             p = ctx.param

@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--M", type=int, default=32768)
     a = ap.parse_args()
     assert _ext.load(), _ext.error()
+    from mamba_distributed_amd.utils.gemm_tuning import enable_tuned_gemms
+    print("tuned table:", enable_tuned_gemms())
     ops = torch.ops.mamba_amd
     dev = "cuda"
     M = a.M
@@ -41,7 +43,7 @@ def main():
         dy = torch.randn(M, N, device=dev).to(torch.bfloat16)
         fl = 2.0 * M * N * K
         ref = torch.nn.functional.linear(x, w)
-        for bm in (256, 128, 1256):
+        for bm in (256, 192, 128):
             try:
                 y = ops.gp_mm(x, w, None, 0, 0, 0, 1, bm)
             except RuntimeError as e:
@@ -53,7 +55,13 @@ def main():
         t = timeit(lambda: torch.nn.functional.linear(x, w), a.reps)
         print(f"{name:8s} fwd   hipBLASLt      {t:8.1f} us {fl / t / 1e6:7.1f} TF/s")
         refd = dy @ w
-        for bm in (256, 128, 1256):
+        wT = w.t().contiguous()  # (in, out): dgrad as a KC.KC product (a per-step cached transpose)
+        for bm in (192, 256):
+            d = ops.gp_mm(dy, wT, None, 0, 0, 0, 1, bm)
+            err = ((d.float() - refd.float()).norm() / refd.float().norm()).item()
+            t = timeit(lambda: ops.gp_mm(dy, wT, None, 0, 0, 0, 1, bm), a.reps)
+            print(f"{name:8s} dgrad gp_mm(W^T KC) bm={bm:4d} {t:8.1f} us {fl / t / 1e6:7.1f} TF/s  rel_err {err:.1e}")
+        for bm in (256, 128):
             try:
                 d = ops.gp_mm(dy, w, None, 0, 1, 0, 1, bm)
             except RuntimeError as e:

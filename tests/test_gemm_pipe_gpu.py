@@ -132,3 +132,19 @@ def test_gp_headline_shapes(cuda, which):
     else:
         C = ops.gp_mm(A, B, None, la, lb, 0, 1, 256)
         assert _rel(C, ref) < 8e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(32768, 768, 1536), (32768, 768, 3352), (1000, 200, 136), (4096, 392, 64)])
+def test_gp_tile_256x192(cuda, M, N, K):
+    """256 x 192 tile (tile code 192, KC.KC): out_proj forward and the in_proj input gradient with the
+    cached W^T, plus ragged M / N / K tails, vs fp32."""
+    ops = _ops()
+    g = torch.Generator(device=cuda).manual_seed(5)
+    A = torch.randn(M, K, device=cuda, generator=g).to(torch.bfloat16)
+    B = torch.randn(N, K, device=cuda, generator=g).to(torch.bfloat16)
+    ref = A.float() @ B.float().t()
+    C = ops.gp_mm(A, B, None, 0, 0, 0, 1, 192)
+    assert _rel(C, ref) < 8e-3
+    out = torch.zeros(1, M, N, device=cuda)
+    ops.gp_mm(A, B, out, 0, 0, 2, 1, 192)
+    assert _rel(out[0], ref) < 1e-5
