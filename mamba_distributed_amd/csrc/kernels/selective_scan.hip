@@ -1378,7 +1378,9 @@ static bool sg_shape_ok(const SelScanArgs& a) {
 // MAMBA_AMD_SELSCAN_LC=0 forces the time-parallel kernel (A/B, tests).
 // Measured at B=32, D=1536, L=1024, N=16 on MI355X: 290 us vs 345 us.
 static bool use_fwd_sg(const SelScanArgs& a) {
-  return sg_shape_ok(a) && a.L % SF_IT == 0 && !env_off("MAMBA_AMD_SELSCAN_LC") && (int64_t)a.B * a.D / 16 >= 2048;
+  // L >= SG_T: the per-tile B / C row reads start at min(t0, L - SG_T)
+  return sg_shape_ok(a) && a.L % SF_IT == 0 && a.L >= SG_T && !env_off("MAMBA_AMD_SELSCAN_LC") &&
+         (int64_t)a.B * a.D / 16 >= 2048;
 }
 // sequential-time backward: needs the forward's 16-step carries; MAMBA_AMD_SELSCAN_BWD_SG=0 keeps the
 // time-parallel backward (and 512-step carries)
