@@ -75,7 +75,7 @@ class _FusedMamba2Step:
             return False
         for blk in bb.layers:
             m = blk.mixer
-            if type(m) is not Mamba2 or blk.mlp is not None or m.norm_before_gate or m.in_proj.bias is not None \
+            if type(m) is not Mamba2 or m._general or blk.mlp is not None or m.norm_before_gate or m.in_proj.bias is not None \
                     or m.out_proj.bias is not None or getattr(m, "cp_group", None) is not None:
                 return False
             if m.conv1d.weight.dtype != torch.bfloat16 or m.headdim % 16 or m.d_state not in (64, 128, 256):

@@ -37,8 +37,6 @@ class Mamba2(nn.Module):
         factory = {"device": device, "dtype": dtype}
         super().__init__()
         assert process_group is None, "head-sharded TP: parallel.tensor_parallel.Mamba2TP.from_full / parallel.parallelize"
-        assert not D_has_hdim, "D_has_hdim is not supported"
-        assert rmsnorm, "the gated RMSNorm output path is the only supported one"
         self.d_model = d_model
         self.d_state = d_state
         self.d_conv = d_conv
@@ -47,7 +45,7 @@ class Mamba2(nn.Module):
         self.d_inner = int(expand * d_model)
         self.headdim = headdim
         self.d_ssm = self.d_inner if d_ssm is None else d_ssm
-        assert self.d_ssm == self.d_inner, "d_ssm < d_inner (extra MLP branch) not supported"
+        assert self.d_ssm <= self.d_inner
         self.ngroups = ngroups
         assert self.d_ssm % headdim == 0
         self.nheads = self.d_ssm // headdim
@@ -79,11 +77,18 @@ class Mamba2(nn.Module):
         A = torch.empty(self.nheads, dtype=torch.float32, device=device).uniform_(*A_init_range)
         self.A_log = nn.Parameter(torch.log(A).to(dtype=dtype or torch.float32))
         self.A_log._no_weight_decay = True
-        self.D = nn.Parameter(torch.ones(self.nheads, device=device))
+        self.D = nn.Parameter(torch.ones(self.d_ssm if D_has_hdim else self.nheads, device=device))
         self.D._no_weight_decay = True
-        self.norm = RMSNormGated(self.d_ssm, eps=1e-5, norm_before_gate=norm_before_gate,
-                                 group_size=self.d_ssm // ngroups, **factory)
+        if rmsnorm:
+            self.norm = RMSNormGated(self.d_ssm, eps=1e-5, norm_before_gate=norm_before_gate,
+                                     group_size=self.d_ssm // ngroups, **factory)
         self.out_proj = nn.Linear(self.d_inner, d_model, bias=bias, **factory)
+        # upstream's other Mamba2 variants (mamba_ssm/modules/mamba2.py): the gate-only output without the
+        # norm (rmsnorm=False), a per-channel skip D (D_has_hdim) and a gated-MLP branch beside a narrower
+        # SSM (d_ssm < d_inner).  They run the same native ops unfused (_forward_general); the default
+        # configuration keeps the fused chain.
+        self.d_mlp = (d_in_proj - 2 * self.d_ssm - 2 * ngroups * d_state - self.nheads) // 2
+        self._general = D_has_hdim or not rmsnorm or self.d_mlp > 0
 
     # ------------------------------------------------------------------
     def forward(self, u, seqlen=None, seq_idx=None, cu_seqlens=None, inference_params=None):
@@ -97,7 +102,10 @@ class Mamba2(nn.Module):
         zxbcdt = linear(u, self.in_proj)
         if seq_idx is None and cu_seqlens is not None:
             seq_idx = seq_idx_from_cu_seqlens(cu_seqlens, l, u.device).expand(b, l)
-        if self.cp_group is not None and conv_state is None:
+        if self._general:
+            assert self.cp_group is None, "context parallelism runs the default Mamba2 configuration only"
+            y = self._forward_general(zxbcdt, seq_idx, conv_state, ssm_state)
+        elif self.cp_group is not None and conv_state is None:
             assert seq_idx is None, "packed sequences (seq_idx) are not supported with context parallelism"
             from ..parallel.context_parallel import mamba2_inner_parallel
             y = mamba2_inner_parallel(zxbcdt, self.conv1d.weight, self.conv1d.bias, self.dt_bias, self.A_log,
@@ -111,6 +119,47 @@ class Mamba2(nn.Module):
         else:
             y = self._prefill(zxbcdt, conv_state, ssm_state)
         return linear(y, self.out_proj)
+
+    def _forward_general(self, zxbcdt, seq_idx=None, conv_state=None, ssm_state=None):
+        """Unfused forward for rmsnorm=False / D_has_hdim / d_mlp > 0 (upstream Mamba2.forward's
+        non-fused branch): conv1d+SiLU -> SSD -> skip / gate / norm -> [silu(z0) x0, y].  With
+        ``conv_state`` / ``ssm_state`` (prefill) the decode cache is filled too."""
+        from ..ops.conv1d import causal_conv1d_fn
+        from ..ops.ssd import mamba_chunk_scan_combined
+        b, l, _ = zxbcdt.shape
+        di, gn, H, P = self.d_ssm, self.ngroups * self.d_state, self.nheads, self.headdim
+        z0, x0, z, xBC, dt = torch.split(zxbcdt, [self.d_mlp, self.d_mlp, di, di + 2 * gn, H], dim=-1)
+        if zxbcdt.stride(-2) % 8:  # e.g. an odd in_proj width (d_mlp > 0): the native ops want aligned rows
+            z, xBC, dt = z.contiguous(), xBC.contiguous(), dt.contiguous()
+        xt = xBC.transpose(1, 2)
+        if conv_state is not None:
+            sl = conv_state.shape[-1]  # upstream layout: the last d_conv inputs
+            conv_state.copy_(F.pad(xt, (max(0, sl - xt.shape[-1]), 0))[..., -sl:])
+        xBC = causal_conv1d_fn(xt, self.conv1d.weight, self.conv1d.bias, "silu", seq_idx=seq_idx).transpose(1, 2)
+        x, B, C = torch.split(xBC, [di, gn, gn], dim=-1)
+        xh = x.unflatten(-1, (H, P))
+        res = mamba_chunk_scan_combined(
+            xh, dt, -torch.exp(self.A_log.float()), B.unflatten(-1, (self.ngroups, self.d_state)),
+            C.unflatten(-1, (self.ngroups, self.d_state)), min(64, self.chunk_size),
+            D=None if self.D_has_hdim else self.D, dt_bias=self.dt_bias, dt_softplus=True,
+            dt_limit=self.dt_limit, seq_idx=seq_idx, return_final_states=ssm_state is not None)
+        y, last = res if ssm_state is not None else (res, None)
+        if last is not None:
+            ssm_state.copy_(last)
+        y = self._skip_gate_norm(y, xh, z)
+        if self.d_mlp > 0:
+            y = torch.cat([F.silu(z0) * x0, y], dim=-1)
+        return y
+
+    def _skip_gate_norm(self, y, xh, z):
+        """y (.., H, P) from the scan -> (.., d_ssm): + x D (per channel), then the gate: silu(z) without
+        the norm (rmsnorm=False, upstream's z inside the scan) or the gated RMSNorm."""
+        if self.D_has_hdim:
+            y = y + xh * self.D.view(self.nheads, self.headdim).to(y.dtype)
+        y = y.flatten(-2)
+        if not self.rmsnorm:
+            return y * F.silu(z)
+        return self.norm(y, z)
 
     def _prefill(self, zxbcdt, conv_state, ssm_state):
         """Prompt pass that also fills the decode cache (conv window + final SSM state): the same fused
@@ -131,15 +180,21 @@ class Mamba2(nn.Module):
         dtype = hidden_states.dtype
         zxbcdt = self.in_proj(hidden_states.squeeze(1))
         di, gn, H = self.d_ssm, self.ngroups * self.d_state, self.nheads
-        z, xBC, dt = torch.split(zxbcdt, [di, di + 2 * gn, H], dim=-1)
+        z0, x0, z, xBC, dt = torch.split(zxbcdt, [self.d_mlp, self.d_mlp, di, di + 2 * gn, H], dim=-1)
+        if zxbcdt.stride(-2) % 8:
+            z, xBC, dt = z.contiguous(), xBC.contiguous(), dt.contiguous()
         xBC = causal_conv1d_update(xBC, conv_state, self.conv1d.weight, self.conv1d.bias, "silu")
         x, B, C = torch.split(xBC, [di, gn, gn], dim=-1)
         A = -torch.exp(self.A_log.float())
-        y = selective_state_update(ssm_state, x.unflatten(-1, (H, self.headdim)), dt, A,
+        xh = x.unflatten(-1, (H, self.headdim))
+        y = selective_state_update(ssm_state, xh, dt, A,
                                    B.unflatten(-1, (self.ngroups, self.d_state)),
-                                   C.unflatten(-1, (self.ngroups, self.d_state)), self.D,
+                                   C.unflatten(-1, (self.ngroups, self.d_state)),
+                                   None if self.D_has_hdim else self.D,
                                    z=None, dt_bias=self.dt_bias, dt_softplus=True)
-        y = self.norm(y.flatten(-2), z)
+        y = self._skip_gate_norm(y, xh, z)
+        if self.d_mlp > 0:
+            y = torch.cat([F.silu(z0) * x0, y], dim=-1)
         out = self.out_proj(y)
         return out.unsqueeze(1).to(dtype), conv_state, ssm_state
 

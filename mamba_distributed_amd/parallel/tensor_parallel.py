@@ -197,6 +197,8 @@ class Mamba2TP(nn.Module):
 
     @classmethod
     def from_full(cls, full, process_group, sequence_parallel=False):
+        assert not getattr(full, "_general", False), \
+            "TP shards the default Mamba2 configuration (rmsnorm, per-head D, d_ssm == d_inner)"
         return cls(full, process_group, sequence_parallel)
 
     # ------------------------------------------------------------------------------------------
