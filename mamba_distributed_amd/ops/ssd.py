@@ -268,17 +268,60 @@ def mamba2_inner_fn(zxbcdt, conv_w, conv_b, dt_bias, A, D, norm_w, eps, headdim,
                             seq_idx, return_final_states, native_ssd=True)
 
 
+def _split_conv1d_scan_general(zxbcdt, conv1d_weight, conv1d_bias, dt_bias, A, D, chunk_size, initial_states,
+                               seq_idx, dt_limit, return_final_states, rmsnorm_weight, rmsnorm_eps, headdim,
+                               ngroups, d_state, norm_before_gate):
+    """conv1d+SiLU -> SSD -> (+ x D per channel) -> silu(z) gate or gated RMSNorm, from the native ops."""
+    from .conv1d import causal_conv1d_fn
+    from .norm import rmsnorm_gated_fn
+    b, l, _ = zxbcdt.shape
+    H = dt_bias.shape[0]
+    di, gn = H * headdim, ngroups * d_state
+    z, xBC, dt = torch.split(zxbcdt, [di, di + 2 * gn, H], dim=-1)
+    if zxbcdt.stride(-2) % 8:
+        z, xBC, dt = z.contiguous(), xBC.contiguous(), dt.contiguous()
+    xBC = causal_conv1d_fn(xBC.transpose(1, 2), conv1d_weight, conv1d_bias, "silu", seq_idx=seq_idx).transpose(1, 2)
+    x, B, C = torch.split(xBC, [di, gn, gn], dim=-1)
+    xh = x.unflatten(-1, (H, headdim))
+    res = mamba_chunk_scan_combined(xh, dt, A, B.unflatten(-1, (ngroups, d_state)),
+                                    C.unflatten(-1, (ngroups, d_state)), chunk_size,
+                                    D=D if D.dim() == 1 else None, dt_bias=dt_bias, dt_softplus=True,
+                                    dt_limit=dt_limit, seq_idx=seq_idx, initial_states=initial_states,
+                                    return_final_states=return_final_states)
+    y, final = res if return_final_states else (res, None)
+    if D.dim() == 2:
+        y = y + xh * D.to(y.dtype)
+    y = y.flatten(-2)
+    if rmsnorm_weight is None:
+        y = y * F.silu(z)
+    else:
+        y = rmsnorm_gated_fn(y, z, rmsnorm_weight, rmsnorm_eps, di // ngroups, norm_before_gate)
+    return (y, final) if return_final_states else y
+
+
 def mamba_split_conv1d_scan_combined(zxbcdt, conv1d_weight, conv1d_bias, dt_bias, A, D, chunk_size,
                                      initial_states=None, seq_idx=None, dt_limit=(0.0, _INF),
                                      return_final_states=False, activation="silu",
                                      rmsnorm_weight=None, rmsnorm_eps=1e-6, outproj_weight=None,
                                      outproj_bias=None, headdim=None, ngroups=1, norm_before_gate=True):
-    """Upstream-compatible entry point (D11).  Requires rmsnorm_weight (the Mamba2 default).
-    ``initial_states`` (b, h, p, n), ``seq_idx`` (b, l) and ``return_final_states`` run through the
-    fused native chain (conv1d_cl_var / ssd_fwd with seq_idx and initial states)."""
-    assert activation in ("silu", "swish") and rmsnorm_weight is not None
+    """Upstream-compatible entry point (D11).  ``initial_states`` (b, h, p, n), ``seq_idx`` (b, l) and
+    ``return_final_states`` run through the fused native chain (conv1d_cl_var / ssd_fwd with seq_idx and
+    initial states).  Upstream's other forms -- no norm (``rmsnorm_weight=None``: y * silu(z)) and a
+    per-channel skip (``D`` of shape (h, p)) -- run the same native ops unfused."""
+    assert activation in ("silu", "swish")
+    if D.dim() == 2:
+        headdim = D.shape[1]
+    assert headdim is not None, "headdim is required with a per-head D"
     H = dt_bias.shape[0]
     d_state = (zxbcdt.shape[-1] - H - 2 * H * headdim) // (2 * ngroups)
+    if rmsnorm_weight is None or D.dim() == 2:
+        out = _split_conv1d_scan_general(zxbcdt, conv1d_weight, conv1d_bias, dt_bias, A, D, chunk_size,
+                                         initial_states, seq_idx, dt_limit, return_final_states, rmsnorm_weight,
+                                         rmsnorm_eps, headdim, ngroups, d_state, norm_before_gate)
+        y, final = out if return_final_states else (out, None)
+        if outproj_weight is not None:
+            y = F.linear(y, outproj_weight, outproj_bias)
+        return (y, final) if return_final_states else y
     out = mamba2_inner_fn(zxbcdt, conv1d_weight, conv1d_bias, dt_bias, A, D, rmsnorm_weight, rmsnorm_eps,
                           headdim, ngroups, d_state, dt_limit, norm_before_gate, chunk_size,
                           initial_states=initial_states, seq_idx=seq_idx,

@@ -114,3 +114,24 @@ def test_variant_native_gpu(kw):
             params.seqlen_offset += 1
     got = torch.cat(out, 1).double().cpu()
     assert ((got - ref).norm() / ref.norm()).item() < 3e-2
+
+
+@pytest.mark.parametrize("form", ["default", "no_norm", "hdim_D", "hdim_D_no_norm"])
+def test_split_conv1d_scan_combined_forms(form):
+    """Upstream's mamba_split_conv1d_scan_combined forms (D11): the functional entry point equals the
+    Mamba2 module with the matching options (whose forward is checked against the fp64 recurrence)."""
+    from mamba_distributed_amd.ops.ssd import mamba_split_conv1d_scan_combined
+    torch.manual_seed(3)
+    kw = dict(rmsnorm="no_norm" not in form, D_has_hdim="hdim" in form)
+    m = Mamba2(64, d_state=16, headdim=16, expand=2, chunk_size=64, layer_idx=0, **kw)
+    with torch.no_grad():
+        m.D.uniform_(0.5, 1.5)
+    u = torch.randn(2, 40, 64)
+    zxbcdt = F.linear(u, m.in_proj.weight)
+    D = m.D.view(m.nheads, m.headdim) if m.D_has_hdim else m.D
+    y = mamba_split_conv1d_scan_combined(
+        zxbcdt, m.conv1d.weight.squeeze(1), m.conv1d.bias, m.dt_bias, -torch.exp(m.A_log), D, 64,
+        rmsnorm_weight=m.norm.weight if m.rmsnorm else None, rmsnorm_eps=1e-5, outproj_weight=m.out_proj.weight,
+        headdim=m.headdim, ngroups=m.ngroups, norm_before_gate=False)
+    ref = _oracle(m, u)
+    assert ((y.double() - ref).norm() / ref.norm()).item() < 1e-4
