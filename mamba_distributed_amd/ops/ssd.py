@@ -104,12 +104,18 @@ def mamba_chunk_scan_combined(x, dt, A, B, C, chunk_size=256, D=None, z=None, dt
             y = y * F.silu(z.float())
         y = y.to(x.dtype)
         return (y, fin) if return_final_states else y
-    if x.dtype == torch.bfloat16 and _ext.use_native(x) and (D is None or D.dim() == 1):
-        out = _SSDFn.apply(x, dt, A, B, C, D, dt_bias, initial_states, dt_softplus,
+    if x.dtype == torch.bfloat16 and _ext.use_native(x):
+        hdim_D = D is not None and D.dim() == 2  # per-channel skip (h, p): added after the native scan
+        out = _SSDFn.apply(x, dt, A, B, C, None if hdim_D else D, dt_bias, initial_states, dt_softplus,
                            float(dt_limit[0]), float(dt_limit[1]), return_final_states, seq_idx)
-        if z is not None:  # upstream's gate y * silu(z) (elementwise, fp32 math, autograd through both)
+        if z is not None or hdim_D:  # upstream's (y + x D) * silu(z) (elementwise, fp32 math, autograd)
             y, fin = out if return_final_states else (out, None)
-            y = (y.float() * F.silu(z.float())).to(y.dtype)
+            yf = y.float()
+            if hdim_D:
+                yf = yf + x.float() * D.float()
+            if z is not None:
+                yf = yf * F.silu(z.float())
+            y = yf.to(y.dtype)
             return (y, fin) if return_final_states else y
         return out
     return ssd_chunked_ref(x, dt, A, B, C, chunk_size, D=D, z=z, dt_bias=dt_bias,

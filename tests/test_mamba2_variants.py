@@ -135,3 +135,22 @@ def test_split_conv1d_scan_combined_forms(form):
         headdim=m.headdim, ngroups=m.ngroups, norm_before_gate=False)
     ref = _oracle(m, u)
     assert ((y.double() - ref).norm() / ref.norm()).item() < 1e-4
+
+
+@pytest.mark.gpu
+def test_chunk_scan_hdim_D_and_z_native(cuda):
+    """mamba_chunk_scan_combined with D of shape (h, p) and z: native scan + elementwise skip/gate on the
+    GPU vs the fp32 chunked reference."""
+    from mamba_distributed_amd.ops import reference as R
+    from mamba_distributed_amd.ops.ssd import mamba_chunk_scan_combined
+    g = torch.Generator(device=cuda).manual_seed(4)
+    b, l, h, p, n = 2, 192, 4, 64, 64
+    rnd = lambda *s: torch.randn(*s, device=cuda, generator=g)  # noqa: E731
+    x, z = rnd(b, l, h, p).bfloat16(), rnd(b, l, h, p).bfloat16()
+    dt = (rnd(b, l, h) * 0.5 - 1).bfloat16()
+    A = -torch.rand(h, device=cuda, generator=g) * 4 - 0.5
+    B, C = rnd(b, l, 1, n).bfloat16(), rnd(b, l, 1, n).bfloat16()
+    D, dt_bias = rnd(h, p), rnd(h) * 0.1
+    y = mamba_chunk_scan_combined(x, dt, A, B, C, 64, D=D, z=z, dt_bias=dt_bias, dt_softplus=True)
+    ref = R.ssd_chunked_ref(x, dt, A, B, C, 64, D=D, z=z, dt_bias=dt_bias, dt_softplus=True)
+    assert ((y.float() - ref.float()).norm() / ref.float().norm()).item() < 2e-2
