@@ -30,6 +30,7 @@ from ..ops.norm import RMSNorm, rms_norm_fn
 from .layers import MHA, GatedMLP
 from .mamba1 import Mamba
 from .mamba2 import Mamba2
+from ..utils.generation import GenerationMixin
 
 
 @dataclass
@@ -181,7 +182,7 @@ class MixerModel(nn.Module):
 CausalLMOutput = namedtuple("CausalLMOutput", ["logits"])
 
 
-class MambaLMHeadModel(nn.Module):
+class MambaLMHeadModel(nn.Module, GenerationMixin):
     def __init__(self, config: MambaConfig, initializer_cfg=None, device=None, dtype=None):
         super().__init__()
         self.config = config
