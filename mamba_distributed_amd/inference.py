@@ -68,7 +68,9 @@ class _FusedMamba2Step:
         dev = next(model.parameters()).device
         if dev.type != "cuda" or not _ext.use_native(next(model.parameters())) or batch_size > 16:
             return False
-        if not (bb.fused_add_norm and bb.residual_in_fp32) or bb.embedding.weight.dtype != torch.bfloat16:
+        from .ops.norm import RMSNorm
+        if not (bb.fused_add_norm and bb.residual_in_fp32) or bb.embedding.weight.dtype != torch.bfloat16 \
+                or not isinstance(bb.norm_f, RMSNorm):
             return False
         d = bb.embedding.weight.shape[1]
         if d % 8 or batch_size * d * 2 > 65536:

@@ -64,11 +64,12 @@ class Block(nn.Module):
             self.mlp = mlp_cls(dim)
         else:
             self.mlp = None
-        if self.fused_add_norm:
-            assert isinstance(self.norm, RMSNorm), "fused add+norm is implemented for RMSNorm"
+        # the fused add+norm kernel is RMSNorm's; with LayerNorm (rms_norm=False) the same prenorm math runs
+        # unfused (upstream's layer_norm_fn with is_rms_norm=False)
+        self._fused_rms = fused_add_norm and isinstance(self.norm, RMSNorm)
 
     def _add_norm(self, norm, hidden_states, residual):
-        if self.fused_add_norm:
+        if self._fused_rms:
             return rms_norm_fn(hidden_states, norm.weight, None, residual=residual, prenorm=True,
                                residual_in_fp32=self.residual_in_fp32, eps=norm.eps)
         residual = (hidden_states + residual) if residual is not None else hidden_states
@@ -172,7 +173,7 @@ class MixerModel(nn.Module):
             else:
                 hidden_states, residual = layer(hidden_states, residual, inference_params=inference_params,
                                                 **mixer_kwargs)
-        if self.fused_add_norm:
+        if self.fused_add_norm and isinstance(self.norm_f, RMSNorm):
             return rms_norm_fn(hidden_states, self.norm_f.weight, None, residual=residual, prenorm=False,
                                residual_in_fp32=self.residual_in_fp32, eps=self.norm_f.eps)
         residual = (hidden_states + residual) if residual is not None else hidden_states

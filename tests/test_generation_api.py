@@ -68,3 +68,24 @@ def test_generate_graph_matches_eager_gpu():
     torch.manual_seed(5)
     s2 = m.generate(prompt, max_length=48, top_k=20, top_p=0.9, temperature=0.8, cg=True)
     assert torch.equal(s1, s2)
+
+
+@pytest.mark.parametrize("layer", ["Mamba2", "Mamba1"])
+def test_layernorm_config_with_fused_add_norm(layer):
+    """MambaConfig(rms_norm=False, fused_add_norm=True) (upstream: fused LayerNorm add) builds, trains and
+    decodes: same prenorm math as the unfused path; cached greedy decode equals the uncached loop."""
+    torch.manual_seed(0)
+    cfg = preset("mamba2-tiny" if layer == "Mamba2" else "mamba1-tiny", vocab_size=256, rms_norm=False)
+    assert cfg.fused_add_norm
+    m = MambaLMHeadModel(cfg)
+    assert isinstance(m.backbone.norm_f, torch.nn.LayerNorm)
+    x = torch.randint(0, 256, (2, 16))
+    m(x).logits.float().square().mean().backward()
+    assert all(p.grad is not None for p in m.parameters() if p.requires_grad)
+    m.eval()
+    out = m.generate(x[:, :6], max_length=12)
+    seq = x[:, :6]
+    with torch.no_grad():
+        for _ in range(6):
+            seq = torch.cat([seq, m(seq).logits[:, -1].argmax(-1, keepdim=True)], 1)
+    assert torch.equal(out, seq)
