@@ -10,6 +10,10 @@ Layers:
 """
 from .config import MambaConfig, preset
 from .lm import LMHeadModel
+# mamba-ssm's top-level names (``from mamba_ssm import Mamba, Mamba2, MambaLMHeadModel``)
+from .models.mamba1 import Mamba
+from .models.mamba2 import Mamba2
+from .models.mixer_seq import MambaLMHeadModel
 
 __version__ = "0.1.0"
-__all__ = ["MambaConfig", "preset", "LMHeadModel"]
+__all__ = ["MambaConfig", "preset", "LMHeadModel", "Mamba", "Mamba2", "MambaLMHeadModel"]
