@@ -35,7 +35,7 @@ def enable_tuned_gemms(path: Optional[str] = None, tune: bool = False, max_tunin
     Returns True if a table is active.  Env ``MAMBA_AMD_TUNED_GEMMS=0`` disables it."""
     if os.environ.get("MAMBA_AMD_TUNED_GEMMS", "1") == "0" or not torch.cuda.is_available():
         return False
-    path = path or DEFAULT_TABLE
+    path = path or os.environ.get("MAMBA_AMD_GEMM_TABLE") or DEFAULT_TABLE  # env: A/B of another table
     if not tune and (not os.path.exists(path) or _arch() != "gfx950"):
         return False
     # The table is keyed by GEMM signatures recorded at the default fp32 matmul precision.  With
