@@ -402,20 +402,6 @@ int pick_hg(int B, int nc, int H, int G) {
   return best;
 }
 
-// forward chunk-output kernel: up to 8 heads per workgroup (C.B^T amortised) while keeping >= 1024
-// workgroups (4 per CU at its ~57 KB of LDS... 2 resident + a second wave of them)
-int pick_hg_fwd(int B, int nc, int H, int G) {
-  const int hpg = H / G;
-  if (const char* e = std::getenv("MAMBA_AMD_SSD_HGF")) {
-    const int v = std::atoi(e);
-    if (v >= 1 && hpg % v == 0) return v;
-  }
-  int best = 1;
-  for (int d = 1; d <= 8 && d <= hpg; ++d)
-    if (hpg % d == 0 && (int64_t)B * nc * (H / d) >= 1024) best = d;
-  return best;
-}
-
 void ssd_common(mamba_amd::SSDArgs& a, const Tensor& x, const Tensor& dt, const Tensor& A, const Tensor& Bm,
                 const Tensor& Cm, int64_t chunk, bool softplus, double dt_min, double dt_max) {
   TORCH_CHECK(chunk == 64, "native SSD chunk must be 64");
@@ -435,8 +421,6 @@ void ssd_common(mamba_amd::SSDArgs& a, const Tensor& x, const Tensor& dt, const 
               Bm.stride(2) % 8 == 0 && Cm.stride(2) % 8 == 0, "B/C rows must be 16-B aligned");
   a.nc = (a.L + 63) / 64; a.Lp = a.nc * 64;
   a.HG = pick_hg(a.B, a.nc, a.H, a.G); a.nhg = a.H / a.HG;
-  a.HGf = pick_hg_fwd(a.B, a.nc, a.H, a.G); a.nhgf = a.H / a.HGf;
-  if (const char* e = std::getenv("MAMBA_AMD_SSD_ABLATE")) a.ablate = std::atoi(e);
   a.x = (const mamba_amd::bf16_t*)x.data_ptr(); a.sxb = x.stride(0); a.sxl = x.stride(1); a.sxh = x.stride(2);
   a.dt = dt.data_ptr(); a.dt_dtype = dcode(dt.scalar_type());
   a.sdtb = dt.stride(0); a.sdtl = dt.stride(1); a.sdth = dt.stride(2);
@@ -883,28 +867,51 @@ Tensor gp_mm(Tensor A, Tensor B, optional<Tensor> out, int64_t la, int64_t lb, i
   return C;
 }
 
-int64_t gp_splits(int64_t M, int64_t N, int64_t K) { return mamba_amd::gemm_pipe_splits((int)M, (int)N, (int)K); }
-void gp_set_ablate(int64_t bits) { mamba_amd::gemm_pipe_set_ablate((int)bits); }
-
-// A HIP stream whose kernels may only be dispatched to the CUs set in `mask` (32 CUs per word, the
-// runtime's logical CU order; hipExtStreamCreateWithCUMask).  Returned as the raw hipStream_t so Python
-// wraps it in torch.cuda.ExternalStream.  Used to partition the CUs between the compute-bound
-// weight-gradient / micro-batch streams and the memory-bound backward (utils/cu_mask.py).  The stream
-// lives for the process (never destroyed: torch may still hold events recorded on it at exit).
-int64_t cu_masked_stream(int64_t device, std::vector<int64_t> mask) {
-  TORCH_CHECK(!mask.empty() && mask.size() <= 64, "cu_masked_stream: 1..64 mask words");
-  std::vector<uint32_t> words(mask.size());
-  bool any = false;
-  for (size_t i = 0; i < mask.size(); ++i) {
-    words[i] = (uint32_t)(mask[i] & 0xffffffffLL);
-    any = any || words[i] != 0u;
+// Persistent MFMA GEMM (kernels/gemm_pipe.hip, gemm_pk_k): C = A . B^T, layouts as gp_mm, no K split.
+// mode 0: bf16 C (optionally row-scaled by the fp32 `rowscale`), 1: fp32 C, 2: fp32 C +=.
+Tensor gp_pk(Tensor A, Tensor B, optional<Tensor> out, int64_t la, int64_t lb, int64_t mode,
+             optional<Tensor> rowscale) {
+  check_cuda(A, "A");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(A.device());
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2, "gp_pk: 2-D operands");
+  TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "gp_pk: bf16 operands");
+  TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1, "gp_pk: unit inner strides");
+  TORCH_CHECK((la == 0 || la == 1) && (lb == 0 || lb == 1) && !(la == 1 && lb == 0) && mode >= 0 && mode <= 2,
+              "gp_pk: args");
+  const int64_t M = la == 0 ? A.size(0) : A.size(1), K = la == 0 ? A.size(1) : A.size(0);
+  const int64_t N = lb == 0 ? B.size(0) : B.size(1), KB = lb == 0 ? B.size(1) : B.size(0);
+  TORCH_CHECK(K == KB, "gp_pk: contraction sizes differ (", K, " vs ", KB, ")");
+  TORCH_CHECK(M < (1ll << 31) && N < (1ll << 31) && K < (1ll << 31), "gp_pk: sizes");
+  TORCH_CHECK((uintptr_t)A.data_ptr() % 16 == 0 && (uintptr_t)B.data_ptr() % 16 == 0, "gp_pk: 16-B aligned operands");
+  const auto dt = mode == 0 ? at::kBFloat16 : at::kFloat;
+  Tensor C;
+  if (out.has_value() && out->defined()) {
+    C = *out;
+  } else {
+    TORCH_CHECK(mode != 2, "gp_pk: mode 2 accumulates into out");
+    C = at::empty({M, N}, A.options().dtype(dt));
   }
-  TORCH_CHECK(any, "cu_masked_stream: empty CU mask");
-  at::hip::HIPGuardMasqueradingAsCUDA guard(at::Device(at::kCUDA, (c10::DeviceIndex)device));
-  hipStream_t s = nullptr;
-  HIPCHK(hipExtStreamCreateWithCUMask(&s, (uint32_t)words.size(), words.data()));
-  return reinterpret_cast<int64_t>(s);
+  TORCH_CHECK(C.dim() == 2 && C.scalar_type() == dt && C.stride(1) == 1 && C.size(0) == M && C.size(1) == N,
+              "gp_pk: out shape/dtype");
+  TORCH_CHECK((uintptr_t)C.data_ptr() % 16 == 0, "gp_pk: 16-B aligned out");
+  const float* rs = nullptr;
+  if (rowscale.has_value() && rowscale->defined()) {
+    TORCH_CHECK(mode == 0 && rowscale->scalar_type() == at::kFloat && rowscale->is_contiguous() &&
+                rowscale->numel() == M, "gp_pk: rowscale is a contiguous fp32 (M,) vector, bf16 output only");
+    rs = rowscale->data_ptr<float>();
+  }
+  const int64_t lda = A.size(0) == 1 ? A.size(1) : A.stride(0), ldb = B.size(0) == 1 ? B.size(1) : B.stride(0);
+  const int64_t ldc = C.size(0) == 1 ? C.size(1) : C.stride(0);
+  TORCH_CHECK(mamba_amd::gemm_pk_supported((int)la, (int)lb, (int)mode, (int)M, (int)N, (int)K, lda, ldb, ldc),
+              "gp_pk: unsupported shape/strides (M=", M, " N=", N, " K=", K, " lda=", lda, " ldb=", ldb, " ldc=", ldc,
+              "; needs strides and N % 8, KC K % 8, XC A M % 8, operands < 4 GB)");
+  HIPCHK(mamba_amd::launch_gemm_pk((int)la, (int)lb, A.data_ptr(), lda, B.data_ptr(), ldb, C.data_ptr(), ldc, (int)M,
+                                   (int)N, (int)K, (int)mode, rs, cur_stream()));
+  return C;
 }
+
+int64_t gp_splits(int64_t M, int64_t N, int64_t K) { return mamba_amd::gemm_pipe_splits((int)M, (int)N, (int)K); }
+
 
 // out (+)= sum over the leading dim of part (S, ...) in fixed order; out fp32 contiguous, numel(out) = numel(part[0])
 void gp_reduce(Tensor part, Tensor out, bool accumulate) {
@@ -1038,10 +1045,9 @@ TORCH_LIBRARY(mamba_amd, m) {
   m.def("gemm_wgrad_cm(Tensor dY, Tensor X, Tensor(a!)? out=None, bool accumulate=False, bool dy_cm=True, "
         "bool x_cm=False) -> Tensor");
   m.def("gp_mm(Tensor A, Tensor B, Tensor(a!)? out=None, int la=0, int lb=0, int mode=0, int splits=1, int bm=256) -> Tensor");
+  m.def("gp_pk(Tensor A, Tensor B, Tensor(a!)? out=None, int la=0, int lb=0, int mode=0, Tensor? rowscale=None) -> Tensor");
   m.def("gp_splits(int M, int N, int K) -> int", &gp_splits);
   m.def("part_rows(str kind, int a, int b=0) -> int", &part_rows);
-  m.def("gp_set_ablate(int bits) -> ()", &gp_set_ablate);
-  m.def("cu_masked_stream(int device, int[] mask) -> int", &cu_masked_stream);
   m.def("gp_reduce(Tensor part, Tensor(a!) out, bool accumulate=False) -> ()");
   m.def("gemm_skinny(Tensor A, Tensor B, Tensor(a!)? out=None, bool accumulate=False) -> Tensor");
   m.def("ssm_state_update(Tensor(a!) state, Tensor x, Tensor dt, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? z, "
@@ -1060,6 +1066,7 @@ TORCH_LIBRARY_IMPL(mamba_amd, CUDA, m) {
   m.impl("gemm_skinny", &gemm_skinny);
   m.impl("gemm_wgrad_cm", &gemm_wgrad_cm);
   m.impl("gp_mm", &gp_mm);
+  m.impl("gp_pk", &gp_pk);
   m.impl("gp_reduce", &gp_reduce);
   m.impl("add_rmsnorm_bwd", &add_rmsnorm_bwd);
   m.impl("gated_rmsnorm_fwd", &gated_rmsnorm_fwd);

@@ -106,7 +106,6 @@ struct GemmPipeArgs {
   const bf16_t* B; int64_t ldb;
   void* C; int64_t ldc; int64_t split_stride;  // elements between the fp32 slabs of consecutive K splits
   int M, N, K, kslice, splits;
-  int ablate;  // diagnostics: bit 0 no vmcnt wait, 1 no DMA, 2 no barrier, 3 no epilogue (results garbage)
 };
 
 // LA / LB: operand layouts (0 = KC, 1 = XC); MI: 16-row tiles per wave along M (BM = 32 MI); EPI: 0 = bf16
@@ -120,16 +119,11 @@ struct GemmPipeArgs {
 // four LDS-DMAs or an MFMA waiting on a fragment read issued fewer than 16 MFMAs earlier.
 // (A persistent variant that streams the next output tile's K-tiles behind this one's was measured slower:
 // the dynamic buffer parity and tile bookkeeping cost more in the K-loop than the hidden epilogue gained.)
-template <int LA, int LB, int MI, int EPI, int ABL = 0, int WN = 4, int NJ_ = 0>
-__global__ __launch_bounds__(128 * WN) void gemm_pipe_k(GemmPipeArgs a) {
-  // WN = 4: 8 waves as 2 x 4, each (BM/2) x 64; WN = 2: 4 waves as 2 x 2, each (BM/2) x 128 (one wave per
-  // SIMD, accumulators in AGPRs, 1/3 fewer fragment bytes per MFMA).
-  // NJ_ = 3 (KC.KC only): BN = 192, each wave (BM/2) x 48 -- for N = 768 outputs (the d_model side of the
-  // 280M projections) 4 column tiles instead of 3, so M = 32768 makes 512 tiles = exactly 2 rounds of
-  // 256 CUs, where 256-wide tiles make 384 = 1.5 rounds (the second half-empty)
-  static_assert(NJ_ == 0 || (NJ_ == 3 && LB == 0 && WN == 4), "BN = 192 is a KC-operand, 8-wave tile");
-  constexpr int NT = 128 * WN;
-  constexpr int NJ = NJ_ ? NJ_ : 16 / WN;     // 16-col tiles per wave (BN = 256, or 192)
+template <int LA, int LB, int EPI>
+__global__ __launch_bounds__(512) void gemm_pipe_k(GemmPipeArgs a) {
+  // 8 waves as 2 x 4, each 128 x 64 of the 256 x 256 tile
+  constexpr int MI = 8, WN = 4, NT = 512;
+  constexpr int NJ = 4;  // 16-col tiles per wave
   constexpr int BM = 32 * MI, BN = 16 * NJ * WN;
   constexpr int SA = BM * 128, SB = BN * 128;  // bytes per K-tile image
   constexpr int SS = SA + SB;
@@ -151,7 +145,6 @@ __global__ __launch_bounds__(128 * WN) void gemm_pipe_k(GemmPipeArgs a) {
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int wr = w / WN, wc = w % WN;
   const int am0 = wr * (BM / 2), bn0 = wc * (BN / WN);
-  constexpr int abl = ABL;  // diagnostics only (0 in every real launch)
 
   // per-thread DMA sources as 32-bit BYTE offsets from the operand base at k = kbeg (host-checked to fit):
   // global_load_lds then takes the saddr + voffset form with no per-DMA 64-bit pointer registers
@@ -184,7 +177,6 @@ __global__ __launch_bounds__(128 * WN) void gemm_pipe_k(GemmPipeArgs a) {
   const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // DMA of K-tile kt into buf; part 0: A's DMAs, 1: B's, 2: both
   auto dma = [&](int kt_, char* buf, bool checked, int part) {
-    if constexpr ((abl & 2) != 0) return;
     const int kt = __builtin_amdgcn_readfirstlane(kt_);  // opaque to LLVM's strength reduction
     const int k0 = kbeg + kt * GP_BK;
     const char* bA = baseA + kt * stepA * 2;
@@ -275,8 +267,8 @@ __global__ __launch_bounds__(128 * WN) void gemm_pipe_k(GemmPipeArgs a) {
     pin<MH, MH * NJ>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave is done reading `cur`
     if (steady || kt + 1 < KT) {
-      if constexpr (!(abl & 1)) vm_wait<0>();                       // tile kt+1 has landed in `nxt`
-      if constexpr (!(abl & 4)) __builtin_amdgcn_s_barrier();       // ... for every wave; every wave is done reading `cur`
+      vm_wait<0>();                    // tile kt+1 has landed in `nxt`
+      __builtin_amdgcn_s_barrier();    // ... for every wave; every wave is done reading `cur`
       __builtin_amdgcn_sched_barrier(0);
       if (steady) dma(kt + 2, cur, false, 0);
       else if (kt + 2 < KT) dma(kt + 2, cur, kt + 2 >= KTF, 0);
@@ -305,7 +297,6 @@ __global__ __launch_bounds__(128 * WN) void gemm_pipe_k(GemmPipeArgs a) {
   }
 
   // epilogue: lane holds C[m][n .. n+3], m = m0 + am0 + 16 i + (l & 15), n = n0 + bn0 + 16 j + 4 (l >> 4)
-  if constexpr ((abl & 8) != 0) return;
   const int mr = l & 15, nc = 4 * (l >> 4);
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
@@ -332,6 +323,263 @@ __global__ __launch_bounds__(128 * WN) void gemm_pipe_k(GemmPipeArgs a) {
   }
 }
 
+// ---- persistent engine --------------------------------------------------------------------------------------
+// The same 256 x 256 K-loop as gemm_pipe_k, but ONE workgroup per CU walks a static list of output tiles, and
+// the K-tile stream runs across tile boundaries: the last two K-tiles of tile i DMA tile i+1's first two
+// K-tiles into the LDS buffers they free, so the next tile's operands land while tile i's epilogue drains.
+// The epilogue's stores are issued AFTER those DMAs and the first wait of the next tile counts past them
+// (vmcnt(NST)): the stores stay in flight under the next tile's first K-tile (vmcnt counts stores too).
+// The ablation of gemm_pipe_k (profiles/r2_v2_gemm_pipe_ablations.log: 252.6 us with the epilogue, 101.6
+// without, at the in_proj forward shape) puts ~60 % of the non-persistent kernel's time in the store tail.
+//
+// The loop body is branch-free (hipcc stops accumulating MFMAs in place across scalar branches and spills):
+// every wave issues exactly NST epilogue stores (lanes outside C write a sink), and after the last tile the
+// "next tile" DMAs re-read the current tile into the free buffers, drained before exit.
+//
+// Operands are DMA'd with buffer_load ... lds through a descriptor that covers exactly the operand's bytes,
+// so rows past M / N and k-rows past K read as zeros (no clamping, no zero page); KC k-chunks past K (the
+// next row's bytes, in range) get an out-of-range offset.
+//
+// bf16 epilogue (EPI 0): each wave stages its 16 x 64 accumulator rows through a private 2 KB LDS slot
+// (XOR-swizzled, conflict-free both ways) so that every global store writes 8 WHOLE 128-B row segments
+// (16 B per lane), instead of 16 rows x 32 B from the accumulator layout.  RS: rows scaled by an fp32
+// `rowscale` vector before rounding (a norm's rstd folded out of the A operand).
+struct GemmPkArgs {
+  const bf16_t* A; int64_t lda;
+  const bf16_t* B; int64_t ldb;
+  void* C; int64_t ldc;
+  const float* rowscale;        // RS: C[m, :] *= rowscale[m]
+  unsigned nbA, nbB;            // operand bytes covered by the buffer descriptors
+  int M, N, K, tn, ntiles, kte; // kte: K-tiles per output tile, rounded up to even (>= 4)
+};
+
+__device__ __attribute__((aligned(64))) uint4 g_pk_sink[64];  // epilogue stores of lanes outside C
+
+template <int LA, int LB, int EPI, bool RS = false, bool TAIL = false>
+__global__ __launch_bounds__(512) void gemm_pk_k(GemmPkArgs a) {
+  constexpr int NT = 512, MI = 8, NJ = 4, WN = 4, MH = 4;
+  constexpr int BM = 256, BN = 256;
+  constexpr int SA = BM * 128, SB = BN * 128, SS = SA + SB;
+  constexpr int GA = 4, GB = 4, G = GA + GB;
+  constexpr int STG = EPI == 0 ? 8 * 2048 : 0;
+  constexpr int NST = EPI == 0 ? 2 * MI : MI * NJ;  // epilogue store instructions per wave
+  __shared__ __attribute__((aligned(1024))) char smem[2 * SS + STG];
+
+  const int nwg = gridDim.x;
+  int tile = xcd_remap(blockIdx.x, nwg);
+  if (tile >= a.ntiles) return;
+  const int w = threadIdx.x >> 6, tid = threadIdx.x;
+  const int wr = w / WN, wc = w % WN;
+  const int am0 = wr * (BM / 2), bn0 = wc * (BN / WN);
+  const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, (short)0, (int)a.nbA, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)a.B, (short)0, (int)a.nbB, 0x00020000);
+
+  // Lane part of the DMA byte offsets, one VGPR per operand: DMA instruction ii of a KC operand moves rows
+  // 64 ii + (tid >> 3) at chunk (tid & 7) ^ ((tid >> 3) & 7) (64 ii does not change r & 7); of an XC operand,
+  // k-rows 32 (ii & 1) + (tid >> 4) of column half ii >> 1 (32 (ii & 1) changes neither xc_swz bit).  The
+  // rest is wave-uniform.
+  auto lane_off = [&](int L, int64_t ld) -> unsigned {
+    if (L == 0) {
+      const int r = tid >> 3, c = (tid & 7) ^ (r & 7);
+      return (unsigned)(((int64_t)r * ld + 8 * c) * 2);
+    }
+    const int r = tid >> 4, c = 8 * ((tid & 15) ^ (2 * xc_swz(r)));
+    return (unsigned)(((int64_t)r * ld + c) * 2);
+  };
+  const unsigned loA = lane_off(LA, a.lda), loB = lane_off(LB, a.ldb);
+  const int kchunk = 8 * ((tid & 7) ^ ((tid >> 3) & 7));  // KC: the lane's k within a K-tile
+  auto ii_off = [&](int L, int ii, int64_t ld) -> unsigned {  // uniform part of DMA instruction ii
+    return L == 0 ? (unsigned)(64 * ii * ld * 2) : (unsigned)((ii & 1) * 32 * ld * 2 + (ii >> 1) * 256);
+  };
+  const unsigned stepA = LA == 0 ? 128u : (unsigned)(64 * a.lda * 2);
+  const unsigned stepB = LB == 0 ? 128u : (unsigned)(64 * a.ldb * 2);
+  auto tbase = [&](int t, bool isA) -> unsigned {  // tile part of an operand's byte offset
+    const int b = isA ? (t / a.tn) * BM : (t % a.tn) * BN;
+    const int L = isA ? LA : LB;
+    const int64_t ld = isA ? a.lda : a.ldb;
+    return (unsigned)(L == 0 ? (int64_t)b * ld * 2 : (int64_t)b * 2);
+  };
+  // DMA K-tile kt of tile t into buf; part 0: A, 1: B, 2: both
+  auto dma = [&](int t, int kt_, char* buf, int part) {
+    const int kt = __builtin_amdgcn_readfirstlane(kt_);
+    const unsigned ba = __builtin_amdgcn_readfirstlane(tbase(t, true) + (unsigned)kt * stepA);
+    const unsigned bb = __builtin_amdgcn_readfirstlane(tbase(t, false) + (unsigned)kt * stepB);
+    const bool dead = TAIL && kt * 64 + kchunk >= a.K;  // KC k-chunk past K (in range: the next row's bytes) -> zeros
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      const bool isA = i < GA;
+      if ((part == 0 && !isA) || (part == 1 && isA)) continue;
+      const int ii = isA ? i : i - GA;
+      const int L = isA ? LA : LB;
+      unsigned v = (isA ? loA : loB) + (isA ? ba : bb) + ii_off(L, ii, isA ? a.lda : a.ldb);
+      if (L == 0 && dead) v = 0xFFFFFFF0u;
+      lds_void* dst = (lds_void*)(buf + (isA ? 0 : SA) + (ii * NT + wu * 64) * 16);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rA : rB, dst, 16, v, 0, 0, 0);
+    }
+  };
+
+  f32x4 acc[MI][NJ];
+  bf16x8 alo[MH], ahi[MH], b0[NJ], b1[NJ];
+  constexpr int NOA = LA == 0 ? 2 : MI, NOB = LB == 0 ? 2 : NJ;
+  int oa[NOA], ob[NOB];
+#pragma unroll
+  for (int i = 0; i < NOA; ++i) oa[i] = LA == 0 ? lane_kc(i) : lane_xc(am0 + 16 * i);
+#pragma unroll
+  for (int j = 0; j < NOB; ++j) ob[j] = LB == 0 ? lane_kc(j) : lane_xc(bn0 + 16 * j);
+  auto fa = [&](const char* img, int i, int ks) -> bf16x8 {
+    const int r0 = am0 + 16 * i;
+    if constexpr (LA == 0) return ld_kc(img, oa[ks], r0);
+    else return ld_xc(img, oa[i], r0, ks);
+  };
+  auto fb = [&](const char* img, int j, int ks) -> bf16x8 {
+    const int c0 = bn0 + 16 * j;
+    if constexpr (LB == 0) return ld_kc(img + SA, ob[ks], c0);
+    else return ld_xc(img + SA, ob[j], c0, ks);
+  };
+  auto rd_lo = [&](const char* img, int ks, bf16x8 (&bf)[NJ]) {
+#pragma unroll
+    for (int i = 0; i < MH; ++i) alo[i] = fa(img, i, ks);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) bf[j] = fb(img, j, ks);
+  };
+  auto rd_hi = [&](const char* img, int ks) {
+#pragma unroll
+    for (int i = 0; i < MH; ++i) ahi[i] = fa(img, MH + i, ks);
+  };
+  // zc: first MFMA of every accumulator in this K-tile (k-step 0) starts from zero
+  auto mm_lo = [&](bf16x8 (&bf)[NJ], bool zc) {
+#pragma unroll
+    for (int i = 0; i < MH; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = mfma16(bf[j], alo[i], zc ? zero4() : acc[i][j]);
+  };
+  auto mm_hi = [&](bf16x8 (&bf)[NJ], bool zc) {
+#pragma unroll
+    for (int i = 0; i < MH; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[MH + i][j] = mfma16(bf[j], ahi[i], zc ? zero4() : acc[MH + i][j]);
+  };
+
+  char* const buf0 = smem;
+  char* const buf1 = smem + SS;
+  const int KTE = a.kte;
+  // One K-tile from `cur` (`nx` holds the next K-tile, landing or landed).  bdma: the B-half DMA (bt, bk) at
+  // k-step 0; the barrier's wait leaves `wst` younger VMEM ops (the previous tile's epilogue stores) in flight;
+  // then the DMA (at, ak) into `cur`, both halves when `aboth`.  Every call site passes constant selectors.
+  auto ktile = [&](char* cur, char* nx, bool bdma, int bt, int bk, bool wst, int at, int ak, bool aboth, bool zc) {
+    rd_hi(cur, 0);
+    if (bdma) dma(bt, bk, nx, 1);
+    mm_lo(b0, zc);
+    pin<MH, MH * NJ, GB>();
+    rd_lo(cur, 1, b1);
+    mm_hi(b0, zc);
+    pin<MH + NJ, MH * NJ>();
+    rd_hi(cur, 1);
+    mm_lo(b1, false);
+    pin<MH, MH * NJ>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (wst) vm_wait<NST>();
+    else vm_wait<0>();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    dma(at, ak, cur, aboth ? 2 : 0);
+    rd_lo(nx, 0, b0);
+    mm_hi(b1, false);
+    pin<MH + NJ, MH * NJ, GA>();
+  };
+
+  // prologue: the first tile's K-tiles 0 and 1, then its K-tile 0
+  dma(tile, 0, buf0, 2);
+  dma(tile, 1, buf1, 2);
+  vm_wait<G>();
+  __builtin_amdgcn_s_barrier();
+  rd_lo(buf0, 0, b0);
+  ktile(buf0, buf1, false, 0, 0, false, tile, 2, false, true);
+
+  for (;;) {
+    int nt = tile + nwg;
+    const bool more = nt < a.ntiles;
+    const int ntc = more ? nt : tile;  // past the last tile: harmless re-reads of this one, drained at exit
+    // K-tile 1 and the steady K-tiles
+    ktile(buf1, buf0, true, tile, 2, false, tile, 3, false, false);
+#pragma unroll 1
+    for (int kt = 2; kt < KTE - 2; kt += 2) {
+      ktile(buf0, buf1, true, tile, kt + 1, false, tile, kt + 2, false, false);
+      ktile(buf1, buf0, true, tile, kt + 2, false, tile, kt + 3, false, false);
+    }
+    // the last two K-tiles stream the next tile's K-tiles 0 and 1 (both halves) into the buffers they free
+    ktile(buf0, buf1, true, tile, KTE - 1, false, ntc, 0, false, false);
+    ktile(buf1, buf0, true, ntc, 0, false, ntc, 1, true, false);
+
+    // ---- epilogue: lane holds C[m][n .. n+3], m = m0 + am0 + 16 i + (l & 15), n = n0 + bn0 + 16 j + 4 (l >> 4)
+    // Lane-derived addressing is recomputed here (lane id from mbcnt, wave id from an SGPR): hoisted out of the
+    // tile loop it would stay live across the K-loop, whose accumulator and fragment registers leave no room.
+    int el;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(el));
+    const int ew = wu;
+    const int eam0 = (ew / WN) * (BM / 2), ebn0 = (ew % WN) * (BN / WN);
+    const int m0 = (tile / a.tn) * BM, n0 = (tile % a.tn) * BN;
+    if constexpr (EPI == 0) {
+      char* stg = smem + 2 * SS + ew * 2048;
+      const int r = el & 15, q = el >> 4;
+      const int rr = el >> 3, cc = el & 7;
+      const int n = n0 + ebn0 + 8 * cc;
+      float rs[MI];
+      if constexpr (RS) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const int mm = m0 + eam0 + 16 * i + r;
+          rs[i] = a.rowscale[mm < a.M ? mm : a.M - 1];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int off = r * 128 + (((2 * j + (q >> 1)) ^ (r & 7)) << 4) + ((q & 1) << 3);
+          f32x4 v = acc[i][j];
+          if constexpr (RS) v = v * rs[i];
+          *reinterpret_cast<uint2*>(stg + off) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int row = rr + 8 * h;
+          const uint4 v = *reinterpret_cast<const uint4*>(stg + row * 128 + ((cc ^ (row & 7)) << 4));
+          const int m = m0 + eam0 + 16 * i + row;
+          uint4* dst = (m < a.M && n < a.N) ? reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(a.C) + (int64_t)m * a.ldc + n)
+                                            : &g_pk_sink[el];
+          *dst = v;
+        }
+      }
+    } else {
+      const int mr = el & 15, nc = 4 * (el >> 4);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int m = m0 + eam0 + 16 * i + mr;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int n = n0 + ebn0 + 16 * j + nc;
+          float4* c = (m < a.M && n < a.N) ? reinterpret_cast<float4*>(reinterpret_cast<float*>(a.C) + (int64_t)m * a.ldc + n)
+                                           : reinterpret_cast<float4*>(&g_pk_sink[el]);
+          float4 v = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+          if constexpr (EPI == 2) {
+            const float4 o = *c;
+            v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+          }
+          *c = v;
+        }
+      }
+    }
+    if (!more) break;
+    tile = nt;
+    // the next tile's K-tile 0 (its K-tile 1 landed before the stores above were issued)
+    ktile(buf0, buf1, false, 0, 0, true, tile, 2, false, true);
+  }
+  vm_wait<0>();  // no LDS-DMA may outlive the workgroup
+}
+
 // out[i] (+)= sum_s part[s][i] in fixed order (the K-split slabs of a weight gradient)
 __global__ void gp_reduce_k(const float* __restrict__ part, int S, int64_t stride, int64_t n, float* __restrict__ out,
                             bool accumulate) {
@@ -344,9 +592,6 @@ __global__ void gp_reduce_k(const float* __restrict__ part, int S, int64_t strid
   }
   *reinterpret_cast<float4*>(out + i) = s;
 }
-
-static int g_gp_ablate = 0;
-void gemm_pipe_set_ablate(int bits) { g_gp_ablate = bits; }
 
 bool gemm_pipe_supported(int la, int lb, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc) {
   if (M <= 0 || N <= 0 || K <= 0) return false;
@@ -374,54 +619,83 @@ hipError_t launch_gemm_pipe(int la, int lb, const void* A, int64_t lda, const vo
                             int64_t ldc, int M, int N, int K, int splits, int64_t split_stride, int epi, int bm,
                             hipStream_t st) {
   if (!gemm_pipe_supported(la, lb, M, N, K, lda, ldb, ldc)) return hipErrorInvalidValue;
-  if (splits < 1 || (splits > 1 && epi == 0)) return hipErrorInvalidValue;
+  if (splits < 1 || (splits > 1 && epi == 0) || bm != 256) return hipErrorInvalidValue;
   GemmPipeArgs a;
   a.A = (const bf16_t*)A; a.lda = lda; a.B = (const bf16_t*)B; a.ldb = ldb;
   a.C = C; a.ldc = ldc; a.split_stride = split_stride;
   a.M = M; a.N = N; a.K = K; a.splits = splits;
-  a.ablate = g_gp_ablate;
   a.kslice = ((K + splits - 1) / splits + GP_BK - 1) / GP_BK * GP_BK;
-  // tile code `bm`: 256 -> 256 x 256, 128 -> 128 x 256, 192 -> 256 x 192 (KC.KC), 1256 -> 256 x 256 on 4 waves
-  const int BM = bm == 128 ? 128 : 256;
-  const int BN = bm == 192 ? 192 : 256;
-  if (bm == 192 && !(la == 0 && lb == 0)) return hipErrorInvalidValue;
-  // 256 x 256 on 4 waves of 128 x 128 (one wave per SIMD, AGPR accumulators): measured 16-27 % slower than
-  // the 8-wave tile under hipcc's schedule (profiles/r2_v3_gemm_pipe_bench.log); kept for A/B
-  const bool w4 = bm == 1256;
-  const int ntiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN) * splits;
-  const int nwg = ntiles;
-#define GP_LAUNCH(LA_, LB_, MI_, EPI_)                                                                 \
-  if (w4 && LA_ == 0 && LB_ == 0)                                                                      \
-    hipLaunchKernelGGL((gemm_pipe_k<0, 0, MI_, EPI_, 0, 2>), dim3(nwg), dim3(256), 0, st, a);           \
-  else                                                                                                 \
-    hipLaunchKernelGGL((gemm_pipe_k<LA_, LB_, MI_, EPI_>), dim3(nwg), dim3(GP_NT), 0, st, a)
-#define GP_EPI(LA_, LB_, MI_)                 \
-  switch (epi) {                              \
-    case 0: GP_LAUNCH(LA_, LB_, MI_, 0); break; \
-    case 1: GP_LAUNCH(LA_, LB_, MI_, 1); break; \
-    default: GP_LAUNCH(LA_, LB_, MI_, 2); break; \
+  const int nwg = ((M + 255) / 256) * ((N + 255) / 256) * splits;
+#define GP_EPI(LA_, LB_)                                                                       \
+  switch (epi) {                                                                               \
+    case 0: hipLaunchKernelGGL((gemm_pipe_k<LA_, LB_, 0>), dim3(nwg), dim3(GP_NT), 0, st, a); break; \
+    case 1: hipLaunchKernelGGL((gemm_pipe_k<LA_, LB_, 1>), dim3(nwg), dim3(GP_NT), 0, st, a); break; \
+    default: hipLaunchKernelGGL((gemm_pipe_k<LA_, LB_, 2>), dim3(nwg), dim3(GP_NT), 0, st, a); break; \
   }
-  if (a.ablate && la == 0 && lb == 0 && BM == 256 && BN == 256 && epi == 0) {
-#define GP_ABL(B_) case B_: hipLaunchKernelGGL((gemm_pipe_k<0, 0, 8, 0, B_>), dim3(nwg), dim3(GP_NT), 0, st, a); break;
-    switch (a.ablate) { GP_ABL(1) GP_ABL(2) GP_ABL(4) GP_ABL(8) GP_ABL(5) GP_ABL(6) GP_ABL(14) default: break; }
-#undef GP_ABL
-  } else if (la == 0 && lb == 0 && BN == 192) {
-    switch (epi) {
-      case 0: hipLaunchKernelGGL((gemm_pipe_k<0, 0, 8, 0, 0, 4, 3>), dim3(nwg), dim3(GP_NT), 0, st, a); break;
-      case 1: hipLaunchKernelGGL((gemm_pipe_k<0, 0, 8, 1, 0, 4, 3>), dim3(nwg), dim3(GP_NT), 0, st, a); break;
-      default: hipLaunchKernelGGL((gemm_pipe_k<0, 0, 8, 2, 0, 4, 3>), dim3(nwg), dim3(GP_NT), 0, st, a); break;
-    }
-  } else if (la == 0 && lb == 0) {
-    if (BM == 256) { GP_EPI(0, 0, 8) } else { GP_EPI(0, 0, 4) }
-  } else if (la == 0 && lb == 1) {
-    if (BM == 256) { GP_EPI(0, 1, 8) } else { GP_EPI(0, 1, 4) }
-  } else if (la == 1 && lb == 1) {
-    GP_EPI(1, 1, 8)
-  } else {
-    return hipErrorInvalidValue;
-  }
+  if (la == 0 && lb == 0) { GP_EPI(0, 0) }
+  else if (la == 0 && lb == 1) { GP_EPI(0, 1) }
+  else if (la == 1 && lb == 1) { GP_EPI(1, 1) }
+  else return hipErrorInvalidValue;
 #undef GP_EPI
-#undef GP_LAUNCH
+  return hipGetLastError();
+}
+
+static int cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+bool gemm_pk_supported(int la, int lb, int epi, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc) {
+  if (M <= 0 || N <= 0 || K <= 192) return false;  // >= 4 K-tiles
+  if (la != 0 || lb != 0 || epi != 0) return false;  // instantiated: KC . KC, bf16 output
+  if (lda % 8 || ldb % 8 || ldc % 8 || N % 8) return false;
+  if ((la == 0 || lb == 0) && K % 8) return false;
+  if (la == 1 && M % 8) return false;
+  if (la == 0 && lda < K) return false;
+  if (lb == 0 && ldb < K) return false;
+  if (la == 1 && lda < M) return false;
+  if (lb == 1 && ldb < N) return false;
+  // every DMA byte offset, including the overhang of partial tiles, must stay below the out-of-range sentinel
+  const int64_t kt = ((K + 63) / 64 + 1) / 2 * 2;
+  const int64_t lim = ((int64_t)1 << 32) - 64;
+  const int64_t Mp = (M + 255) / 256 * 256, Np = (N + 255) / 256 * 256;
+  const int64_t exA = la == 0 ? (Mp * lda + kt * 64) * 2 : (kt * 64 * lda + Mp) * 2;
+  const int64_t exB = lb == 0 ? (Np * ldb + kt * 64) * 2 : (kt * 64 * ldb + Np) * 2;
+  return exA < lim && exB < lim;
+}
+
+hipError_t launch_gemm_pk(int la, int lb, const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
+                          int64_t ldc, int M, int N, int K, int epi, const float* rowscale, hipStream_t st) {
+  if (!gemm_pk_supported(la, lb, epi, M, N, K, lda, ldb, ldc)) return hipErrorInvalidValue;
+  GemmPkArgs a;
+  a.A = (const bf16_t*)A; a.lda = lda; a.B = (const bf16_t*)B; a.ldb = ldb;
+  a.C = C; a.ldc = ldc; a.rowscale = rowscale;
+  a.nbA = (unsigned)(la == 0 ? ((int64_t)(M - 1) * lda + K) * 2 : ((int64_t)(K - 1) * lda + M) * 2);
+  a.nbB = (unsigned)(lb == 0 ? ((int64_t)(N - 1) * ldb + K) * 2 : ((int64_t)(K - 1) * ldb + N) * 2);
+  a.M = M; a.N = N; a.K = K;
+  a.tn = (N + 255) / 256;
+  a.ntiles = ((M + 255) / 256) * a.tn;
+  a.kte = ((K + 63) / 64 + 1) / 2 * 2;
+  const int nwg = std::min(a.ntiles, cu_count());
+  // K-tail handling only where a KC operand has k-chunks past K inside its rows
+  const bool tail = K % 64 != 0 || a.kte * 64 != K;
+  // instantiated for the projection / lm_head forward and input-gradient products: KC . KC, bf16 output
+  // (input gradients read a per-step cached W^T); the K-split weight gradients stay on gemm_pipe_k
+#define PK_EPI(LA_, LB_)                                                                                     \
+  if (rowscale) {                                                                                           \
+    if (tail) hipLaunchKernelGGL((gemm_pk_k<LA_, LB_, 0, true, true>), dim3(nwg), dim3(512), 0, st, a);     \
+    else hipLaunchKernelGGL((gemm_pk_k<LA_, LB_, 0, true, false>), dim3(nwg), dim3(512), 0, st, a);         \
+  } else {                                                                                                  \
+    if (tail) hipLaunchKernelGGL((gemm_pk_k<LA_, LB_, 0, false, true>), dim3(nwg), dim3(512), 0, st, a);    \
+    else hipLaunchKernelGGL((gemm_pk_k<LA_, LB_, 0, false, false>), dim3(nwg), dim3(512), 0, st, a);        \
+  }
+  PK_EPI(0, 0)
+#undef PK_EPI
   return hipGetLastError();
 }
 

@@ -95,13 +95,17 @@ hipError_t launch_gemm_wgrad(const void* dY, int64_t ldy, const void* X, int64_t
 
 // ---- gemm_pipe.hip: pipelined 256x256 MFMA GEMM engine, C[M,N] (op)= A . B^T ----------------------------
 // la / lb: 0 = operand stored [rows][K] (K contiguous), 1 = stored [K][rows]; epi: 0 = bf16 C, 1 = fp32 C
-// (K split `splits` ways into slabs split_stride elements apart), 2 = fp32 C +=; bm: 256 or 128 tile rows
+// (K split `splits` ways into slabs split_stride elements apart), 2 = fp32 C +=; bm: 256 (the only tile)
 bool gemm_pipe_supported(int la, int lb, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc);
 int gemm_pipe_splits(int M, int N, int K);
-void gemm_pipe_set_ablate(int bits);  // diagnostics only (scripts/gemm_bench.py --ablate)
 hipError_t launch_gemm_pipe(int la, int lb, const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
                             int64_t ldc, int M, int N, int K, int splits, int64_t split_stride, int epi, int bm,
                             hipStream_t st);
+// persistent variant (one workgroup per CU walking the output tiles; KC . KC, bf16 output (epi 0) only,
+// staged through LDS into whole-row stores; rowscale (epi 0, nullable): C[m, :] *= rowscale[m])
+bool gemm_pk_supported(int la, int lb, int epi, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc);
+hipError_t launch_gemm_pk(int la, int lb, const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
+                          int64_t ldc, int M, int N, int K, int epi, const float* rowscale, hipStream_t st);
 // out[i] (+)= sum_s part[s * stride + i], fixed order
 hipError_t launch_gp_reduce(const float* part, int S, int64_t stride, int64_t n, float* out, bool accumulate,
                             hipStream_t st);

@@ -1365,27 +1365,23 @@ __global__ void selscan_reduce_bc_k(SelScanArgs a) {
     else return hipErrorInvalidValue;                                               \
   } while (0)
 
-static bool env_off(const char* name) {
-  const char* e = std::getenv(name);
-  return e && std::atoi(e) == 0;
-}
 // the wave-per-state-group kernels: bf16 rows, 64-channel workgroups inside one B/C group
 static bool sg_shape_ok(const SelScanArgs& a) {
   return a.dtype == kBF16 && a.vec && a.vecbc && (!a.z_ || a.vecz) && a.N == 16 && a.D % 64 == 0 &&
          (a.D / a.G) % 64 == 0;
 }
 // sequential-time forward walk when the batch has the channels to fill the GPU (>= 2048 wavefronts);
-// MAMBA_AMD_SELSCAN_LC=0 forces the time-parallel kernel (A/B, tests).
+// otherwise (small batches, L not a multiple of the walk's step tile) the time-parallel DPP-scan kernel.
 // Measured at B=32, D=1536, L=1024, N=16 on MI355X: 290 us vs 345 us.
 static bool use_fwd_sg(const SelScanArgs& a) {
   // L >= SG_T: the per-tile B / C row reads start at min(t0, L - SG_T)
-  return sg_shape_ok(a) && a.L % SF_IT == 0 && a.L >= SG_T && !env_off("MAMBA_AMD_SELSCAN_LC") &&
+  return sg_shape_ok(a) && a.L % SF_IT == 0 && a.L >= SG_T &&
          (int64_t)a.B * a.D / 16 >= 2048;
 }
-// sequential-time backward: needs the forward's 16-step carries; MAMBA_AMD_SELSCAN_BWD_SG=0 keeps the
-// time-parallel backward (and 512-step carries)
+// sequential-time backward: needs the forward's 16-step carries; the time-parallel backward (and 512-step
+// carries) otherwise
 int selscan_carry_t(const SelScanArgs& a) {
-  return (use_fwd_sg(a) && a.L % SGB_T == 0 && !env_off("MAMBA_AMD_SELSCAN_BWD_SG")) ? SGB_T : SB_T;
+  return (use_fwd_sg(a) && a.L % SGB_T == 0) ? SGB_T : SB_T;
 }
 static bool use_bwd_sg(const SelScanArgs& a) {
   // 32-bit in-kernel offsets: 64 rows of every (b, d, l) tensor, 64 carry rows

@@ -7,8 +7,6 @@ namespace mamba_amd {
 struct SSDArgs {
   int B, L, H, G, N, nc, Lp;  // Lp = nc * 64
   int HG, nhg;                // heads per workgroup in the chunk kernels, nhg = H / HG
-  int HGf, nhgf;              // heads per workgroup in the forward chunk (output) kernel
-  int ablate;                 // profiling only (MAMBA_AMD_SSD_ABLATE bits; results are wrong when set)
   // forward inputs
   const bf16_t* x; int64_t sxb, sxl, sxh;  // (b, l, h, p) unit p stride
   const void* dt; int dt_dtype; int64_t sdtb, sdtl, sdth;

@@ -754,292 +754,6 @@ __global__ __launch_bounds__(256) void ssd_dbc_bwd_k(SSDArgs a) {
   store_tile<Q, N>(a.dB + (int64_t)b * a.sdBb + (int64_t)c * Q * a.sdBl + (int64_t)g * a.sdBg, a.sdBl, Os, LDN, valid);
 }
 
-// load at a 32-bit BYTE offset from a workgroup-uniform base: selects the SGPR-base + VGPR-offset form
-// (one VGPR of address per load instead of a 64-bit pointer pair)
-template <typename T>
-__device__ __forceinline__ T ldg_off(const void* base, uint32_t byte_off) {
-  return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + byte_off);
-}
-
-// ============================== state walk (dstates for the backward; states for the forward) =====
-// cur <- e^{cl_c} cur + U_c^T V_c chunk by chunk, out[c] = cur before the update:
-//   fwd: U = x rows scaled by w_j = e^{cl-cum_j} dt_j, V = B, c = 0..nc-1, cur0 = init,   out = states
-//   bwd: U = dY rows scaled by e^{cum_i},             V = C, c = nc-1..0, cur0 = dfinal, out = dstates
-// Every state column is independent, so one workgroup owns a 64-column block of (b, h)'s state: the
-// walk is 2x (N=128) as parallel as a whole-state walk, each chunk step is 8 MFMAs per wave, and a
-// workgroup needs only 20 KB of LDS and few VGPRs, so ~6 workgroups share a CU and hide each other's
-// load latency (the walk is HBM-bound: U, V in, bf16 states out).  Wave w owns state columns
-// n0+16w.. as the ROWS of the transposed product S^T = V^T U, so a lane holds 4 consecutive n of one p:
-// the bf16 state goes to HBM as 8-B stores straight from the accumulators (no LDS staging).
-template <bool BWD, int WALK_D>
-__global__ __launch_bounds__(256) void ssd_walk_k(SSDArgs a) {
-  constexpr int LDW = 64 + 16;  // padded rows: conflict-free ds_read_b64_tr_b16 (see LD64)
-  __shared__ __attribute__((aligned(16))) bf16_t Us[Q * LDW];
-  __shared__ __attribute__((aligned(16))) bf16_t Vs[Q * LDW];
-  __shared__ __attribute__((aligned(16))) bf16_t Ss[P * LDW];  // out[c] staged as [p][n]: full-line stores
-  const int nblk = a.N / 64;
-  const int lid = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x));  // neighbours share an L2
-  const int nb = lid % nblk, h = (lid / nblk) % a.H, b = lid / (nblk * a.H);
-  const int g = h / (a.H / a.G);
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63, li = l & 15, lg = l >> 4;
-  const int n0 = 64 * nb;
-  const float* __restrict__ cumbh = a.cum + ((int64_t)b * a.H + h) * a.Lp;
-  const float* __restrict__ dtbh = a.dtp + ((int64_t)b * a.H + h) * a.Lp;
-  const bf16_t* __restrict__ ug = BWD ? a.dy + (int64_t)b * a.sdyb + (int64_t)h * a.sdyh : a.x + (int64_t)b * a.sxb + (int64_t)h * a.sxh;
-  const int64_t sul = BWD ? a.sdyl : a.sxl;
-  const bf16_t* __restrict__ vg = BWD ? a.Cm + (int64_t)b * a.sCb + (int64_t)g * a.sCg + n0 : a.Bm + (int64_t)b * a.sBb + (int64_t)g * a.sBg + n0;
-  const int64_t svl = BWD ? a.sCl : a.sBl;
-  // this thread's two 16-B pieces of each 64 x 64 tile: rows r0 and r0 + 32, columns c8..c8+7
-  const int r0 = threadIdx.x >> 3, c8 = (threadIdx.x & 7) * 8;
-  // WALK_D-deep register ring: a chunk step is only 8 MFMAs per wave, so with one chunk in flight the
-  // walk would wait a full HBM round trip per step; WALK_D chunks in flight hide it.
-  struct Stage {
-    uint4 u[2], v[2];
-    float cum[2], dt[2], cl;
-    int valid;
-  };
-  Stage ring[WALK_D];
-  auto prefetch = [&](Stage& sg, int c) {
-    sg.valid = min(Q, a.L - c * Q);
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      // clamped row: always a legal address, zeroed in stage().  32-bit offsets from the workgroup-
-      // uniform bases (the binding checks L * row stride < 2^31): SGPR base + VGPR offset addressing
-      // keeps the ring's address registers at one dword per load.
-      const uint32_t t = (uint32_t)(c * Q + min(r0 + 32 * k, sg.valid - 1));
-      sg.u[k] = ldg_off<uint4>(ug, (t * (uint32_t)sul + c8) * 2u);
-      sg.v[k] = ldg_off<uint4>(vg, (t * (uint32_t)svl + c8) * 2u);
-      sg.cum[k] = ldg_off<float>(cumbh, (uint32_t)(c * Q + r0 + 32 * k) * 4u);  // cum / dtp padded to Lp
-      sg.dt[k] = BWD ? 0.f : ldg_off<float>(dtbh, (uint32_t)(c * Q + r0 + 32 * k) * 4u);
-    }
-    sg.cl = ldg_off<float>(cumbh, (uint32_t)(c * Q + Q - 1) * 4u);
-  };
-  auto stage = [&](const Stage& sg) {
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int r = r0 + 32 * k;
-      const float sc = BWD ? __expf(sg.cum[k]) : __expf(sg.cl - sg.cum[k]) * sg.dt[k];
-      uint4 u = make_uint4(0, 0, 0, 0), v = make_uint4(0, 0, 0, 0);
-      if (r < sg.valid) {
-        float f[8];
-        ld8bf(reinterpret_cast<const bf16_t*>(&sg.u[k]), f);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] *= sc;
-        st8bf(reinterpret_cast<bf16_t*>(&u), f);
-        v = sg.v[k];
-      }
-      *reinterpret_cast<uint4*>(Us + r * LDW + c8) = u;
-      *reinterpret_cast<uint4*>(Vs + r * LDW + c8) = v;
-    }
-  };
-  f32x4 cur[4];  // S^T[n = n0 + 16w + 4lg + r][p = 16pt + li]
-  const int64_t sbase = (((int64_t)b * a.H + h) * P) * a.N + n0 + 16 * w + 4 * lg;
-  const float* src = BWD ? a.dfinal : a.init;
-#pragma unroll
-  for (int pt = 0; pt < 4; ++pt) {
-    cur[pt] = zero4();
-    if (src) {
-      const float4 v = *reinterpret_cast<const float4*>(src + sbase + (int64_t)(16 * pt + li) * a.N);
-      cur[pt] = f32x4{v.x, v.y, v.z, v.w};
-    }
-  }
-  bf16_t* outg = BWD ? a.dstates : a.states;
-  auto chunk_of = [&](int it) { return BWD ? a.nc - 1 - min(it, a.nc - 1) : min(it, a.nc - 1); };
-  // one chunk step; `refill` re-arms the ring slot (unconditionally: a clamped chunk index past the end
-  // loads valid, unused data) so every iteration of the main loop issues the same vector-memory ops and
-  // the compiler can count vmcnt instead of draining to 0
-  auto step = [&](Stage& sg, int it, bool refill) {
-    const int c = chunk_of(it);
-    __syncthreads();  // the previous chunk's MFMAs are done with Us / Vs, every wave has stored Ss
-    stage(sg);
-    // out[c] = cur -> LDS [p][n] (8-B writes), then whole 128-B rows to HBM: the accumulator layout
-    // would give 32-B row pieces per store instruction, which cost ~2x the HBM write time
-#pragma unroll
-    for (int pt = 0; pt < 4; ++pt)
-      *reinterpret_cast<uint2*>(Ss + (16 * pt + li) * LDW + 16 * w + 4 * lg) =
-          make_uint2(pack2(cur[pt][0], cur[pt][1]), pack2(cur[pt][2], cur[pt][3]));
-    const float decay = __expf(sg.cl);
-    __syncthreads();
-    // stores before the next loads (vmcnt completes in order; see ssd_fused_fwd_k)
-    if (!(a.ablate & 1)) {
-      bf16_t* og = outg + ((((int64_t)b * a.nc + c) * a.H + h) * P) * a.N + n0;
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int r = r0 + 32 * k;
-        *reinterpret_cast<uint4*>(og + (int64_t)r * a.N + c8) = *reinterpret_cast<const uint4*>(Ss + r * LDW + c8);
-      }
-    }
-    if (refill && !(a.ablate & 2)) {
-      // pinned: hoisted refills would hold a second copy of the ring slot in fresh (SSA) registers
-      __builtin_amdgcn_sched_barrier(0);
-      prefetch(sg, chunk_of(it + WALK_D));
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#pragma unroll
-    for (int pt = 0; pt < 4; ++pt) cur[pt] *= decay;
-    if (!(a.ablate & 4)) {
-#pragma unroll
-      for (int ks = 0; ks < Q / 32; ++ks) {
-        const bf16x8 A = frag_tr(Vs, LDW, 32 * ks, 16 * w);
-#pragma unroll
-        for (int pt = 0; pt < 4; ++pt) cur[pt] = mfma16(A, frag_tr(Us, LDW, 32 * ks, 16 * pt), cur[pt]);
-      }
-    }
-  };
-#pragma unroll
-  for (int k = 0; k < WALK_D; ++k) prefetch(ring[k], chunk_of(k));
-  int it0 = 0;
-  for (; it0 + WALK_D <= a.nc; it0 += WALK_D) {
-#pragma unroll
-    for (int k = 0; k < WALK_D; ++k) step(ring[k], it0 + k, true);
-  }
-#pragma unroll
-  for (int k = 0; k < WALK_D; ++k)
-    if (it0 + k < a.nc) step(ring[k], it0 + k, false);
-  float* dst = BWD ? a.dinit : a.final_state;
-  if (dst) {
-#pragma unroll
-    for (int pt = 0; pt < 4; ++pt)
-      *reinterpret_cast<float4*>(dst + sbase + (int64_t)(16 * pt + li) * a.N) =
-          make_float4(cur[pt][0], cur[pt][1], cur[pt][2], cur[pt][3]);
-  }
-}
-
-// ============================== forward chunk outputs (parallel over chunks) ==================
-// Y^T[p][i] = e^{cum_i} S_c[p] . C_i  +  sum_{j<=i} X^T[p][j] M^T[j][i]  +  D x_i[p],
-// M[i][j] = (C_i . B_j) e^{cum_i - cum_j} dt_j, with S_c the state entering chunk c (ssd_walk_k<false>).
-// Workgroup per (chunk, head group, b): C / B staged once, C.B^T tiles kept in VGPRs across the heads.
-// Per head: wave w owns output columns p in [16w, 16w+16) for all 64 steps, so
-//   * its S rows are MFMA A operands loaded straight from HBM (16-B loads, no LDS),
-//   * the y tile is staged in LDS [i][p] (8-B writes of 4 consecutive p from the accumulators) and
-//     leaves as whole 128-B rows while the next head loads,
-//   * M is computed once per head (wave w: rows i of tile w) into LDS [i][j] and read back as
-//     k-contiguous B fragments; its exp / mask inputs are prefetched with the head's other loads.
-template <int N>
-__global__ __launch_bounds__(256) void ssd_chunk_fwd_k(SSDArgs a) {
-  constexpr int LDN = N + 16;
-  __shared__ __attribute__((aligned(16))) bf16_t Cs[Q * LDN];
-  __shared__ __attribute__((aligned(16))) bf16_t Bs[Q * LDN];
-  __shared__ __attribute__((aligned(16))) bf16_t Xs[Q * LD64];
-  __shared__ __attribute__((aligned(16))) bf16_t Ms[Q * LD64];
-  __shared__ __attribute__((aligned(16))) bf16_t Ys[Q * LD64];  // y of the previous head, [i][p]
-  const int c = blockIdx.x, hgi = blockIdx.y, b = blockIdx.z;
-  const int h0 = hgi * a.HGf, g = h0 / (a.H / a.G);
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63, li = l & 15, lg = l >> 4;
-  const int valid = min(Q, a.L - c * Q);
-  stage_tile<Q, N>(Cs, LDN, a.Cm + (int64_t)b * a.sCb + (int64_t)c * Q * a.sCl + (int64_t)g * a.sCg, a.sCl, valid);
-  stage_tile<Q, N>(Bs, LDN, a.Bm + (int64_t)b * a.sBb + (int64_t)c * Q * a.sBl + (int64_t)g * a.sBg, a.sBl, valid);
-  // per-head prefetch: X tile (2 x 16 B per thread), S rows 16w+li (A fragments), cum/dt for M
-  Tile64<256> px;
-  bf16x8 ps[N / 32];
-  float pci;              // cum_i of this lane's M row i = 16w + li
-  float4 pcj[4], pdj[4];  // cum_j / dt_j, j = 16jt + 4lg .. +3
-  float pce[4];           // cum_i, i = 16it + li (the e^{cum_i} scale of Y_off)
-  auto prefetch = [&](int h) {
-    px.load(a.x + (int64_t)b * a.sxb + (int64_t)c * Q * a.sxl + (int64_t)h * a.sxh, a.sxl, valid);
-    const bf16_t* sg = a.states + ((((int64_t)b * a.nc + c) * a.H + h) * P + 16 * w + li) * N + 8 * lg;
-#pragma unroll
-    for (int ks = 0; ks < N / 32; ++ks) ps[ks] = *reinterpret_cast<const bf16x8*>(sg + 32 * ks);
-    const float* cb = a.cum + ((int64_t)b * a.H + h) * a.Lp + c * Q;
-    const float* db = a.dtp + ((int64_t)b * a.H + h) * a.Lp + c * Q;
-    pci = cb[16 * w + li];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      pcj[t] = *reinterpret_cast<const float4*>(cb + 16 * t + 4 * lg);
-      pdj[t] = *reinterpret_cast<const float4*>(db + 16 * t + 4 * lg);
-      pce[t] = cb[16 * t + li];
-    }
-  };
-  prefetch(h0);
-  __syncthreads();
-  // C.B^T for rows i of tile w: cbt[jt][r] = C_i . B_j, i = 16w + li, j = 16jt + 4lg + r  (jt <= w)
-  f32x4 cbt[4];
-#pragma unroll
-  for (int jt = 0; jt < 4; ++jt) {
-    cbt[jt] = zero4();
-    if (jt <= w) {
-#pragma unroll
-      for (int ks = 0; ks < N / 32; ++ks)
-        cbt[jt] = mfma16(frag_kc(Bs, LDN, 16 * jt, 32 * ks), frag_kc(Cs, LDN, 16 * w, 32 * ks), cbt[jt]);
-    }
-  }
-  const int i_m = 16 * w + li;  // this lane's M row
-  // y rows of head hy staged in Ys -> whole 128-B rows to HBM (2 x 16 B per thread)
-  auto store_y = [&](int hy) {
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int i = (threadIdx.x >> 3) + 32 * k, col = (threadIdx.x & 7) * 8;
-      if (i < valid)
-        *reinterpret_cast<uint4*>(a.y + (int64_t)b * a.syb + (int64_t)(c * Q + i) * a.syl + (int64_t)hy * a.syh + col) =
-            *reinterpret_cast<const uint4*>(Ys + i * LD64 + col);
-    }
-  };
-  for (int hh = 0; hh < a.HGf; ++hh) {
-    const int h = h0 + hh;
-    __syncthreads();  // the previous head is done with Xs / Ms and has staged its y in Ys
-    if (hh > 0) store_y(h - 1);
-    px.store(Xs, LD64);
-    // M rows i of tile w (8-B writes of 4 consecutive j); j > i masked
-#pragma unroll
-    for (int jt = 0; jt < 4; ++jt) {
-      float m[4] = {0.f, 0.f, 0.f, 0.f};
-      if (jt <= w) {
-        const float cj[4] = {pcj[jt].x, pcj[jt].y, pcj[jt].z, pcj[jt].w};
-        const float dj[4] = {pdj[jt].x, pdj[jt].y, pdj[jt].z, pdj[jt].w};
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int j = 16 * jt + 4 * lg + r;
-          m[r] = j <= i_m ? cbt[jt][r] * __expf(pci - cj[r]) * dj[r] : 0.f;
-        }
-      }
-      *reinterpret_cast<uint2*>(Ms + i_m * LD64 + 16 * jt + 4 * lg) = make_uint2(pack2(m[0], m[1]), pack2(m[2], m[3]));
-    }
-    bf16x8 sA[N / 32];
-#pragma unroll
-    for (int ks = 0; ks < N / 32; ++ks) sA[ks] = ps[ks];
-    float ei[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) ei[t] = __expf(pce[t]);
-    __syncthreads();
-    if (hh + 1 < a.HGf) prefetch(h + 1);
-    const float Dh = a.D ? a.D[h] : 0.f;
-    // Y^T tiles: rows p = 16w + 4lg + r, cols i = 16it + li
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      f32x4 acc = zero4();
-#pragma unroll
-      for (int ks = 0; ks < N / 32; ++ks) acc = mfma16(sA[ks], frag_kc(Cs, LDN, 16 * it, 32 * ks), acc);
-      acc *= ei[it];
-#pragma unroll
-      for (int m = 0; m < 2; ++m)
-        if (2 * m <= it) acc = mfma16(frag_tr(Xs, LD64, 32 * m, 16 * w), frag_kc(Ms, LD64, 16 * it, 32 * m), acc);
-      const int i = 16 * it + li;
-      float xv[4];
-      ld4<bf16_t>(Xs + i * LD64 + 16 * w + 4 * lg, xv);
-      *reinterpret_cast<uint2*>(Ys + i * LD64 + 16 * w + 4 * lg) =
-          make_uint2(pack2(acc[0] + Dh * xv[0], acc[1] + Dh * xv[1]), pack2(acc[2] + Dh * xv[2], acc[3] + Dh * xv[3]));
-    }
-  }
-  __syncthreads();
-  store_y(h0 + a.HGf - 1);
-}
-
-// MAMBA_AMD_SSD_WALK=0: the previous whole-state sequential kernels (ssd_fused_fwd_k / ssd_dstate_bwd_k),
-// kept for A/B and as a cross-check in the tests; 1..3: the walk with that ring depth
-static int ssd_walk_mode() {
-  const char* e = std::getenv("MAMBA_AMD_SSD_WALK");
-  const int v = e ? std::atoi(e) : 0;  // measured in isolation at the 280M shape: walk+chunk fwd 210 us vs
-                                       // fused 172 us; walk bwd 75 us vs dstate 76 us -> legacy default
-  return v < 0 ? 0 : (v > 3 ? 3 : v);
-}
-template <bool BWD>
-static void launch_walk(const SSDArgs& a, int depth, hipStream_t st) {
-  const dim3 grid((unsigned)(a.B * a.H * (a.N / 64)));
-  if (depth == 1) hipLaunchKernelGGL((ssd_walk_k<BWD, 1>), grid, dim3(256), 0, st, a);
-  else if (depth == 2) hipLaunchKernelGGL((ssd_walk_k<BWD, 2>), grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((ssd_walk_k<BWD, 3>), grid, dim3(256), 0, st, a);
-}
-
 // ============================== launchers =====================================================
 #define N_SWITCH(Nv, ...)                                       \
   do {                                                          \
@@ -1113,21 +827,12 @@ hipError_t launch_ssd_fwd(const SSDArgs& a, hipStream_t st) {
   const int64_t waves = (int64_t)a.B * a.H * a.nc;
   hipLaunchKernelGGL(ssd_cumsum_k, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, a);
   MAMBA_HIP_CHECK(hipGetLastError());
-  if (const int wm = ssd_walk_mode()) {  // states by the column-split walk, then every chunk's outputs in parallel
-    launch_walk<false>(a, wm, st);
-    MAMBA_HIP_CHECK(hipGetLastError());
-    N_SWITCH(a.N, hipLaunchKernelGGL(ssd_chunk_fwd_k<NN>, dim3(a.nc, a.nhgf, a.B), dim3(256), 0, st, a));
-    return hipGetLastError();
-  }
   N_SWITCH(a.N, hipLaunchKernelGGL(ssd_fused_fwd_k<NN>, dim3(a.H, a.B), dim3(256), 0, st, a));
   return hipGetLastError();
 }
 
 hipError_t launch_ssd_bwd(const SSDArgs& a, hipStream_t st) {
-  if (const int wm = ssd_walk_mode())
-    launch_walk<true>(a, wm, st);
-  else
-    N_SWITCH(a.N, hipLaunchKernelGGL(ssd_dstate_bwd_k<NN>, dim3(a.H, a.B), dim3(256), 0, st, a));
+  N_SWITCH(a.N, hipLaunchKernelGGL(ssd_dstate_bwd_k<NN>, dim3(a.H, a.B), dim3(256), 0, st, a));
   MAMBA_HIP_CHECK(hipGetLastError());
   N_SWITCH(a.N, hipLaunchKernelGGL(ssd_chunk_bwd_k<NN>, dim3(a.nc, a.nhg, a.B), dim3(512), 0, st, a));
   MAMBA_HIP_CHECK(hipGetLastError());

@@ -117,7 +117,9 @@ def evaluate(model_type, hf_model_name: str, device: str = "cuda", checkpoint_pa
              data_dir: str = "hellaswag", num_examples: int = 2000, out_file: str = "log/hellaswag_eval.txt",
              dtype: str = "fp32", model: Optional[LMHeadModel] = None, verbose: bool = True,
              allow_byte_tokenizer: bool = False, enc=None) -> float:
-    torch.set_float32_matmul_precision("high")
+    # the reference's "high" (TF32 on A100, eval.py:125) has no gfx950 counterpart, and under "high" a
+    # replayed TunableOp table can select garbage GEMMs (utils/gemm_tuning.py): keep exact fp32
+    torch.set_float32_matmul_precision("highest")
     enc = enc if enc is not None else get_encoding("gpt2")
     tok_name = getattr(enc, "name", type(enc).__name__)
     if tok_name == "bytes" and not allow_byte_tokenizer:

@@ -60,6 +60,24 @@ class _FusedMamba2Step:
         self.norm_f = bb.norm_f
         self.norm_f_w = f32(bb.norm_f.weight)
 
+    @torch.no_grad()
+    def refresh(self):
+        """Re-derive the parameter copies IN PLACE from the model's current weights (after training steps), so
+        a captured graph that points at them stays valid."""
+        bb = self.model.backbone
+        for blk, L in zip(bb.layers, self.layers):
+            m = blk.mixer
+            L["norm_w"].copy_(blk.norm.weight)
+            L["W_in"].copy_(m.in_proj.weight)
+            L["conv_w"].copy_(m.conv1d.weight.reshape(m.conv1d.weight.shape[0], -1))
+            if L["conv_b"] is not None:
+                L["conv_b"].copy_(m.conv1d.bias)
+            L["A"].copy_(-torch.exp(m.A_log.float()))
+            L["D"].copy_(m.D)
+            L["dt_bias"].copy_(m.dt_bias)
+            L["W_out"].copy_(m.out_proj.weight.float() * m.norm.weight.float()[None, :])
+        self.norm_f_w.copy_(bb.norm_f.weight)
+
     @staticmethod
     def supported(model: MambaLMHeadModel, batch_size: int) -> bool:
         from .models.mamba2 import Mamba2
@@ -132,6 +150,11 @@ class GraphedDecoder:
         for t in self._states():
             t.zero_()
         self.params.seqlen_offset = 0
+
+    def refresh(self):
+        """Pick up weight updates made since construction (the fused step's derived copies)."""
+        if self.fused is not None:
+            self.fused.refresh()
 
     @torch.no_grad()
     def prefill(self, input_ids: torch.Tensor) -> torch.Tensor:

@@ -51,16 +51,26 @@ def accumulation_scope(defer_reduce: bool = True):
     if _scope_depth == 0:
         _defer_scope = bool(defer_reduce)
     _scope_depth += 1
+    ok = False
     try:
         yield
+        ok = True
     finally:
         _scope_depth -= 1
         if _scope_depth == 0:
             _direct = False
             _wcache.clear()
+            # partials added on a no-sync micro-step and never reduced on the sync one would be lost: the
+            # parameter got no gradient on the last micro-step.  Fail loudly on a normal exit.
+            stuck = [key[1] for key, ent in _bufs.items() if ent[2]]
             for ent in _bufs.values():  # buffers are kept (reused next step); their contents are dead
                 ent[2] = False
             join_side()
+            if ok and stuck:
+                raise RuntimeError(
+                    f"grad_accum: deferred gradient partials ({sorted(set(stuck))}) were accumulated on no-sync "
+                    "micro-steps but never reduced: the last micro-step produced no gradient for those "
+                    "parameters. Run with MAMBA_AMD_DEFER_REDUCE=0 for such models.")
 
 
 def set_direct(enabled: bool) -> None:
@@ -82,9 +92,7 @@ def side_stream(device: torch.device):
     idx = device.index if device.index is not None else torch.cuda.current_device()
     s = _side.get(idx)
     if s is None:
-        from ..utils.cu_mask import env_eighths, masked_stream
-        k = env_eighths("MAMBA_AMD_SIDE_CUS")  # optional CU partition (utils/cu_mask.py)
-        s = masked_stream(idx, k) if k else torch.cuda.Stream(device=idx)
+        s = torch.cuda.Stream(device=idx)
         _side[idx] = s
     _side_dirty.add(idx)
     return s
@@ -117,6 +125,13 @@ def deferred(param, tag: str, shape, device):
     key = (id(param), tag)
     shape = tuple(int(v) for v in shape)
     ent = _bufs.get(key)
+    if ent is not None and ent[0] is param and ent[2] and (tuple(ent[1].shape) != shape or ent[1].device != device):
+        # the partial-row / slab layout depends on the micro-batch shape (rows = f(B*L)); a different shape
+        # inside one optimizer step (a short last micro-batch, varlen packing) cannot add into the pending
+        # partials, and starting a new buffer would drop them: refuse instead
+        raise RuntimeError(
+            f"grad_accum: micro-batch shape changed inside one optimizer step ({tag}: partials {tuple(ent[1].shape)} "
+            f"-> {shape}); deferred reductions need equal micro-batches. Run with MAMBA_AMD_DEFER_REDUCE=0.")
     if ent is None or ent[0] is not param or tuple(ent[1].shape) != shape or ent[1].device != device:
         ent = [param, torch.empty(shape, device=device, dtype=torch.float32), False]
         _bufs[key] = ent

@@ -1,8 +1,9 @@
-"""Bias-free projection (nn.Linear without bias) with a native weight-gradient GEMM.
+"""Bias-free projection (nn.Linear without bias) on the native MFMA GEMM engines.
 
-Forward and input-gradient GEMMs are plain GEMMs (no fusion) on hipBLASLt with the pinned TunableOp table
-(``utils/gemm_tuning``), measured faster at these shapes than the native engine, whose 256 x 192 tile for the
-d_model-wide outputs stays available as an opt-in (``_narrow_native``).  The weight
+Forward and input-gradient GEMMs run on the persistent engine (``gp_pk``: one workgroup per CU walks the
+output tiles; the next tile's operands stream into LDS while the previous tile's bf16 epilogue drains as
+whole-row stores), the input gradient as dY . (W^T)^T against a transposed weight cached per optimizer step;
+shapes it does not take (short K, small token counts) fall back to hipBLASLt.  The weight
 gradient dW = dY^T X reduces over all B*T tokens into a small output (3352 x 768 for in_proj), where the
 library leaves most CUs idle: the native engine (csrc/kernels/gemm_pipe.hip, ``gp_mm`` with both operands
 token-major) splits the tokens into S K-slices written as fp32 slabs.  Inside an accumulation scope the
@@ -64,41 +65,14 @@ def _wgrad_native(p, dy2: torch.Tensor, x2: torch.Tensor):
     return dw
 
 
-def _native_dgrad_ok(dy2: torch.Tensor, w: torch.Tensor) -> bool:
-    """Opt-in (MAMBA_AMD_NATIVE_DGRAD=1): the input gradient dX = dY W on the native pipelined engine for
-    short contractions (K = out_features <= 1024, the out_proj of the d_model=768 models).  In isolation it
-    is 3% faster than the tuned hipBLASLt solution (91.6-94 vs 94-97 us, profiles/r2_v3_gemm_pipe_bench.log)
-    but the whole 280M step is 1% slower with it (276.6k vs 279.3k tok/s, interleaved A/B,
-    profiles/r2_v5_ab_native_dgrad.txt: its 128 KB-LDS workgroups crowd the overlapped micro-batch's
-    kernels), so hipBLASLt stays the default."""
+def _pk_ok(a2: torch.Tensor, n_out: int, k: int) -> bool:
+    """The persistent native GEMM (csrc/kernels/gemm_pipe.hip::gemm_pk_k, ``gp_pk``) for a forward or
+    input-gradient projection: a2 (T, k) token-major bf16 times a k-contiguous (n_out, k) weight image.
+    MAMBA_AMD_PROJ_GEMM=lib keeps hipBLASLt (A/B)."""
     import os
-    return (os.environ.get("MAMBA_AMD_NATIVE_DGRAD", "0") == "1" and dy2.dtype == torch.bfloat16
-            and w.dtype == torch.bfloat16 and dy2.is_cuda and w.is_contiguous() and w.shape[0] <= 1024
-            and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0 and dy2.shape[0] >= 4096)
-
-
-def _dgrad_native(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """dX (T, in) = dY (T, out) . W (out, in): A k-contiguous, B (k rows, n contiguous), bf16 epilogue."""
-    return _ext.ops().gp_mm(dy2, w, None, 0, 1, 0, 1, 256)
-
-
-def _narrow_native() -> bool:
-    """MAMBA_AMD_NATIVE_NARROW=1 (opt-in; default off): GEMMs whose OUTPUT is d_model <= 1024 wide -- the out_proj
-    forward and the in_proj input gradient of the 280M models -- on the native engine's 256 x 192 tile
-    (gemm_pipe.hip, tile code 192): N = 768 makes 4 column tiles, so 32768 rows are 512 tiles = exactly two
-    rounds of 256 CUs, where 256-wide tiles (ours or the library's) leave the second round half empty.  The
-    input gradient reads W^T as a k-contiguous operand, transposed once per optimizer step
-    (grad_accum.cached_transpose).  Measured on one MI355X (profiles/r2_v7_narrow_tile_ab.txt): the out_proj
-    forward 71.4 us against hipBLASLt's 69.5 (256 x 256: 79.7), the in_proj input gradient 203 against 167,
-    whole 280M step -2.2 % (277.5k vs 283.6k tok/s, interleaved), so the library stays the default."""
-    import os
-    return os.environ.get("MAMBA_AMD_NATIVE_NARROW", "0") == "1"
-
-
-def _narrow_ok(a: torch.Tensor, n_out: int, k: int) -> bool:
-    return (a.is_cuda and a.dtype == torch.bfloat16 and a.dim() == 2 and a.stride(-1) == 1
-            and a.stride(0) % 8 == 0 and a.data_ptr() % 16 == 0 and a.shape[0] >= 8192
-            and 384 <= n_out <= 1024 and n_out % 8 == 0 and k % 8 == 0 and _narrow_native())
+    return (a2.is_cuda and a2.dtype == torch.bfloat16 and a2.dim() == 2 and a2.stride(-1) == 1
+            and a2.stride(0) % 8 == 0 and a2.data_ptr() % 16 == 0 and a2.shape[0] >= 4096 and k > 192
+            and k % 8 == 0 and n_out % 8 == 0 and os.environ.get("MAMBA_AMD_PROJ_GEMM", "lib") != "lib")
 
 
 class _ProjFn(torch.autograd.Function):
@@ -106,8 +80,8 @@ class _ProjFn(torch.autograd.Function):
     def forward(ctx, x, weight, cd):
         x2 = x.reshape(-1, x.shape[-1]).to(cd)
         w = grad_accum.cached_cast(weight, cd)
-        if _narrow_ok(x2, w.shape[0], w.shape[1]) and w.is_contiguous():
-            y = _ext.ops().gp_mm(x2, w, None, 0, 0, 0, 1, 192)
+        if _pk_ok(x2, w.shape[0], w.shape[1]) and w.is_contiguous():
+            y = _ext.ops().gp_pk(x2, w)
         else:
             y = F.linear(x2, w)
         ctx.save_for_backward(x2, w)
@@ -126,10 +100,9 @@ class _ProjFn(torch.autograd.Function):
             dy2 = dy2.contiguous()
         dx = None
         if ctx.needs_input_grad[0]:
-            if _narrow_ok(dy2, w.shape[1], w.shape[0]):
-                dx = _ext.ops().gp_mm(dy2, grad_accum.cached_transpose(ctx.param, w.dtype), None, 0, 0, 0, 1, 192)
-            elif _native_dgrad_ok(dy2, w):
-                dx = _dgrad_native(dy2, w)
+            if _pk_ok(dy2, w.shape[1], w.shape[0]):
+                # dX = dY W as a KC . KC product against W^T, transposed once per optimizer step
+                dx = _ext.ops().gp_pk(dy2, grad_accum.cached_transpose(ctx.param, w.dtype))
             else:
                 dx = torch.mm(dy2, w)
         dw = None

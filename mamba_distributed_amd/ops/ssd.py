@@ -190,7 +190,9 @@ class _Mamba2InnerFn(torch.autograd.Function):
         d_n = grad_accum.deferred(pn, "gated_rmsnorm", (ops.part_rows("gated_rmsnorm", b * l), di), dev)
         d_s = grad_accum.deferred(pA, "ssd_small", (b * ((l + NATIVE_CHUNK - 1) // NATIVE_CHUNK), 3, H), dev)
         ck = "conv_cl" if seq_idx is None else "conv_cl_var"
-        d_c = grad_accum.deferred(pw, ck, (ops.part_rows(ck, b, l), conv_dim, w2.shape[1] + 1), dev)
+        # one tag for both conv kernels: their partial rows differ, so seq_idx appearing on only some micro-steps
+        # of a step is refused by grad_accum.deferred instead of silently starting a second buffer
+        d_c = grad_accum.deferred(pw, "conv_cl", (ops.part_rows(ck, b, l), conv_dim, w2.shape[1] + 1), dev)
         # gated norm backward writes dz straight into its slice of d(zxbcdt)
         dy, _, dnorm_w = ops.gated_rmsnorm_bwd(dyn.reshape(b * l, di), y.view(b * l, di),
                                                z.flatten(0, 1), norm_w, rstd, di // ngroups, nbg,

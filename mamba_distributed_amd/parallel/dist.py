@@ -52,10 +52,7 @@ def init_distributed(backend: str = "auto", device_type: str = "auto", timeout_s
         backend = "nccl" if want_cuda else "gloo"
     if want_cuda:
         rccl_env_defaults()
-        # MAMBA_AMD_SHARE_GPU=1: rehearsal of the multi-rank RCCL path on a box with fewer GPUs than ranks
-        # (ranks wrap onto the visible devices; never set for a real node run)
-        share = os.environ.get("MAMBA_AMD_SHARE_GPU", "0") == "1"
-        dev = f"cuda:{local_rank % torch.cuda.device_count() if share else local_rank}"
+        dev = f"cuda:{local_rank}"
         torch.cuda.set_device(dev)
     else:
         dev = "cpu"

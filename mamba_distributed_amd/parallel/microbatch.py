@@ -112,10 +112,7 @@ def run_micro_batches(model, next_batch: Callable, accum: int, compute_loss: Cal
     if other is None:
         # same priority as the caller's stream (a high-priority compute stream makes both micro-batch
         # streams outrank the weight-gradient side stream, ops/grad_accum.py)
-        from ..utils.cu_mask import env_eighths, masked_stream
-        k = env_eighths("MAMBA_AMD_OTHER_CUS")  # optional CU partition (utils/cu_mask.py)
-        other = _OTHER[dev] = (masked_stream(dev, k) if k else
-                               torch.cuda.Stream(device=dev, priority=main.priority))
+        other = _OTHER[dev] = torch.cuda.Stream(device=dev, priority=main.priority)
     streams = [main if (accum - 1 - k) % 2 == 0 else other for k in range(accum)]
     # everything the caller queued on ``main`` (the previous optimizer step updating the weights and
     # reading the gradients that zero_grad just released) precedes the first forward when that runs

@@ -62,6 +62,7 @@ class GradReducer:
             self._attach(p)
         self._hooks = [p.register_post_accumulate_grad_hook(self._hook) for p in params]
         self._armed = False
+        self._main = None  # the stream that called arm() (the caller's / main micro-batch stream)
         # exposed all-reduce time per sync step: stream time from the end of the last backward
         # (finish() entry, in stream order) to the averaged gradients being ready (finish() exit)
         self.timing = False
@@ -92,6 +93,7 @@ class GradReducer:
 
     def arm(self) -> None:
         """Call right before the sync micro-step's backward: its gradient hooks launch the buckets."""
+        self._main = torch.cuda.current_stream(self.flat.device) if self.flat.is_cuda else None
         self._armed = True
         self._left = [n for _, _, n in self.buckets]
         self._next = 0
@@ -106,9 +108,27 @@ class GradReducer:
             self._works.append(self._all_reduce(self.flat[s:e]))
             self._next += 1
 
+    def _join_producers(self) -> None:
+        """Order the bucket's collective after EVERY stream that may have produced or accumulated one of its
+        gradients.  Autograd runs a parameter's AccumulateGrad (and fires this hook) on whichever stream its
+        node was created on -- with two micro-batch graphs alive that is often the other micro-batch stream
+        (parallel/microbatch.py) -- so the stream current here need not be the one that wrote every
+        gradient of the bucket.  RCCL orders its collective after the current stream only: make that stream
+        wait for the default, the second micro-batch and the weight-gradient side stream first."""
+        if not self.flat.is_cuda:
+            return
+        from ..ops import grad_accum
+        from .microbatch import _OTHER
+        dev = self.flat.device.index if self.flat.device.index is not None else torch.cuda.current_device()
+        cur = torch.cuda.current_stream(dev)
+        for s in (torch.cuda.default_stream(dev), self._main, _OTHER.get(dev), grad_accum._side.get(dev)):
+            if s is not None and s != cur:
+                cur.wait_stream(s)
+
     def _all_reduce(self, t: torch.Tensor):
         if self.world == 1:
             return None
+        self._join_producers()
         if self.comm_dtype is None:
             return (dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True), None, None)
         tmp = t.mul(1.0 / self.world).to(self.comm_dtype)

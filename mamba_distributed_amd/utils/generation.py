@@ -13,13 +13,15 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import Optional, Tuple
 
+import weakref
+
 import torch
 
 
 @dataclass
 class DecodeOutput:
     sequences: torch.Tensor                     # (b, prompt + generated)
-    scores: Optional[Tuple[torch.Tensor, ...]] = None  # per generated token: (b, V) processed logits
+    scores: Optional[Tuple[torch.Tensor, ...]] = None  # per generated token: (b, V) logits before the penalty
 
 
 def modify_logits_for_top_p_filtering(logits: torch.Tensor, top_p: float) -> None:
@@ -72,6 +74,9 @@ def sample(logits: torch.Tensor, top_k: int = 1, top_p: float = 0.0, min_p: floa
     return torch.multinomial(torch.softmax(work, dim=-1), num_samples=1).squeeze(-1)
 
 
+_DECODERS: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()  # model -> {(b, max_length, cg, dev): decoder}
+
+
 @torch.no_grad()
 def decode(input_ids: torch.Tensor, model, max_length: int, top_k: int = 1, top_p: float = 0.0,
            min_p: float = 0.0, temperature: float = 1.0, repetition_penalty: float = 1.0,
@@ -84,7 +89,15 @@ def decode(input_ids: torch.Tensor, model, max_length: int, top_k: int = 1, top_
     from ..inference import GraphedDecoder
     b, l0 = input_ids.shape
     dev = input_ids.device
-    dec = GraphedDecoder(model, batch_size=b, max_seqlen=max_length, use_graph=None if cg else False)
+    # one decoder (caches + captured graph) per (batch, max_length, cg), kept on the model like upstream's
+    # graph cache; reused calls reset the states and re-derive the fused step's weight copies
+    cache = _DECODERS.setdefault(model, {})
+    key = (b, max_length, bool(cg), dev)
+    dec = cache.get(key)
+    if dec is None:
+        dec = cache[key] = GraphedDecoder(model, batch_size=b, max_seqlen=max_length, use_graph=None if cg else False)
+    else:
+        dec.refresh()
     seqs = [input_ids]
     scores = []
     logits = dec.prefill(input_ids)
@@ -93,15 +106,16 @@ def decode(input_ids: torch.Tensor, model, max_length: int, top_k: int = 1, top_
         logits = logits.float()
         if vocab_size is not None:
             logits = logits[:, :vocab_size]
+        if output_scores:  # the raw logits, like upstream (the penalty only shapes the sampling copy)
+            scores.append(logits.clone())
+        work = logits
         if repetition_penalty != 1.0:
-            logits = modify_logit_for_repetition_penalty(logits.clone(), torch.cat(seqs, 1), repetition_penalty)
+            work = modify_logit_for_repetition_penalty(logits.clone(), torch.cat(seqs, 1), repetition_penalty)
         pos = sum(s.shape[1] for s in seqs)
         if teacher_outputs is not None and pos < teacher_outputs.shape[1]:
             tok = teacher_outputs[:, pos]
         else:
-            tok = sample(logits, top_k=top_k, top_p=top_p, min_p=min_p, temperature=temperature)
-        if output_scores:
-            scores.append(logits.clone())
+            tok = sample(work, top_k=top_k, top_p=top_p, min_p=min_p, temperature=temperature)
         seqs.append(tok.unsqueeze(1))
         if eos_token_id is not None:
             done |= tok == eos_token_id

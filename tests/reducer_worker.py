@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--accum", type=int, default=3)
     ap.add_argument("--bucket-mb", type=float, default=0.25)
     ap.add_argument("--comm-dtype", default="fp32")
+    ap.add_argument("--impl", default="native", choices=["native", "ddp"])
     a = ap.parse_args()
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
@@ -57,8 +58,15 @@ def main():
     with grad_accum.accumulation_scope():
         run_micro_batches(ref, lambda: next(it), n_micro, loss_fn(ref, n_micro), overlap=False)
 
-    dm = wrap_reducer(model, None, a.bucket_mb, comm_dtype=a.comm_dtype)
-    assert len(dm.reducer.buckets) > 4, len(dm.reducer.buckets)
+    if a.impl == "native":
+        dm = wrap_reducer(model, None, a.bucket_mb, comm_dtype=a.comm_dtype)
+        assert len(dm.reducer.buckets) > 4, len(dm.reducer.buckets)
+        nb = len(dm.reducer.buckets)
+    else:  # torch DDP through the same micro-batch loop (sync forward issued after the earlier backwards)
+        from mamba_distributed_amd.parallel.dist import DistInfo
+        info = DistInfo(ddp=True, rank=rank, local_rank=0, world_size=world, device=dev, backend="gloo")
+        dm = ddp_mod.wrap_ddp(model, info, bucket_cap_mb=a.bucket_mb, grad_comm_dtype=a.comm_dtype)
+        nb = -1
     mine = iter(data[rank::world])
     for rep in range(2):  # a second step checks zero_grad + re-arming
         ddp_mod.zero_grad(dm, None)
@@ -71,7 +79,8 @@ def main():
             err = ((p.grad - q.grad).norm() / (q.grad.norm() + 1e-12)).item()
             worst = max(worst, err)
             assert err < tol, (rep, k, err)
-        print(f"rank {rank} step {rep}: buckets={len(dm.reducer.buckets)} worst_rel_err={worst:.2e}", flush=True)
+        print(f"rank {rank} step {rep}: impl={a.impl} accum={a.accum} buckets={nb} worst_rel_err={worst:.2e}",
+              flush=True)
         mine = iter(data[rank::world])
     dist.destroy_process_group()
     print(f"rank {rank} OK", flush=True)

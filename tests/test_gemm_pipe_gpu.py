@@ -34,18 +34,13 @@ def _rel(a, b):
 @pytest.mark.parametrize("la,lb", [(0, 0), (0, 1), (1, 1)])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 768), (300, 264, 200), (1000, 3352, 96),
                                    (768, 520, 1544), (64, 8, 32), (512, 256, 1024)])
-@pytest.mark.parametrize("bm", [256, 128, 1256])
-def test_gp_bf16(cuda, la, lb, M, N, K, bm):
+def test_gp_bf16(cuda, la, lb, M, N, K):
     if la == 1 and (M % 8):
         pytest.skip("XC A needs M % 8 == 0")
-    if la == 1 and bm == 128:
-        pytest.skip("XC A is instantiated at BM = 256 only")
-    if bm == 1256 and (la, lb) != (0, 0):
-        pytest.skip("the 4-wave tile is instantiated for KC.KC only")
     ops = _ops()
     g = torch.Generator(device=cuda).manual_seed(M * 7 + N * 3 + K)
     A, B = _mk(M, K, la, cuda, g), _mk(N, K, lb, cuda, g)
-    C = ops.gp_mm(A, B, None, la, lb, 0, 1, bm)
+    C = ops.gp_mm(A, B, None, la, lb, 0, 1, 256)
     ref = _ref(A, B, la, lb)
     assert C.shape == (M, N) and C.dtype == torch.bfloat16
     assert torch.isfinite(C.float()).all()
@@ -134,17 +129,51 @@ def test_gp_headline_shapes(cuda, which):
         assert _rel(C, ref) < 8e-3
 
 
-@pytest.mark.parametrize("M,N,K", [(32768, 768, 1536), (32768, 768, 3352), (1000, 200, 136), (4096, 392, 64)])
-def test_gp_tile_256x192(cuda, M, N, K):
-    """256 x 192 tile (tile code 192, KC.KC): out_proj forward and the in_proj input gradient with the
-    cached W^T, plus ragged M / N / K tails, vs fp32."""
+# ---- persistent engine (gp_pk: KC . KC, bf16 out, optional row scale) --------------------------------------
+@pytest.mark.parametrize("M,N,K", [(256, 256, 256), (512, 768, 768), (300, 264, 200), (1000, 3352, 776),
+                                   (768, 520, 1544), (64, 8, 256), (4096, 392, 3352), (2048, 1000, 320)])
+def test_gp_pk_bf16(cuda, M, N, K):
+    """Persistent tile walk: ragged M / N (rows past the descriptor read as zeros, stores into the sink),
+    K tails (out-of-range offsets), more tiles than CUs (several tiles per workgroup), fewer tiles than CUs."""
     ops = _ops()
-    g = torch.Generator(device=cuda).manual_seed(5)
-    A = torch.randn(M, K, device=cuda, generator=g).to(torch.bfloat16)
-    B = torch.randn(N, K, device=cuda, generator=g).to(torch.bfloat16)
-    ref = A.float() @ B.float().t()
-    C = ops.gp_mm(A, B, None, 0, 0, 0, 1, 192)
-    assert _rel(C, ref) < 8e-3
-    out = torch.zeros(1, M, N, device=cuda)
-    ops.gp_mm(A, B, out, 0, 0, 2, 1, 192)
-    assert _rel(out[0], ref) < 1e-5
+    g = torch.Generator(device=cuda).manual_seed(M * 5 + N * 3 + K)
+    A, B = _mk(M, K, 0, cuda, g), _mk(N, K, 0, cuda, g)
+    C = ops.gp_pk(A, B)
+    ref = _ref(A, B, 0, 0)
+    assert C.shape == (M, N) and C.dtype == torch.bfloat16
+    assert _rel(C, ref) < 8e-3, _rel(C, ref)
+    rs = torch.rand(M, device=cuda, generator=g) + 0.5
+    Cs = ops.gp_pk(A, B, None, 0, 0, 0, rs)
+    assert _rel(Cs, ref * rs[:, None]) < 8e-3
+    # deterministic across launches
+    assert torch.equal(C, ops.gp_pk(A, B))
+
+
+def test_gp_pk_strided_out_and_unsupported(cuda):
+    """C written into a column slice of a wider buffer (neighbours untouched); K <= 192 is refused."""
+    ops = _ops()
+    g = torch.Generator(device=cuda).manual_seed(9)
+    A = torch.randn(640, 768, device=cuda, generator=g).to(torch.bfloat16)
+    W = torch.randn(264, 768, device=cuda, generator=g).to(torch.bfloat16)
+    outbig = torch.zeros(640, 400, device=cuda, dtype=torch.bfloat16)
+    C = outbig[:, 64:64 + 264]
+    ops.gp_pk(A, W, C)
+    assert _rel(C, A.float() @ W.float().t()) < 8e-3
+    assert (outbig[:, :64] == 0).all() and (outbig[:, 64 + 264:] == 0).all()
+    with pytest.raises(RuntimeError):
+        ops.gp_pk(A[:, :128], W[:, :128])
+
+
+@pytest.mark.parametrize("which", ["in_fwd", "in_dgrad", "out_fwd", "out_dgrad", "lm_fwd"])
+def test_gp_pk_headline_shapes(cuda, which):
+    """The persistent engine at the Mamba-2 280M bench micro-batch (32 x 1024 tokens), input gradients through
+    the transposed weight (KC . KC), vs fp32."""
+    ops = _ops()
+    g = torch.Generator(device=cuda).manual_seed(3)
+    T, d, dp, di = 32768, 768, 3352, 1536
+    rnd = lambda *s: (torch.randn(*s, device=cuda, generator=g) * 0.5).to(torch.bfloat16)  # noqa: E731
+    A, B = {"in_fwd": lambda: (rnd(T, d), rnd(dp, d)), "in_dgrad": lambda: (rnd(T, dp), rnd(d, dp)),
+            "out_fwd": lambda: (rnd(T, di), rnd(d, di)), "out_dgrad": lambda: (rnd(T, d), rnd(di, d)),
+            "lm_fwd": lambda: (rnd(8192, d), rnd(50304, d))}[which]()
+    C = ops.gp_pk(A, B)
+    assert _rel(C, A.float() @ B.float().t()) < 8e-3

@@ -103,3 +103,38 @@ def test_defer_reduce_policy_by_width(monkeypatch):
             assert grad_accum.deferred(p, "t", (2, 4), p.device) is None
     finally:
         grad_accum.release_buffers()
+
+
+def test_deferred_partials_refuse_silent_drops(monkeypatch):
+    """a shape change of a (param, tag) partial buffer with pending partials, or partials added on a
+    no-sync micro-step and never reduced, must raise instead of silently dropping gradient contributions."""
+    import pytest
+    from mamba_distributed_amd.ops import grad_accum
+    monkeypatch.setenv("MAMBA_AMD_DEFER_REDUCE", "1")
+    p = torch.nn.Parameter(torch.zeros(4))
+    try:
+        # equal shapes: no-sync store, no-sync add, sync add + reduce
+        with grad_accum.accumulation_scope():
+            grad_accum.set_direct(True)
+            assert grad_accum.deferred(p, "t", (2, 4), p.device)[1] == 1
+            assert grad_accum.deferred(p, "t", (2, 4), p.device)[1] == 2
+            grad_accum.set_direct(False)
+            assert grad_accum.deferred(p, "t", (2, 4), p.device)[1] == 4
+        # a short micro-batch (different partial-row count) while partials are pending
+        with pytest.raises(RuntimeError, match="shape changed"):
+            with grad_accum.accumulation_scope():
+                grad_accum.set_direct(True)
+                grad_accum.deferred(p, "t", (2, 4), p.device)
+                grad_accum.deferred(p, "t", (3, 4), p.device)
+        # partials of a no-sync micro-step that the sync micro-step never reduces
+        with pytest.raises(RuntimeError, match="never reduced"):
+            with grad_accum.accumulation_scope():
+                grad_accum.set_direct(True)
+                grad_accum.deferred(p, "t", (2, 4), p.device)
+                grad_accum.set_direct(False)
+        # the next step starts clean
+        with grad_accum.accumulation_scope():
+            grad_accum.set_direct(False)
+            assert grad_accum.deferred(p, "t", (3, 4), p.device)[1] == 3
+    finally:
+        grad_accum.release_buffers()
