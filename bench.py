@@ -207,6 +207,8 @@ def main():
             },
         }
         print(json.dumps(out), flush=True)
+    from mamba_distributed_amd.ops import grad_accum
+    grad_accum.release_buffers()
     destroy()
 
 

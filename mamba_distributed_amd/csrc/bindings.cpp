@@ -835,7 +835,7 @@ Tensor gp_mm(Tensor A, Tensor B, optional<Tensor> out, int64_t la, int64_t lb, i
   TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "gp_mm: bf16 operands");
   TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1, "gp_mm: unit inner strides");
   TORCH_CHECK((la == 0 || la == 1) && (lb == 0 || lb == 1) && mode >= 0 && mode <= 2 && splits >= 1, "gp_mm: args");
-  TORCH_CHECK(!(la == 1 && lb == 0), "gp_mm: (la, lb) = (1, 0) is not instantiated");
+  TORCH_CHECK(!(la == 1 && lb == 0 && mode == 0), "gp_mm: (la, lb) = (1, 0) is instantiated for fp32 output only");
   const int64_t M = la == 0 ? A.size(0) : A.size(1), K = la == 0 ? A.size(1) : A.size(0);
   const int64_t N = lb == 0 ? B.size(0) : B.size(1), KB = lb == 0 ? B.size(1) : B.size(0);
   TORCH_CHECK(K == KB, "gp_mm: contraction sizes differ (", K, " vs ", KB, ")");

@@ -35,7 +35,10 @@ HIPCC = os.path.join(ROCM, "bin", "hipcc")
 # MFMA accumulators in arch VGPRs instead of AGPRs where the kernels fit in 256 VGPRs anyway: the
 # SSD chunk walks touch their running state with VALU every chunk (decay, bf16 staging), and in
 # AGPRs each touch costs a v_accvgpr_read/write pair (~100 extra VALU per chunk in the forward).
-PER_FILE_FLAGS = {"ssd.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+PER_FILE_FLAGS = {"ssd.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"],
+                  # the persistent GEMM's one-lane tile claim: without this the atomic optimizer consumes the
+                  # returned value on the spot (s_waitcnt vmcnt(0) behind every in-flight K-tile DMA)
+                  "gemm_pipe.hip": ["-mllvm", "-amdgpu-atomic-optimizer-strategy=None"]}
 
 
 def torch_paths():

@@ -324,13 +324,21 @@ __global__ __launch_bounds__(512) void gemm_pipe_k(GemmPipeArgs a) {
 }
 
 // ---- persistent engine --------------------------------------------------------------------------------------
-// The same 256 x 256 K-loop as gemm_pipe_k, but ONE workgroup per CU walks a static list of output tiles, and
-// the K-tile stream runs across tile boundaries: the last two K-tiles of tile i DMA tile i+1's first two
-// K-tiles into the LDS buffers they free, so the next tile's operands land while tile i's epilogue drains.
-// The epilogue's stores are issued AFTER those DMAs and the first wait of the next tile counts past them
-// (vmcnt(NST)): the stores stay in flight under the next tile's first K-tile (vmcnt counts stores too).
-// The ablation of gemm_pipe_k (profiles/r2_v2_gemm_pipe_ablations.log: 252.6 us with the epilogue, 101.6
-// without, at the in_proj forward shape) puts ~60 % of the non-persistent kernel's time in the store tail.
+// The same K-loop as gemm_pipe_k (256 x 256 or 128 x 256 tiles, 8 waves, 64-deep K-tiles in two LDS buffers),
+// but ONE workgroup per CU walks output tiles, and the K-tile stream runs across tile boundaries: the last two
+// K-tiles of tile i DMA tile i+1's first two K-tiles into the LDS buffers they free, so the next tile's
+// operands land while tile i's epilogue drains.  The epilogue's stores are issued AFTER those DMAs and the
+// first wait of the next tile counts past them (vmcnt(NST)): the stores stay in flight under the next tile's
+// first K-tile (vmcnt counts stores too, in order).  gemm_pipe_k's ablation put ~60 % of its time at the
+// in_proj forward shape in that store tail (profiles/r2_v2_gemm_pipe_ablations.log).
+//
+// Tiles are CLAIMED, not assigned: a workgroup's first tile is its (XCD-remapped) block index, every later
+// one comes from a per-launch atomic counter (one lane, issued a K-tile ahead, published through LDS).  With
+// a static walk a workgroup that starts late -- its CU still busy with the other micro-batch stream's kernels
+// -- holds back its whole share of tiles; a claimed walk gives late starters fewer tiles
+// (profiles/r3/pk2_whole_step_engine_ab.txt: static persistent tiles lost 4 % of the overlapped step while
+// winning in isolation).  Tiles are numbered in groups of 8 M-panels, column-major inside a group, so tiles
+// claimed together share A and B panels.
 //
 // The loop body is branch-free (hipcc stops accumulating MFMAs in place across scalar branches and spills):
 // every wave issues exactly NST epilogue stores (lanes outside C write a sink), and after the last tile the
@@ -340,30 +348,32 @@ __global__ __launch_bounds__(512) void gemm_pipe_k(GemmPipeArgs a) {
 // so rows past M / N and k-rows past K read as zeros (no clamping, no zero page); KC k-chunks past K (the
 // next row's bytes, in range) get an out-of-range offset.
 //
-// bf16 epilogue (EPI 0): each wave stages its 16 x 64 accumulator rows through a private 2 KB LDS slot
-// (XOR-swizzled, conflict-free both ways) so that every global store writes 8 WHOLE 128-B row segments
-// (16 B per lane), instead of 16 rows x 32 B from the accumulator layout.  RS: rows scaled by an fp32
-// `rowscale` vector before rounding (a norm's rstd folded out of the A operand).
+// bf16 epilogue: each wave stages its 16 x 64 accumulator rows through a private 2 KB LDS slot (XOR-swizzled,
+// conflict-free both ways) so that every global store writes 8 WHOLE 128-B row segments (16 B per lane),
+// instead of 16 rows x 32 B from the accumulator layout.  RS: rows scaled by an fp32 `rowscale` vector before
+// rounding (a norm's rstd folded out of the A operand).
 struct GemmPkArgs {
   const bf16_t* A; int64_t lda;
   const bf16_t* B; int64_t ldb;
-  void* C; int64_t ldc;
+  bf16_t* C; int64_t ldc;
   const float* rowscale;        // RS: C[m, :] *= rowscale[m]
+  int* ctr;                     // this launch's counter pair {next claim, finished workgroups}, zero on entry
   unsigned nbA, nbB;            // operand bytes covered by the buffer descriptors
-  int M, N, K, tn, ntiles, kte; // kte: K-tiles per output tile, rounded up to even (>= 4)
+  int M, N, K, tm, tn, ntiles, kte; // kte: K-tiles per output tile, rounded up to even (>= 4)
 };
 
 __device__ __attribute__((aligned(64))) uint4 g_pk_sink[64];  // epilogue stores of lanes outside C
 
-template <int LA, int LB, int EPI, bool RS = false, bool TAIL = false>
+template <int MI, bool RS, bool TAIL>
 __global__ __launch_bounds__(512) void gemm_pk_k(GemmPkArgs a) {
-  constexpr int NT = 512, MI = 8, NJ = 4, WN = 4, MH = 4;
-  constexpr int BM = 256, BN = 256;
+  constexpr int NT = 512, NJ = 4, WN = 4, MH = MI / 2;
+  constexpr int BM = 32 * MI, BN = 256;
   constexpr int SA = BM * 128, SB = BN * 128, SS = SA + SB;
-  constexpr int GA = 4, GB = 4, G = GA + GB;
-  constexpr int STG = EPI == 0 ? 8 * 2048 : 0;
-  constexpr int NST = EPI == 0 ? 2 * MI : MI * NJ;  // epilogue store instructions per wave
-  __shared__ __attribute__((aligned(1024))) char smem[2 * SS + STG];
+  constexpr int GA = BM / 64, GB = 4, G = GA + GB;
+  constexpr int STG = 8 * 2048;
+  constexpr int NST = 2 * MI;  // epilogue store instructions per wave
+  __shared__ __attribute__((aligned(1024))) char smem[2 * SS + STG + 64];
+  int* const claim = reinterpret_cast<int*>(smem + 2 * SS + STG);  // the claimed next tile, LDS-broadcast
 
   const int nwg = gridDim.x;
   int tile = xcd_remap(blockIdx.x, nwg);
@@ -375,46 +385,33 @@ __global__ __launch_bounds__(512) void gemm_pk_k(GemmPkArgs a) {
 
   const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, (short)0, (int)a.nbA, 0x00020000);
   const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)a.B, (short)0, (int)a.nbB, 0x00020000);
-
-  // Lane part of the DMA byte offsets, one VGPR per operand: DMA instruction ii of a KC operand moves rows
-  // 64 ii + (tid >> 3) at chunk (tid & 7) ^ ((tid >> 3) & 7) (64 ii does not change r & 7); of an XC operand,
-  // k-rows 32 (ii & 1) + (tid >> 4) of column half ii >> 1 (32 (ii & 1) changes neither xc_swz bit).  The
-  // rest is wave-uniform.
-  auto lane_off = [&](int L, int64_t ld) -> unsigned {
-    if (L == 0) {
-      const int r = tid >> 3, c = (tid & 7) ^ (r & 7);
-      return (unsigned)(((int64_t)r * ld + 8 * c) * 2);
-    }
-    const int r = tid >> 4, c = 8 * ((tid & 15) ^ (2 * xc_swz(r)));
-    return (unsigned)(((int64_t)r * ld + c) * 2);
-  };
-  const unsigned loA = lane_off(LA, a.lda), loB = lane_off(LB, a.ldb);
-  const int kchunk = 8 * ((tid & 7) ^ ((tid >> 3) & 7));  // KC: the lane's k within a K-tile
-  auto ii_off = [&](int L, int ii, int64_t ld) -> unsigned {  // uniform part of DMA instruction ii
-    return L == 0 ? (unsigned)(64 * ii * ld * 2) : (unsigned)((ii & 1) * 32 * ld * 2 + (ii >> 1) * 256);
-  };
-  const unsigned stepA = LA == 0 ? 128u : (unsigned)(64 * a.lda * 2);
-  const unsigned stepB = LB == 0 ? 128u : (unsigned)(64 * a.ldb * 2);
-  auto tbase = [&](int t, bool isA) -> unsigned {  // tile part of an operand's byte offset
-    const int b = isA ? (t / a.tn) * BM : (t % a.tn) * BN;
-    const int L = isA ? LA : LB;
-    const int64_t ld = isA ? a.lda : a.ldb;
-    return (unsigned)(L == 0 ? (int64_t)b * ld * 2 : (int64_t)b * 2);
+  // KC operands: DMA instruction ii moves rows 64 ii + (tid >> 3) at 16-B chunk (tid & 7) ^ (row & 7)
+  // (64 ii does not change row & 7), so the lane part of every offset is one VGPR per operand
+  const int lrow = tid >> 3, lch = (tid & 7) ^ (lrow & 7);
+  const unsigned loA = (unsigned)(((int64_t)lrow * a.lda + 8 * lch) * 2);
+  const unsigned loB = (unsigned)(((int64_t)lrow * a.ldb + 8 * lch) * 2);
+  const int kchunk = 8 * lch;
+  auto tile_mn = [&](int t, int& m0, int& n0) {  // groups of 8 M-panels, column-major inside a group
+    const int gsz = 8 * a.tn, g = t / gsz, r = t - g * gsz;
+    const int gm = min(8, a.tm - 8 * g);
+    m0 = (8 * g + r % gm) * BM;
+    n0 = (r / gm) * BN;
   };
   // DMA K-tile kt of tile t into buf; part 0: A, 1: B, 2: both
   auto dma = [&](int t, int kt_, char* buf, int part) {
     const int kt = __builtin_amdgcn_readfirstlane(kt_);
-    const unsigned ba = __builtin_amdgcn_readfirstlane(tbase(t, true) + (unsigned)kt * stepA);
-    const unsigned bb = __builtin_amdgcn_readfirstlane(tbase(t, false) + (unsigned)kt * stepB);
-    const bool dead = TAIL && kt * 64 + kchunk >= a.K;  // KC k-chunk past K (in range: the next row's bytes) -> zeros
+    int m0, n0;
+    tile_mn(t, m0, n0);
+    const unsigned ba = __builtin_amdgcn_readfirstlane((unsigned)((int64_t)m0 * a.lda * 2) + (unsigned)kt * 128u);
+    const unsigned bb = __builtin_amdgcn_readfirstlane((unsigned)((int64_t)n0 * a.ldb * 2) + (unsigned)kt * 128u);
+    const bool dead = TAIL && kt * 64 + kchunk >= a.K;  // KC k-chunk past K (in range: the next row's bytes)
 #pragma unroll
     for (int i = 0; i < G; ++i) {
       const bool isA = i < GA;
       if ((part == 0 && !isA) || (part == 1 && isA)) continue;
       const int ii = isA ? i : i - GA;
-      const int L = isA ? LA : LB;
-      unsigned v = (isA ? loA : loB) + (isA ? ba : bb) + ii_off(L, ii, isA ? a.lda : a.ldb);
-      if (L == 0 && dead) v = 0xFFFFFFF0u;
+      unsigned v = isA ? loA + ba + (unsigned)(64 * ii * a.lda * 2) : loB + bb + (unsigned)(64 * ii * a.ldb * 2);
+      if (dead) v = 0xFFFFFFF0u;
       lds_void* dst = (lds_void*)(buf + (isA ? 0 : SA) + (ii * NT + wu * 64) * 16);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rA : rB, dst, 16, v, 0, 0, 0);
     }
@@ -422,22 +419,9 @@ __global__ __launch_bounds__(512) void gemm_pk_k(GemmPkArgs a) {
 
   f32x4 acc[MI][NJ];
   bf16x8 alo[MH], ahi[MH], b0[NJ], b1[NJ];
-  constexpr int NOA = LA == 0 ? 2 : MI, NOB = LB == 0 ? 2 : NJ;
-  int oa[NOA], ob[NOB];
-#pragma unroll
-  for (int i = 0; i < NOA; ++i) oa[i] = LA == 0 ? lane_kc(i) : lane_xc(am0 + 16 * i);
-#pragma unroll
-  for (int j = 0; j < NOB; ++j) ob[j] = LB == 0 ? lane_kc(j) : lane_xc(bn0 + 16 * j);
-  auto fa = [&](const char* img, int i, int ks) -> bf16x8 {
-    const int r0 = am0 + 16 * i;
-    if constexpr (LA == 0) return ld_kc(img, oa[ks], r0);
-    else return ld_xc(img, oa[i], r0, ks);
-  };
-  auto fb = [&](const char* img, int j, int ks) -> bf16x8 {
-    const int c0 = bn0 + 16 * j;
-    if constexpr (LB == 0) return ld_kc(img + SA, ob[ks], c0);
-    else return ld_xc(img + SA, ob[j], c0, ks);
-  };
+  const int ok0 = lane_kc(0), ok1 = lane_kc(1);
+  auto fa = [&](const char* img, int i, int ks) -> bf16x8 { return ld_kc(img, ks ? ok1 : ok0, am0 + 16 * i); };
+  auto fb = [&](const char* img, int j, int ks) -> bf16x8 { return ld_kc(img + SA, ks ? ok1 : ok0, bn0 + 16 * j); };
   auto rd_lo = [&](const char* img, int ks, bf16x8 (&bf)[NJ]) {
 #pragma unroll
     for (int i = 0; i < MH; ++i) alo[i] = fa(img, i, ks);
@@ -465,12 +449,20 @@ __global__ __launch_bounds__(512) void gemm_pk_k(GemmPkArgs a) {
   char* const buf0 = smem;
   char* const buf1 = smem + SS;
   const int KTE = a.kte;
+  int nt = a.ntiles;  // the claimed next tile (>= ntiles: none)
   // One K-tile from `cur` (`nx` holds the next K-tile, landing or landed).  bdma: the B-half DMA (bt, bk) at
   // k-step 0; the barrier's wait leaves `wst` younger VMEM ops (the previous tile's epilogue stores) in flight;
-  // then the DMA (at, ak) into `cur`, both halves when `aboth`.  Every call site passes constant selectors.
-  auto ktile = [&](char* cur, char* nx, bool bdma, int bt, int bk, bool wst, int at, int ak, bool aboth, bool zc) {
+  // rdc: read the claimed next tile (published by the barrier) before the DMA (at, ak) into `cur`, both halves
+  // when `aboth`, at < 0 meaning "the claimed tile, or this one again if none".  Every call site passes
+  // constant selectors.
+  // clm: one lane claims the tile after this one (issued at k-step 0, landed by the barrier's vmcnt(0)) and
+  // stores it in LDS after the barrier; a later barrier publishes it to every wave (rdc)
+  auto ktile = [&](char* cur, char* nx, bool bdma, int bt, int bk, bool wst, int at, int ak, bool aboth, bool zc,
+                   bool rdc, bool clm) {
     rd_hi(cur, 0);
     if (bdma) dma(bt, bk, nx, 1);
+    int old = 0;
+    if (clm && tid == 0) old = __hip_atomic_fetch_add(a.ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     mm_lo(b0, zc);
     pin<MH, MH * NJ, GB>();
     rd_lo(cur, 1, b1);
@@ -484,7 +476,10 @@ __global__ __launch_bounds__(512) void gemm_pk_k(GemmPkArgs a) {
     else vm_wait<0>();
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    dma(at, ak, cur, aboth ? 2 : 0);
+    if (clm && tid == 0) *claim = nwg + old;
+    if (rdc) nt = __builtin_amdgcn_readfirstlane(*claim);
+    const int t = at >= 0 ? at : (nt < a.ntiles ? nt : tile);
+    dma(t, ak, cur, aboth ? 2 : 0);
     rd_lo(nx, 0, b0);
     mm_hi(b1, false);
     pin<MH + NJ, MH * NJ, GA>();
@@ -496,32 +491,31 @@ __global__ __launch_bounds__(512) void gemm_pk_k(GemmPkArgs a) {
   vm_wait<G>();
   __builtin_amdgcn_s_barrier();
   rd_lo(buf0, 0, b0);
-  ktile(buf0, buf1, false, 0, 0, false, tile, 2, false, true);
+  ktile(buf0, buf1, false, 0, 0, false, tile, 2, false, true, false, false);
 
   for (;;) {
-    int nt = tile + nwg;
-    const bool more = nt < a.ntiles;
-    const int ntc = more ? nt : tile;  // past the last tile: harmless re-reads of this one, drained at exit
-    // K-tile 1 and the steady K-tiles
-    ktile(buf1, buf0, true, tile, 2, false, tile, 3, false, false);
+    // K-tile 1 and the steady K-tiles (KTE >= 4)
+    ktile(buf1, buf0, true, tile, 2, false, tile, 3, false, false, false, true);
 #pragma unroll 1
     for (int kt = 2; kt < KTE - 2; kt += 2) {
-      ktile(buf0, buf1, true, tile, kt + 1, false, tile, kt + 2, false, false);
-      ktile(buf1, buf0, true, tile, kt + 2, false, tile, kt + 3, false, false);
+      ktile(buf0, buf1, true, tile, kt + 1, false, tile, kt + 2, false, false, false, false);
+      ktile(buf1, buf0, true, tile, kt + 2, false, tile, kt + 3, false, false, false, false);
     }
-    // the last two K-tiles stream the next tile's K-tiles 0 and 1 (both halves) into the buffers they free
-    ktile(buf0, buf1, true, tile, KTE - 1, false, ntc, 0, false, false);
-    ktile(buf1, buf0, true, ntc, 0, false, ntc, 1, true, false);
+    // the last two K-tiles stream the claimed tile's K-tiles 0 and 1 (both halves) into the buffers they free
+    ktile(buf0, buf1, true, tile, KTE - 1, false, -1, 0, false, false, true, false);
+    const int ntc = nt < a.ntiles ? nt : tile;  // past the last tile: harmless re-reads of this one
+    ktile(buf1, buf0, true, ntc, 0, false, ntc, 1, true, false, false, false);
 
     // ---- epilogue: lane holds C[m][n .. n+3], m = m0 + am0 + 16 i + (l & 15), n = n0 + bn0 + 16 j + 4 (l >> 4)
     // Lane-derived addressing is recomputed here (lane id from mbcnt, wave id from an SGPR): hoisted out of the
     // tile loop it would stay live across the K-loop, whose accumulator and fragment registers leave no room.
-    int el;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(el));
-    const int ew = wu;
-    const int eam0 = (ew / WN) * (BM / 2), ebn0 = (ew % WN) * (BN / WN);
-    const int m0 = (tile / a.tn) * BM, n0 = (tile % a.tn) * BN;
-    if constexpr (EPI == 0) {
+    {
+      int el;
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(el));
+      const int ew = wu;
+      const int eam0 = (ew / WN) * (BM / 2), ebn0 = (ew % WN) * (BN / WN);
+      int m0, n0;
+      tile_mn(tile, m0, n0);
       char* stg = smem + 2 * SS + ew * 2048;
       const int r = el & 15, q = el >> 4;
       const int rr = el >> 3, cc = el & 7;
@@ -548,36 +542,25 @@ __global__ __launch_bounds__(512) void gemm_pk_k(GemmPkArgs a) {
           const int row = rr + 8 * h;
           const uint4 v = *reinterpret_cast<const uint4*>(stg + row * 128 + ((cc ^ (row & 7)) << 4));
           const int m = m0 + eam0 + 16 * i + row;
-          uint4* dst = (m < a.M && n < a.N) ? reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(a.C) + (int64_t)m * a.ldc + n)
-                                            : &g_pk_sink[el];
+          uint4* dst = (m < a.M && n < a.N) ? reinterpret_cast<uint4*>(a.C + (int64_t)m * a.ldc + n) : &g_pk_sink[el];
           *dst = v;
         }
       }
-    } else {
-      const int mr = el & 15, nc = 4 * (el >> 4);
-#pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        const int m = m0 + eam0 + 16 * i + mr;
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const int n = n0 + ebn0 + 16 * j + nc;
-          float4* c = (m < a.M && n < a.N) ? reinterpret_cast<float4*>(reinterpret_cast<float*>(a.C) + (int64_t)m * a.ldc + n)
-                                           : reinterpret_cast<float4*>(&g_pk_sink[el]);
-          float4 v = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
-          if constexpr (EPI == 2) {
-            const float4 o = *c;
-            v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
-          }
-          *c = v;
-        }
-      }
     }
-    if (!more) break;
+    if (nt >= a.ntiles) break;
     tile = nt;
     // the next tile's K-tile 0 (its K-tile 1 landed before the stores above were issued)
-    ktile(buf0, buf1, false, 0, 0, true, tile, 2, false, true);
+    ktile(buf0, buf1, false, 0, 0, true, tile, 2, false, true, false, false);
   }
   vm_wait<0>();  // no LDS-DMA may outlive the workgroup
+  // the last workgroup to finish re-arms this launch's counter pair for its next use
+  if (tid == 0) {
+    const int done = __hip_atomic_fetch_add(a.ctr + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (done == nwg - 1) {
+      __hip_atomic_store(a.ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.ctr + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 // out[i] (+)= sum_s part[s][i] in fixed order (the K-split slabs of a weight gradient)
@@ -635,6 +618,7 @@ hipError_t launch_gemm_pipe(int la, int lb, const void* A, int64_t lda, const vo
   if (la == 0 && lb == 0) { GP_EPI(0, 0) }
   else if (la == 0 && lb == 1) { GP_EPI(0, 1) }
   else if (la == 1 && lb == 1) { GP_EPI(1, 1) }
+  else if (la == 1 && lb == 0 && epi != 0) { GP_EPI(1, 0) }  // the Mamba-1 out_proj weight gradient
   else return hipErrorInvalidValue;
 #undef GP_EPI
   return hipGetLastError();
@@ -653,49 +637,64 @@ static int cu_count() {
 bool gemm_pk_supported(int la, int lb, int epi, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc) {
   if (M <= 0 || N <= 0 || K <= 192) return false;  // >= 4 K-tiles
   if (la != 0 || lb != 0 || epi != 0) return false;  // instantiated: KC . KC, bf16 output
-  if (lda % 8 || ldb % 8 || ldc % 8 || N % 8) return false;
-  if ((la == 0 || lb == 0) && K % 8) return false;
-  if (la == 1 && M % 8) return false;
-  if (la == 0 && lda < K) return false;
-  if (lb == 0 && ldb < K) return false;
-  if (la == 1 && lda < M) return false;
-  if (lb == 1 && ldb < N) return false;
+  if (lda % 8 || ldb % 8 || ldc % 8 || N % 8 || K % 8 || lda < K || ldb < K) return false;
   // every DMA byte offset, including the overhang of partial tiles, must stay below the out-of-range sentinel
   const int64_t kt = ((K + 63) / 64 + 1) / 2 * 2;
   const int64_t lim = ((int64_t)1 << 32) - 64;
   const int64_t Mp = (M + 255) / 256 * 256, Np = (N + 255) / 256 * 256;
-  const int64_t exA = la == 0 ? (Mp * lda + kt * 64) * 2 : (kt * 64 * lda + Mp) * 2;
-  const int64_t exB = lb == 0 ? (Np * ldb + kt * 64) * 2 : (kt * 64 * ldb + Np) * 2;
-  return exA < lim && exB < lim;
+  return (Mp * lda + kt * 64) * 2 < lim && (Np * ldb + kt * 64) * 2 < lim;
+}
+
+// per-launch tile-claim counters: a ring of zeroed {next, done} pairs, each re-armed by its launch's last
+// workgroup; launches in flight at once (two micro-batch streams) never share a pair
+static int* pk_counters(int dev, int& slot) {
+  constexpr int R = 16384;
+  static int* bufs[16] = {};
+  static unsigned seq[16] = {};
+  if (dev < 0 || dev >= 16) return nullptr;
+  if (!bufs[dev]) {
+    void* p = nullptr;
+    if (hipMalloc(&p, R * 2 * sizeof(int)) != hipSuccess || hipMemset(p, 0, R * 2 * sizeof(int)) != hipSuccess)
+      return nullptr;
+    bufs[dev] = (int*)p;
+  }
+  slot = (int)(seq[dev]++ % R);
+  return bufs[dev] + 2 * slot;
 }
 
 hipError_t launch_gemm_pk(int la, int lb, const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
                           int64_t ldc, int M, int N, int K, int epi, const float* rowscale, hipStream_t st) {
   if (!gemm_pk_supported(la, lb, epi, M, N, K, lda, ldb, ldc)) return hipErrorInvalidValue;
+  int dev = 0, slot = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidValue;
   GemmPkArgs a;
   a.A = (const bf16_t*)A; a.lda = lda; a.B = (const bf16_t*)B; a.ldb = ldb;
-  a.C = C; a.ldc = ldc; a.rowscale = rowscale;
-  a.nbA = (unsigned)(la == 0 ? ((int64_t)(M - 1) * lda + K) * 2 : ((int64_t)(K - 1) * lda + M) * 2);
-  a.nbB = (unsigned)(lb == 0 ? ((int64_t)(N - 1) * ldb + K) * 2 : ((int64_t)(K - 1) * ldb + N) * 2);
+  a.C = (bf16_t*)C; a.ldc = ldc; a.rowscale = rowscale;
+  a.ctr = pk_counters(dev, slot);
+  if (!a.ctr) return hipErrorOutOfMemory;
+  a.nbA = (unsigned)(((int64_t)(M - 1) * lda + K) * 2);
+  a.nbB = (unsigned)(((int64_t)(N - 1) * ldb + K) * 2);
   a.M = M; a.N = N; a.K = K;
-  a.tn = (N + 255) / 256;
-  a.ntiles = ((M + 255) / 256) * a.tn;
   a.kte = ((K + 63) / 64 + 1) / 2 * 2;
-  const int nwg = std::min(a.ntiles, cu_count());
-  // K-tail handling only where a KC operand has k-chunks past K inside its rows
+  const int ncu = cu_count();
+  // tile height: 256 unless 128-row tiles fill the rounds better (e.g. N = 768 outputs: 384 tiles of 256 rows
+  // are 1.5 rounds of 256 CUs, 768 of 128 rows are 3 full rounds; a 128-row tile costs ~0.55 of a 256-row one)
+  const int t256 = ((M + 255) / 256) * ((N + 255) / 256), t128 = ((M + 127) / 128) * ((N + 255) / 256);
+  const double c256 = (double)((t256 + ncu - 1) / ncu), c128 = 0.55 * ((t128 + ncu - 1) / ncu);
+  const int bm = c128 < c256 ? 128 : 256;
+  a.tm = (M + bm - 1) / bm; a.tn = (N + 255) / 256;
+  a.ntiles = a.tm * a.tn;
   const bool tail = K % 64 != 0 || a.kte * 64 != K;
-  // instantiated for the projection / lm_head forward and input-gradient products: KC . KC, bf16 output
-  // (input gradients read a per-step cached W^T); the K-split weight gradients stay on gemm_pipe_k
-#define PK_EPI(LA_, LB_)                                                                                     \
-  if (rowscale) {                                                                                           \
-    if (tail) hipLaunchKernelGGL((gemm_pk_k<LA_, LB_, 0, true, true>), dim3(nwg), dim3(512), 0, st, a);     \
-    else hipLaunchKernelGGL((gemm_pk_k<LA_, LB_, 0, true, false>), dim3(nwg), dim3(512), 0, st, a);         \
-  } else {                                                                                                  \
-    if (tail) hipLaunchKernelGGL((gemm_pk_k<LA_, LB_, 0, false, true>), dim3(nwg), dim3(512), 0, st, a);    \
-    else hipLaunchKernelGGL((gemm_pk_k<LA_, LB_, 0, false, false>), dim3(nwg), dim3(512), 0, st, a);        \
+  const int nwg = std::min(a.ntiles, ncu);
+#define PK_L(MI_, RS_)                                                                                  \
+  if (tail) hipLaunchKernelGGL((gemm_pk_k<MI_, RS_, true>), dim3(nwg), dim3(512), 0, st, a);            \
+  else hipLaunchKernelGGL((gemm_pk_k<MI_, RS_, false>), dim3(nwg), dim3(512), 0, st, a)
+  if (bm == 256) {
+    if (rowscale) { PK_L(8, true); } else { PK_L(8, false); }
+  } else {
+    if (rowscale) { PK_L(4, true); } else { PK_L(4, false); }
   }
-  PK_EPI(0, 0)
-#undef PK_EPI
+#undef PK_L
   return hipGetLastError();
 }
 

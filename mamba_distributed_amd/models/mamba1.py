@@ -26,6 +26,7 @@ import torch.nn.functional as F
 
 from ..ops import _ext, grad_accum
 from ..ops.conv1d import causal_conv1d_fn, causal_conv1d_update
+from ..ops.linear import mm_nt
 from ..ops.reference import causal_conv1d_ref, selective_scan_ref, softplus_inverse
 from ..ops.selective_scan import selective_scan_fn, selective_state_update
 
@@ -74,7 +75,7 @@ class _InProjCMFn(torch.autograd.Function):
         w = grad_accum.cached_cast(weight, cd)
         ctx.save_for_backward(h2, w)
         ctx.param = weight
-        return torch.mm(w, h2.t())
+        return mm_nt(w, h2)  # (2di, b*l): the persistent native GEMM (ops/linear.py) or hipBLASLt
 
     @staticmethod
     def backward(ctx, dxz):
@@ -161,6 +162,44 @@ def _wgrad_native_cm(p, dY, X, dy_cm, x_cm):
     return True, grad_accum.defer(p, _ext.ops().gemm_wgrad_cm(dY, X, None, False, dy_cm, x_cm).to(p.dtype))
 
 
+class _OutProjCMFn(torch.autograd.Function):
+    """out (b*l, d) = y2^T W_out^T for the channel-major SSM output y2 (di, b*l), the Mamba-1 out_proj.
+    Backward: d y2 comes out channel-major directly (W^T . dout^T), and dW = dout^T . y2^T runs on the native
+    pipelined engine as fp32 split-K slabs (csrc/kernels/gemm_pipe.hip, dout token-major, y2 k-contiguous),
+    deferred to the sync micro-step like the Mamba-2 projections (ops/linear.py::_wgrad_native)."""
+
+    @staticmethod
+    def forward(ctx, y2, weight, cd):
+        w = grad_accum.cached_cast(weight, cd)
+        ctx.save_for_backward(y2, w)
+        ctx.param = weight
+        return F.linear(y2.t(), w)
+
+    @staticmethod
+    def backward(ctx, dout):
+        from ..ops.linear import _native_ok, _wgrad_native
+        y2, w = ctx.saved_tensors
+        if dout.dtype != w.dtype:
+            dout = dout.to(w.dtype)
+        dout = dout.contiguous()
+        dy2 = None
+        if ctx.needs_input_grad[0]:
+            dy2 = mm_nt(grad_accum.cached_transpose(ctx.param, w.dtype), dout)  # (di, b*l)
+        dw = None
+        if ctx.needs_input_grad[1]:
+            p = ctx.param
+            T = dout.shape[0]
+            ok = (_native_ok(dout, dout) and y2.stride(1) == 1 and y2.stride(0) % 8 == 0 and y2.data_ptr() % 16 == 0
+                  and y2.shape[0] % 8 == 0 and T % 8 == 0 and y2.dtype == torch.bfloat16)
+            if ok:
+                dw = _wgrad_native(p, dout, y2, lb=0)
+                if dw is not None:
+                    dw = grad_accum.defer(p, dw.to(p.dtype))
+            else:
+                dw = grad_accum.defer(p, torch.mm(dout.t(), y2.t()).to(p.dtype))
+        return dy2, dw, None
+
+
 class _Mamba1InnerFn(torch.autograd.Function):
     """conv1d+SiLU -> x_proj -> dt_proj -> selective scan(+D, *silu(z)) ; returns y as (di, b*l)."""
 
@@ -176,7 +215,7 @@ class _Mamba1InnerFn(torch.autograd.Function):
         w2 = conv_w.reshape(di, -1)
         conv_out = ops.conv1d_cf_fwd(x, w2, conv_b, True)                  # (b,di,l) in (di,b,l) memory
         co2 = _flat(conv_out)
-        Wx, Wdt = W_x.to(cd), W_dt.to(cd)
+        Wx, Wdt = grad_accum.cached_cast(W_x, cd), grad_accum.cached_cast(W_dt, cd)  # once per optimizer step
         x_dbl = _mm_cm(Wx, co2)                                             # (R+2N, b*l)
         delta = _mm_cm(Wdt, x_dbl[:R])                                      # (di, b*l)
         Bm = _cm(x_dbl[R:R + N], b, l).unsqueeze(1)                         # (b,1,N,l)
@@ -308,10 +347,11 @@ class Mamba(nn.Module):
             y2 = _Mamba1InnerFn.apply(xz, self.conv1d.weight, self.conv1d.bias, self.x_proj.weight,
                                       self.dt_proj.weight, self.dt_proj.bias.float(), A, self.D.float(),
                                       b, l, cd)
-            # out_proj stays on hipBLASLt end to end: a native dW with a channel-major y operand
-            # (gemm_wgrad_cm, x_cm=True) measured -4.5% in an interleaved A/B
-            out = F.linear(y2.t().to(cd), self.out_proj.weight.to(cd),
-                           None if self.out_proj.bias is None else self.out_proj.bias.to(cd))
+            if self.out_proj.bias is None and y2.dtype == cd:
+                out = _OutProjCMFn.apply(y2, self.out_proj.weight, cd)
+            else:
+                out = F.linear(y2.t().to(cd), grad_accum.cached_cast(self.out_proj.weight, cd),
+                               None if self.out_proj.bias is None else self.out_proj.bias.to(cd))
             return out.view(b, l, -1)
         xz3 = _cm(xz, b, l)
         if conv_state is not None:  # prefill: remember the last d_conv-1 inputs for decoding

@@ -17,7 +17,8 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
-from . import _ext
+from . import _ext, grad_accum
+from .linear import _proj_engine, mm_nt
 
 
 def _inv_count(targets, ignore_index):
@@ -58,9 +59,9 @@ class _FusedLinearCEFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h, weight, targets, ignore_index, compute_dtype):
         h2 = h.reshape(-1, h.shape[-1]).to(compute_dtype)
-        w = weight.to(compute_dtype)
+        w = grad_accum.cached_cast(weight, compute_dtype)        # once per optimizer step
         t = targets.reshape(-1)
-        logits = torch.mm(h2, w.t())                              # hipBLASLt
+        logits = mm_nt(h2, w)                                    # persistent native GEMM or hipBLASLt
         inv = _inv_count(t, ignore_index)
         need_grad = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
         losses = _ext.ops().ce_fwd(logits, t, ignore_index, inv, logits if need_grad else None)
@@ -68,6 +69,7 @@ class _FusedLinearCEFn(torch.autograd.Function):
         if need_grad:
             ctx.save_for_backward(h2, w, logits)               # logits now hold dlogits
         ctx.hshape, ctx.hdtype, ctx.wdtype = h.shape, h.dtype, weight.dtype
+        ctx.param = weight
         return loss
 
     @staticmethod
@@ -76,7 +78,9 @@ class _FusedLinearCEFn(torch.autograd.Function):
         g = gloss.to(torch.float32)
         dh = dw = None
         if ctx.needs_input_grad[0]:
-            dh = torch.mm(dlogits, w).mul_(g).view(ctx.hshape).to(ctx.hdtype)
+            # dh = dlogits W: a K-contiguous product against W^T (cached once per optimizer step)
+            wt = grad_accum.cached_transpose(ctx.param, w.dtype) if _proj_engine() != "lib" else None
+            dh = (mm_nt(dlogits, wt) if wt is not None else torch.mm(dlogits, w)).mul_(g).view(ctx.hshape).to(ctx.hdtype)
         if ctx.needs_input_grad[1]:
             dw = torch.mm(dlogits.t(), h2).to(ctx.wdtype).mul_(g)
         return dh, dw, None, None, None

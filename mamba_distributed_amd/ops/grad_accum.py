@@ -142,8 +142,11 @@ def deferred(param, tag: str, shape, device):
 
 
 def release_buffers() -> None:
-    """Free every deferred-reduction buffer (e.g. before switching models)."""
+    """Free every deferred-reduction buffer and cached weight copy (training end, switching models)."""
+    if _scope_depth:
+        raise RuntimeError("grad_accum.release_buffers() inside an accumulation_scope")
     _bufs.clear()
+    _wcache.clear()
 
 
 def in_scope() -> bool:

@@ -33,14 +33,16 @@ def _native_ok(dy: torch.Tensor, x: torch.Tensor) -> bool:
             and dy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0)
 
 
-def _wgrad_native(p, dy2: torch.Tensor, x2: torch.Tensor):
-    """dW = dy2^T x2 (fp32) on the native engine; None when deferred to the sync micro-step."""
+def _wgrad_native(p, dy2: torch.Tensor, x2: torch.Tensor, lb: int = 1):
+    """dW = dy2^T x2 (fp32) on the native engine; None when deferred to the sync micro-step.  dy2 is token-major
+    (T, P); x2 is token-major (T, Q) (lb = 1) or channel-major (Q, T) (lb = 0: the Mamba-1 out_proj input)."""
     ops = _ext.ops()
-    T, P, Q = dy2.shape[0], dy2.shape[1], x2.shape[1]
+    T, P = dy2.shape[0], dy2.shape[1]
+    Q = x2.shape[1] if lb == 1 else x2.shape[0]
     S = ops.gp_splits(P, Q, T)
     d = grad_accum.deferred(p, "wgrad", (S, P, Q), dy2.device)
     if d is None:  # outside an accumulation scope: transient slabs, reduce now
-        part = ops.gp_mm(dy2, x2, None, 1, 1, 1, S, 256)
+        part = ops.gp_mm(dy2, x2, None, 1, lb, 1, S, 256)
         dw = torch.empty(P, Q, device=dy2.device, dtype=torch.float32)
         ops.gp_reduce(part, dw, False)
         return dw
@@ -51,28 +53,48 @@ def _wgrad_native(p, dy2: torch.Tensor, x2: torch.Tensor):
         # stream beside the rest of the backward (joined before the sync micro-step)
         side = grad_accum.side_stream(dy2.device)
         if side is None:
-            ops.gp_mm(dy2, x2, buf, 1, 1, slab_mode, S, 256)
+            ops.gp_mm(dy2, x2, buf, 1, lb, slab_mode, S, 256)
         else:
             side.wait_stream(torch.cuda.current_stream(dy2.device))
             with torch.cuda.stream(side):
-                ops.gp_mm(dy2, x2, buf, 1, 1, slab_mode, S, 256)
+                ops.gp_mm(dy2, x2, buf, 1, lb, slab_mode, S, 256)
             dy2.record_stream(side)
             x2.record_stream(side)
         return None
-    ops.gp_mm(dy2, x2, buf, 1, 1, slab_mode, S, 256)
+    ops.gp_mm(dy2, x2, buf, 1, lb, slab_mode, S, 256)
     dw = torch.empty(P, Q, device=dy2.device, dtype=torch.float32)
     ops.gp_reduce(buf, dw, False)
     return dw
 
 
-def _pk_ok(a2: torch.Tensor, n_out: int, k: int) -> bool:
-    """The persistent native GEMM (csrc/kernels/gemm_pipe.hip::gemm_pk_k, ``gp_pk``) for a forward or
-    input-gradient projection: a2 (T, k) token-major bf16 times a k-contiguous (n_out, k) weight image.
-    MAMBA_AMD_PROJ_GEMM=lib keeps hipBLASLt (A/B)."""
+def _proj_engine() -> str:
+    """Forward / input-gradient projection GEMM: "pk" (the persistent native engine, gemm_pk_k) or "lib"
+    (hipBLASLt).  MAMBA_AMD_PROJ_GEMM selects (A/B)."""
     import os
+    return os.environ.get("MAMBA_AMD_PROJ_GEMM", "lib")
+
+
+def _pk_ok(a2: torch.Tensor, n_out: int, k: int) -> bool:
+    """The native persistent GEMM for a forward or input-gradient projection: a2 (T, k) token-major bf16 times a
+    k-contiguous (n_out, k) weight image (csrc/kernels/gemm_pipe.hip)."""
     return (a2.is_cuda and a2.dtype == torch.bfloat16 and a2.dim() == 2 and a2.stride(-1) == 1
             and a2.stride(0) % 8 == 0 and a2.data_ptr() % 16 == 0 and a2.shape[0] >= 4096 and k > 192
-            and k % 8 == 0 and n_out % 8 == 0 and os.environ.get("MAMBA_AMD_PROJ_GEMM", "lib") != "lib")
+            and k % 8 == 0 and n_out % 8 == 0 and _proj_engine() != "lib")
+
+
+def _pk_mm(a2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    return _ext.ops().gp_pk(a2, w)
+
+
+def mm_nt(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """``a @ b.T`` for two K-contiguous bf16 operands (a: (M, K), b: (N, K)) on the native persistent GEMM when
+    the shape suits it (M * N >= 2^24, K > 192), else torch.mm.  E.g. the Mamba-1 channel-major in_proj
+    xz = W_in h^T."""
+    ok = (a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.dim() == 2 and b.dim() == 2
+          and a.stride(-1) == 1 and b.stride(-1) == 1 and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0
+          and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0 and a.shape[1] > 192 and a.shape[1] % 8 == 0
+          and b.shape[0] % 8 == 0 and a.shape[0] * b.shape[0] >= (1 << 24) and _proj_engine() != "lib")
+    return _pk_mm(a, b) if ok else torch.mm(a, b.t())
 
 
 class _ProjFn(torch.autograd.Function):
@@ -81,7 +103,7 @@ class _ProjFn(torch.autograd.Function):
         x2 = x.reshape(-1, x.shape[-1]).to(cd)
         w = grad_accum.cached_cast(weight, cd)
         if _pk_ok(x2, w.shape[0], w.shape[1]) and w.is_contiguous():
-            y = _ext.ops().gp_pk(x2, w)
+            y = _pk_mm(x2, w)
         else:
             y = F.linear(x2, w)
         ctx.save_for_backward(x2, w)
@@ -102,7 +124,7 @@ class _ProjFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             if _pk_ok(dy2, w.shape[1], w.shape[0]):
                 # dX = dY W as a KC . KC product against W^T, transposed once per optimizer step
-                dx = _ext.ops().gp_pk(dy2, grad_accum.cached_transpose(ctx.param, w.dtype))
+                dx = _pk_mm(dy2, grad_accum.cached_transpose(ctx.param, w.dtype))
             else:
                 dx = torch.mm(dy2, w)
         dw = None

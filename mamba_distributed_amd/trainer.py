@@ -366,6 +366,10 @@ class Trainer:
                   f"(excluding eval/sample steps)")
         if metrics:
             metrics.close()
+        # the deferred-reduction slabs (~66 MB per 280M out_proj) and partial buffers are dead once training
+        # ends: free them before any in-process eval / generation
+        from .ops import grad_accum
+        grad_accum.release_buffers()
         destroy()
 
 

@@ -130,26 +130,34 @@ def test_gp_headline_shapes(cuda, which):
 
 
 # ---- persistent engine (gp_pk: KC . KC, bf16 out, optional row scale) --------------------------------------
+def _pmm(ops, eng, A, B, rs=None):
+    return ops.gp_pk(A, B, None, 0, 0, 0, rs)
+
+
+@pytest.mark.parametrize("eng", ["pk"])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 256), (512, 768, 768), (300, 264, 200), (1000, 3352, 776),
-                                   (768, 520, 1544), (64, 8, 256), (4096, 392, 3352), (2048, 1000, 320)])
-def test_gp_pk_bf16(cuda, M, N, K):
+                                   (768, 520, 1544), (64, 8, 256), (4096, 392, 3352), (2048, 1000, 320),
+                                   (70000, 136, 448)])
+def test_gp_pk_bf16(cuda, eng, M, N, K):
     """Persistent tile walk: ragged M / N (rows past the descriptor read as zeros, stores into the sink),
     K tails (out-of-range offsets), more tiles than CUs (several tiles per workgroup), fewer tiles than CUs."""
     ops = _ops()
     g = torch.Generator(device=cuda).manual_seed(M * 5 + N * 3 + K)
     A, B = _mk(M, K, 0, cuda, g), _mk(N, K, 0, cuda, g)
-    C = ops.gp_pk(A, B)
+    C = _pmm(ops, eng, A, B)
     ref = _ref(A, B, 0, 0)
     assert C.shape == (M, N) and C.dtype == torch.bfloat16
     assert _rel(C, ref) < 8e-3, _rel(C, ref)
     rs = torch.rand(M, device=cuda, generator=g) + 0.5
-    Cs = ops.gp_pk(A, B, None, 0, 0, 0, rs)
+    Cs = _pmm(ops, eng, A, B, rs)
     assert _rel(Cs, ref * rs[:, None]) < 8e-3
-    # deterministic across launches
-    assert torch.equal(C, ops.gp_pk(A, B))
+    # deterministic across launches, and every row / column written (no stale parked tile)
+    assert torch.equal(C, _pmm(ops, eng, A, B))
+    assert torch.isfinite(C.float()).all()
 
 
-def test_gp_pk_strided_out_and_unsupported(cuda):
+@pytest.mark.parametrize("eng", ["pk"])
+def test_gp_pk_strided_out_and_unsupported(cuda, eng):
     """C written into a column slice of a wider buffer (neighbours untouched); K <= 192 is refused."""
     ops = _ops()
     g = torch.Generator(device=cuda).manual_seed(9)
@@ -161,11 +169,12 @@ def test_gp_pk_strided_out_and_unsupported(cuda):
     assert _rel(C, A.float() @ W.float().t()) < 8e-3
     assert (outbig[:, :64] == 0).all() and (outbig[:, 64 + 264:] == 0).all()
     with pytest.raises(RuntimeError):
-        ops.gp_pk(A[:, :128], W[:, :128])
+        _pmm(ops, eng, A[:, :128], W[:, :128])
 
 
+@pytest.mark.parametrize("eng", ["pk"])
 @pytest.mark.parametrize("which", ["in_fwd", "in_dgrad", "out_fwd", "out_dgrad", "lm_fwd"])
-def test_gp_pk_headline_shapes(cuda, which):
+def test_gp_pk_headline_shapes(cuda, eng, which):
     """The persistent engine at the Mamba-2 280M bench micro-batch (32 x 1024 tokens), input gradients through
     the transposed weight (KC . KC), vs fp32."""
     ops = _ops()
@@ -175,5 +184,26 @@ def test_gp_pk_headline_shapes(cuda, which):
     A, B = {"in_fwd": lambda: (rnd(T, d), rnd(dp, d)), "in_dgrad": lambda: (rnd(T, dp), rnd(d, dp)),
             "out_fwd": lambda: (rnd(T, di), rnd(d, di)), "out_dgrad": lambda: (rnd(T, d), rnd(di, d)),
             "lm_fwd": lambda: (rnd(8192, d), rnd(50304, d))}[which]()
-    C = ops.gp_pk(A, B)
+    C = _pmm(ops, eng, A, B)
     assert _rel(C, A.float() @ B.float().t()) < 8e-3
+
+
+def test_gp_pk_concurrent_streams(cuda):
+    """Tile claims are per launch: many back-to-back launches on two streams (as under the micro-batch overlap)
+    each produce the exact single-launch result."""
+    ops = _ops()
+    g = torch.Generator(device=cuda).manual_seed(11)
+    A1, B1 = _mk(4096, 768, 0, cuda, g), _mk(3352, 768, 0, cuda, g)
+    A2, B2 = _mk(8192, 1536, 0, cuda, g), _mk(768, 1536, 0, cuda, g)
+    r1, r2 = ops.gp_pk(A1, B1), ops.gp_pk(A2, B2)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = []
+    for _ in range(20):
+        with torch.cuda.stream(s1):
+            o1 = ops.gp_pk(A1, B1)
+        with torch.cuda.stream(s2):
+            o2 = ops.gp_pk(A2, B2)
+        outs.append((o1, o2))
+    torch.cuda.synchronize()
+    for o1, o2 in outs:
+        assert torch.equal(o1, r1) and torch.equal(o2, r2)

@@ -301,10 +301,13 @@ def test_model_native_vs_reference(cuda, layer):
     assert not bad, bad
 
 
+@pytest.mark.parametrize("engine", ["lib", "pk"])
 @pytest.mark.parametrize("layer", ["Mamba1", "Mamba2"])
-def test_model_native_vs_reference_headline_width(cuda, layer):
+def test_model_native_vs_reference_headline_width(cuda, monkeypatch, layer, engine):
     """The 280M configs' layer width and sequence length (d_model 768, T=1024, 16 SSD chunks, 24 heads)
-    through 2 layers: loss and every parameter gradient, native kernels vs the fp32 reference ops."""
+    through 2 layers: loss and every parameter gradient, native kernels vs the fp32 reference ops, with the
+    projection / lm_head forward and input-gradient GEMMs on hipBLASLt and on the persistent native engine."""
+    monkeypatch.setenv("MAMBA_AMD_PROJ_GEMM", engine)
     from mamba_distributed_amd import LMHeadModel, MambaConfig
     torch.manual_seed(0)
     cfg = MambaConfig(d_model=768, n_layer=2, vocab_size=4096, ssm_cfg={"layer": layer})
@@ -604,7 +607,9 @@ def test_native_reducer_two_ranks_one_gpu(cuda, layer, comm, accum, impl):
            "--accum", str(accum), "--impl", impl]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=110,
                        env=dict(os.environ, PYTHONPATH=root, OMP_NUM_THREADS="4"))
-    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    if r.returncode != 0:  # the launcher's banner hides the worker's error at the end of stderr
+        keep = [ln for ln in r.stderr.splitlines() if "Error" in ln or "assert" in ln or ln.startswith("  File")]
+        pytest.fail("worker failed:\n" + r.stdout[-2000:] + "\n" + "\n".join(keep[-40:]))
     assert r.stdout.count("OK") == 2, r.stdout
 
 
