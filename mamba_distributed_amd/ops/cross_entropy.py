@@ -18,7 +18,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _ext, grad_accum
-from .linear import _proj_engine, mm_nt
+from .linear import _pk_wins, mm_nt
 
 
 def _inv_count(targets, ignore_index):
@@ -79,7 +79,8 @@ class _FusedLinearCEFn(torch.autograd.Function):
         dh = dw = None
         if ctx.needs_input_grad[0]:
             # dh = dlogits W: a K-contiguous product against W^T (cached once per optimizer step)
-            wt = grad_accum.cached_transpose(ctx.param, w.dtype) if _proj_engine() != "lib" else None
+            wt = (grad_accum.cached_transpose(ctx.param, w.dtype)
+                  if _pk_wins(dlogits.shape[0], w.shape[1], w.shape[0]) else None)
             dh = (mm_nt(dlogits, wt) if wt is not None else torch.mm(dlogits, w)).mul_(g).view(ctx.hshape).to(ctx.hdtype)
         if ctx.needs_input_grad[1]:
             dw = torch.mm(dlogits.t(), h2).to(ctx.wdtype).mul_(g)

@@ -68,10 +68,21 @@ def _wgrad_native(p, dy2: torch.Tensor, x2: torch.Tensor, lb: int = 1):
 
 
 def _proj_engine() -> str:
-    """Forward / input-gradient projection GEMM: "pk" (the persistent native engine, gemm_pk_k) or "lib"
-    (hipBLASLt).  MAMBA_AMD_PROJ_GEMM selects (A/B)."""
+    """Forward / input-gradient projection GEMM: "pk" (the persistent native engine, gemm_pk_k, for every shape
+    it takes), "auto" (pk only for the short-K shapes where it measured faster than the library) or "lib"
+    (hipBLASLt).  MAMBA_AMD_PROJ_GEMM selects."""
     import os
     return os.environ.get("MAMBA_AMD_PROJ_GEMM", "lib")
+
+
+def _pk_wins(m: int, n_out: int, k: int) -> bool:
+    """Engine choice for an (m, n_out, k) product.  Isolated timings at the 280M shapes
+    (profiles/r3/pk*_vs_hipblaslt.log): pk wins at K = 768 with moderate outputs (in_proj fwd 143 vs 166 us,
+    out_proj dgrad 61 vs 66 us) and loses at K >= 1536 and on the 50k-wide lm_head."""
+    e = _proj_engine()
+    if e == "lib":
+        return False
+    return e == "pk" or (k <= 1024 and m * n_out <= (1 << 28))
 
 
 def _pk_ok(a2: torch.Tensor, n_out: int, k: int) -> bool:
@@ -79,7 +90,7 @@ def _pk_ok(a2: torch.Tensor, n_out: int, k: int) -> bool:
     k-contiguous (n_out, k) weight image (csrc/kernels/gemm_pipe.hip)."""
     return (a2.is_cuda and a2.dtype == torch.bfloat16 and a2.dim() == 2 and a2.stride(-1) == 1
             and a2.stride(0) % 8 == 0 and a2.data_ptr() % 16 == 0 and a2.shape[0] >= 4096 and k > 192
-            and k % 8 == 0 and n_out % 8 == 0 and _proj_engine() != "lib")
+            and k % 8 == 0 and n_out % 8 == 0 and _pk_wins(a2.shape[0], n_out, k))
 
 
 def _pk_mm(a2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
@@ -93,7 +104,8 @@ def mm_nt(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     ok = (a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.dim() == 2 and b.dim() == 2
           and a.stride(-1) == 1 and b.stride(-1) == 1 and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0
           and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0 and a.shape[1] > 192 and a.shape[1] % 8 == 0
-          and b.shape[0] % 8 == 0 and a.shape[0] * b.shape[0] >= (1 << 24) and _proj_engine() != "lib")
+          and b.shape[0] % 8 == 0 and a.shape[0] * b.shape[0] >= (1 << 24)
+          and _pk_wins(a.shape[0], b.shape[0], a.shape[1]))
     return _pk_mm(a, b) if ok else torch.mm(a, b.t())
 
 

@@ -76,8 +76,10 @@ def zero_grad(model, optimizer) -> None:
     r = _reducer(model)
     if r is not None:
         r.zero_grad()
-    else:
+    elif optimizer is not None:
         optimizer.zero_grad(set_to_none=True)
+    else:
+        model.zero_grad(set_to_none=True)
 
 
 def set_grad_sync(model, enabled: bool):
