@@ -544,9 +544,14 @@ std::vector<Tensor> ssd_bwd(Tensor dy, Tensor x, Tensor dt, Tensor A, Tensor Bm,
   a.sddtb = ddt.stride(0); a.sddtl = ddt.stride(1); a.sddth = ddt.stride(2);
   a.dB = (mamba_amd::bf16_t*)dB.data_ptr(); a.sdBb = dB.stride(0); a.sdBl = dB.stride(1); a.sdBg = dB.stride(2);
   a.dC = (mamba_amd::bf16_t*)dC.data_ptr(); a.sdCb = dC.stride(0); a.sdCl = dC.stride(1); a.sdCg = dC.stride(2);
-  auto part_dcb = at::empty({a.B, a.nc, a.nhg, 64, 64}, fo);
-  auto part_db = at::empty({a.B, a.nc, a.nhg, 64, a.N}, fo);
-  auto part_dc = at::empty({a.B, a.nc, a.nhg, 64, a.N}, fo);
+  // one head group per B/C group: the chunk kernel finishes dB / dC itself (no head-group partials)
+  a.fuse_dbc = std::getenv("MAMBA_AMD_SSD_FUSE_DBC") ? std::atoi(std::getenv("MAMBA_AMD_SSD_FUSE_DBC")) != 0 &&
+                                                         a.HG == a.H / a.G
+                                                     : a.HG == a.H / a.G;
+  const int64_t pn = a.fuse_dbc ? 0 : 1;
+  auto part_dcb = at::empty({pn * a.B, a.nc, a.nhg, 64, 64}, fo);
+  auto part_db = at::empty({pn * a.B, a.nc, a.nhg, 64, a.N}, fo);
+  auto part_dc = at::empty({pn * a.B, a.nc, a.nhg, 64, a.N}, fo);
   const PartMode pm = part_mode(part_mode_);
   Tensor part_small = part_tensor(part_buf, part_mode_, {a.B * a.nc, 3, a.H}, x.options());
   a.pacc = pm.pacc;
@@ -622,7 +627,8 @@ std::tuple<Tensor, Tensor, Tensor> selscan_fwd(Tensor u, Tensor delta, Tensor A,
 std::vector<Tensor> selscan_bwd_impl(Tensor dout, Tensor u, Tensor delta, Tensor A, Tensor Bm, Tensor Cm,
                                      optional<Tensor> D, optional<Tensor> z, optional<Tensor> delta_bias, Tensor carries,
                                      bool softplus, optional<Tensor> dz_out, optional<Tensor> dB_out,
-                                     optional<Tensor> dC_out) {
+                                     optional<Tensor> dC_out, optional<Tensor> part_buf = c10::nullopt,
+                                     int64_t part_mode_ = 0) {
   check_cuda(u, "u");
   at::hip::HIPGuardMasqueradingAsCUDA guard(u.device());
   mamba_amd::SelScanArgs a{};
@@ -666,14 +672,30 @@ std::vector<Tensor> selscan_bwd_impl(Tensor dout, Tensor u, Tensor delta, Tensor
   const int ndg = (a.D + a.Kc - 1) / a.Kc;
   auto part_bc = at::empty({2, a.B, ndg, a.N, a.L}, fo);
   a.part_dB = part_bc[0].data_ptr<float>(); a.part_dC = part_bc[1].data_ptr<float>();
-  auto part_dA = at::zeros({a.B, a.D, a.N}, fo);
-  auto part_dd = at::zeros({2, a.B, a.D}, fo);
-  a.part_dA = part_dA.data_ptr<float>(); a.part_dD = part_dd[0].data_ptr<float>(); a.part_dbias = part_dd[1].data_ptr<float>();
+  // A / D / delta_bias gradient partials: one flat fp32 buffer [dA (B, D, N) | dD (B, D) | dbias (B, D)].
+  // part_mode (ops/grad_accum.py::deferred): 0 transient, reduced now; 1 / 2 store / add into the persistent
+  // buffer, no reduction (empty dA / dD / dbias); 3 / 4 store / add, then reduce over the batch.
+  const PartMode pm = part_mode(part_mode_);
+  const int64_t nA = (int64_t)a.B * a.D * a.N, nd = (int64_t)a.B * a.D;
+  const bool direct = part_mode_ > 0 && mamba_amd::selscan_bwd_sequential(a);  // kernel writes the buffer itself
+  Tensor pb = direct ? part_tensor(part_buf, part_mode_, {nA + 2 * nd}, u.options()) : at::zeros({nA + 2 * nd}, fo);
+  a.part_dA = pb.data_ptr<float>(); a.part_dD = a.part_dA + nA; a.part_dbias = a.part_dD + nd;
+  a.pacc = direct && pm.pacc;
   HIPCHK(mamba_amd::launch_selscan_bwd(a, cur_stream()));
-  Tensor dA = part_dA.sum(0).to(A.scalar_type());
-  auto s2 = part_dd.sum(1);
-  Tensor dD = D.has_value() && D->defined() ? s2[0].to(D->scalar_type()) : at::empty({0}, fo);
-  Tensor dbias = delta_bias.has_value() && delta_bias->defined() ? s2[1].to(delta_bias->scalar_type()) : at::empty({0}, fo);
+  if (part_mode_ > 0 && !direct) {  // time-parallel kernels accumulate into zeroed partials: fold them in here
+    Tensor dst = part_tensor(part_buf, part_mode_, {nA + 2 * nd}, u.options());
+    if (pm.pacc) dst.add_(pb); else dst.copy_(pb);
+    pb = dst;
+  }
+  Tensor dA, dD, dbias;
+  if (pm.reduce) {
+    dA = pb.narrow(0, 0, nA).view({a.B, a.D, a.N}).sum(0).to(A.scalar_type());
+    auto s2 = pb.narrow(0, nA, 2 * nd).view({2, a.B, a.D}).sum(1);
+    dD = D.has_value() && D->defined() ? s2[0].to(D->scalar_type()) : at::empty({0}, fo);
+    dbias = delta_bias.has_value() && delta_bias->defined() ? s2[1].to(delta_bias->scalar_type()) : at::empty({0}, fo);
+  } else {
+    dA = at::empty({0}, fo); dD = at::empty({0}, fo); dbias = at::empty({0}, fo);
+  }
   if (!dz.defined()) dz = at::empty({0}, u.options());
   return {du, ddelta, dA, dB, dC, dD, dz, dbias};
 }
@@ -686,8 +708,10 @@ std::vector<Tensor> selscan_bwd(Tensor dout, Tensor u, Tensor delta, Tensor A, T
 
 std::vector<Tensor> selscan_bwd_into(Tensor dout, Tensor u, Tensor delta, Tensor A, Tensor Bm, Tensor Cm,
                                      optional<Tensor> D, optional<Tensor> z, optional<Tensor> delta_bias, Tensor carries,
-                                     bool softplus, Tensor dz_out, Tensor dB_out, Tensor dC_out) {
-  return selscan_bwd_impl(dout, u, delta, A, Bm, Cm, D, z, delta_bias, carries, softplus, dz_out, dB_out, dC_out);
+                                     bool softplus, Tensor dz_out, Tensor dB_out, Tensor dC_out,
+                                     optional<Tensor> part_buf, int64_t part_mode) {
+  return selscan_bwd_impl(dout, u, delta, A, Bm, Cm, D, z, delta_bias, carries, softplus, dz_out, dB_out, dC_out,
+                          part_buf, part_mode);
 }
 
 // decode-time recurrent update; Mamba-1: state (b,d,n), x/dt/z (b,d), A (d,n), B/C (b,n), D (d)
@@ -798,7 +822,8 @@ Tensor gemm_wgrad(Tensor dY, Tensor X, optional<Tensor> out, bool accumulate) {
 
 // dW (fp32, (P, Q)) (+)= dY^T X over M tokens where either operand may be CHANNEL-major:
 //   dy_cm: dY given as (P, M) (else (M, P));  x_cm: X given as (Q, M) (else (M, Q)).  At least one is.
-Tensor gemm_wgrad_cm(Tensor dY, Tensor X, optional<Tensor> out, bool accumulate, bool dy_cm, bool x_cm) {
+Tensor gemm_wgrad_cm(Tensor dY, Tensor X, optional<Tensor> out, bool accumulate, bool dy_cm, bool x_cm,
+                     optional<Tensor> part_buf, int64_t part_mode_) {
   check_cuda(dY, "dY");
   at::hip::HIPGuardMasqueradingAsCUDA guard(dY.device());
   TORCH_CHECK(dy_cm || x_cm, "gemm_wgrad_cm: use gemm_wgrad for two token-major operands");
@@ -816,10 +841,14 @@ Tensor gemm_wgrad_cm(Tensor dY, Tensor X, optional<Tensor> out, bool accumulate,
               "gemm_wgrad_cm: out must be contiguous fp32 (P,Q)");
   TORCH_CHECK(!accumulate || (out.has_value() && out->defined()), "gemm_wgrad_cm: accumulate needs out");
   const int S = mamba_amd::gemm_wgrad_splits((int)M, (int)P, (int)Q);
-  auto part = at::empty({S, P, Q}, dY.options().dtype(at::kFloat));
+  // part_mode (ops/grad_accum.py::deferred): 0 transient slabs reduced now; 1 / 2 store / add into the
+  // persistent slabs, no reduction (returns an empty tensor); 3 / 4 store / add, then reduce into C
+  const PartMode pm = part_mode(part_mode_);
+  Tensor part = part_tensor(part_buf, part_mode_, {S, P, Q}, dY.options());
+  if (!pm.reduce) C = at::empty({0}, dY.options().dtype(at::kFloat));
   HIPCHK(mamba_amd::launch_gemm_wgrad_cm(dY.data_ptr(), dY.stride(0), X.data_ptr(), X.stride(0), part.data_ptr<float>(),
-                                         C.data_ptr<float>(), (int)M, (int)P, (int)Q, accumulate, dy_cm, x_cm,
-                                         cur_stream()));
+                                         pm.reduce ? C.data_ptr<float>() : nullptr, (int)M, (int)P, (int)Q, accumulate,
+                                         dy_cm, x_cm, cur_stream(), pm.pacc, pm.reduce));
   return C;
 }
 
@@ -835,7 +864,6 @@ Tensor gp_mm(Tensor A, Tensor B, optional<Tensor> out, int64_t la, int64_t lb, i
   TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "gp_mm: bf16 operands");
   TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1, "gp_mm: unit inner strides");
   TORCH_CHECK((la == 0 || la == 1) && (lb == 0 || lb == 1) && mode >= 0 && mode <= 2 && splits >= 1, "gp_mm: args");
-  TORCH_CHECK(!(la == 1 && lb == 0 && mode == 0), "gp_mm: (la, lb) = (1, 0) is instantiated for fp32 output only");
   const int64_t M = la == 0 ? A.size(0) : A.size(1), K = la == 0 ? A.size(1) : A.size(0);
   const int64_t N = lb == 0 ? B.size(0) : B.size(1), KB = lb == 0 ? B.size(1) : B.size(0);
   TORCH_CHECK(K == KB, "gp_mm: contraction sizes differ (", K, " vs ", KB, ")");
@@ -910,6 +938,7 @@ Tensor gp_pk(Tensor A, Tensor B, optional<Tensor> out, int64_t la, int64_t lb, i
   return C;
 }
 
+int64_t wgrad_splits(int64_t M, int64_t P, int64_t Q) { return mamba_amd::gemm_wgrad_splits((int)M, (int)P, (int)Q); }
 int64_t gp_splits(int64_t M, int64_t N, int64_t K) { return mamba_amd::gemm_pipe_splits((int)M, (int)N, (int)K); }
 
 
@@ -1038,12 +1067,13 @@ TORCH_LIBRARY(mamba_amd, m) {
   m.def("selscan_bwd(Tensor dout, Tensor u, Tensor delta, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? z, "
         "Tensor? delta_bias, Tensor carries, bool softplus) -> Tensor[]");
   m.def("selscan_bwd_into(Tensor dout, Tensor u, Tensor delta, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? z, "
-        "Tensor? delta_bias, Tensor carries, bool softplus, Tensor(a!) dz_out, Tensor(b!) dB_out, Tensor(c!) dC_out) "
-        "-> Tensor[]");
+        "Tensor? delta_bias, Tensor carries, bool softplus, Tensor(a!) dz_out, Tensor(b!) dB_out, Tensor(c!) dC_out, "
+        "Tensor(z!)? part_buf=None, int part_mode=0) -> Tensor[]");
   m.def("gemm_tn(Tensor A, Tensor B, Tensor(a!)? out=None) -> Tensor");
   m.def("gemm_wgrad(Tensor dY, Tensor X, Tensor(a!)? out=None, bool accumulate=False) -> Tensor");
   m.def("gemm_wgrad_cm(Tensor dY, Tensor X, Tensor(a!)? out=None, bool accumulate=False, bool dy_cm=True, "
-        "bool x_cm=False) -> Tensor");
+        "bool x_cm=False, Tensor(z!)? part_buf=None, int part_mode=0) -> Tensor");
+  m.def("wgrad_splits(int M, int P, int Q) -> int", &wgrad_splits);
   m.def("gp_mm(Tensor A, Tensor B, Tensor(a!)? out=None, int la=0, int lb=0, int mode=0, int splits=1, int bm=256) -> Tensor");
   m.def("gp_pk(Tensor A, Tensor B, Tensor(a!)? out=None, int la=0, int lb=0, int mode=0, Tensor? rowscale=None) -> Tensor");
   m.def("gp_splits(int M, int N, int K) -> int", &gp_splits);

@@ -152,7 +152,8 @@ struct WStage {  // one 64 x 128 bf16 tile = 1024 16-B chunks, 4 per thread
 
 __global__ __launch_bounds__(256) void gemm_wgrad_k(const bf16_t* __restrict__ dY, int64_t ldy,
                                                     const bf16_t* __restrict__ X, int64_t ldx,
-                                                    float* __restrict__ part, int M, int P, int Q, int mslice) {
+                                                    float* __restrict__ part, int M, int P, int Q, int mslice,
+                                                    bool pacc = false) {
   __shared__ __attribute__((aligned(16))) bf16_t As[2][WK * WLD];
   __shared__ __attribute__((aligned(16))) bf16_t Bs[2][WK * WLD];
   const int tq = (Q + WB - 1) / WB, tp = (P + WB - 1) / WB;
@@ -207,7 +208,10 @@ __global__ __launch_bounds__(256) void gemm_wgrad_k(const bf16_t* __restrict__ d
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int p = p0 + wp * 64 + 16 * i + 4 * (l >> 4) + r, q = q0 + wq * 64 + 16 * j + (l & 15);
-        if (p < P && q < Q) pc[(int64_t)p * Q + q] = acc[i][j][r];
+        if (p < P && q < Q) {
+          float* d = pc + (int64_t)p * Q + q;
+          *d = pacc ? *d + acc[i][j][r] : acc[i][j][r];  // pacc: add into persistent slabs (deferred reduce)
+        }
       }
 }
 
@@ -243,7 +247,8 @@ __device__ __forceinline__ bf16x8 wfrag(const char* lds, int k0, int c0) {
 template <int TP, int TQ, bool CM, bool CMB = false>
 __global__ __launch_bounds__(512) void gemm_wgrad_big_k(const bf16_t* __restrict__ dY, int64_t ldy,
                                                         const bf16_t* __restrict__ X, int64_t ldx,
-                                                        float* __restrict__ part, int M, int P, int Q, int mslice) {
+                                                        float* __restrict__ part, int M, int P, int Q, int mslice,
+                                                        bool pacc = false) {
   constexpr int HB = WK * WB * 2;            // one [64][128] half-tile: 16 KB
   constexpr int AB = (TP / WB) * HB, BB = (TQ / WB) * HB;
   constexpr int WQN = 4, WPN = 2;            // wave grid
@@ -343,7 +348,10 @@ __global__ __launch_bounds__(512) void gemm_wgrad_big_k(const bf16_t* __restrict
       for (int r = 0; r < 4; ++r) {
         const int p = p0 + wp * (TP / WPN) + 16 * i + 4 * (l >> 4) + r;
         const int q = q0 + wq * (TQ / WQN) + 16 * j + (l & 15);
-        if (p < P && q < Q) pc[(int64_t)p * Q + q] = acc[i][j][r];
+        if (p < P && q < Q) {
+          float* d = pc + (int64_t)p * Q + q;
+          *d = pacc ? *d + acc[i][j][r] : acc[i][j][r];  // pacc: add into persistent slabs (deferred reduce)
+        }
       }
 }
 
@@ -529,27 +537,31 @@ hipError_t launch_gemm_skinny(const void* A, int64_t lda, const void* B, int64_t
   return hipGetLastError();
 }
 
-// dW (P, Q) (+)= dY X with a channel-major dY (P, M) (Mamba-1 d(xz)) and token-major X (M, Q)
+// dW (P, Q) (+)= dY X with a channel-major dY (P, M) (Mamba-1 d(xz)) and token-major X (M, Q).
+// pacc: the split-K slabs in `part` are added into (they persist across the micro-steps of an optimizer
+// step); reduce: sum the slabs into `out` (else the slabs are left for a later micro-step).
 bool gemm_wgrad_cm_supported(int M, int P, int Q, int64_t ldy, int64_t ldx) {
   return M % WK == 0 && P % 8 == 0 && Q % 8 == 0 && ldy % 8 == 0 && ldx % 8 == 0 && P >= 8 && Q >= 8;
 }
 
 hipError_t launch_gemm_wgrad_cm(const void* dY, int64_t ldy, const void* X, int64_t ldx, float* part, float* out,
-                                int M, int P, int Q, bool accumulate, bool dy_cm, bool x_cm, hipStream_t st) {
+                                int M, int P, int Q, bool accumulate, bool dy_cm, bool x_cm, hipStream_t st,
+                                bool pacc, bool reduce) {
   if (!gemm_wgrad_cm_supported(M, P, Q, ldy, ldx) || (!dy_cm && !x_cm)) return hipErrorInvalidValue;
   const int S = wgrad_splits(M, P, Q, true);
   const int mslice = ((M + S - 1) / S + WK - 1) / WK * WK;
   const int tiles = ((P + BT - 1) / BT) * ((Q + BT - 1) / BT);
   if (dy_cm && x_cm)
     hipLaunchKernelGGL((gemm_wgrad_big_k<BT, BT, true, true>), dim3(tiles * S), dim3(512), 0, st, (const bf16_t*)dY,
-                       ldy, (const bf16_t*)X, ldx, part, M, P, Q, mslice);
+                       ldy, (const bf16_t*)X, ldx, part, M, P, Q, mslice, pacc);
   else if (dy_cm)
     hipLaunchKernelGGL((gemm_wgrad_big_k<BT, BT, true, false>), dim3(tiles * S), dim3(512), 0, st, (const bf16_t*)dY,
-                       ldy, (const bf16_t*)X, ldx, part, M, P, Q, mslice);
+                       ldy, (const bf16_t*)X, ldx, part, M, P, Q, mslice, pacc);
   else
     hipLaunchKernelGGL((gemm_wgrad_big_k<BT, BT, false, true>), dim3(tiles * S), dim3(512), 0, st, (const bf16_t*)dY,
-                       ldy, (const bf16_t*)X, ldx, part, M, P, Q, mslice);
+                       ldy, (const bf16_t*)X, ldx, part, M, P, Q, mslice, pacc);
   MAMBA_HIP_CHECK(hipGetLastError());
+  if (!reduce) return hipSuccess;
   const int64_t n = (int64_t)P * Q;
   hipLaunchKernelGGL(wgrad_reduce_k, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, st, part, S, n, out,
                      accumulate);

@@ -618,7 +618,7 @@ hipError_t launch_gemm_pipe(int la, int lb, const void* A, int64_t lda, const vo
   if (la == 0 && lb == 0) { GP_EPI(0, 0) }
   else if (la == 0 && lb == 1) { GP_EPI(0, 1) }
   else if (la == 1 && lb == 1) { GP_EPI(1, 1) }
-  else if (la == 1 && lb == 0 && epi != 0) { GP_EPI(1, 0) }  // the Mamba-1 out_proj weight gradient
+  else if (la == 1 && lb == 0) { GP_EPI(1, 0) }  // the Mamba-1 out_proj: forward (bf16) and weight gradient
   else return hipErrorInvalidValue;
 #undef GP_EPI
   return hipGetLastError();

@@ -89,7 +89,8 @@ hipError_t launch_gemm_tn_bf16(const void* A, int64_t lda, const void* B, int64_
 int gemm_wgrad_splits(int M, int P, int Q);
 bool gemm_wgrad_cm_supported(int M, int P, int Q, int64_t ldy, int64_t ldx);
 hipError_t launch_gemm_wgrad_cm(const void* dY, int64_t ldy, const void* X, int64_t ldx, float* part, float* out,
-                                int M, int P, int Q, bool accumulate, bool dy_cm, bool x_cm, hipStream_t st);
+                                int M, int P, int Q, bool accumulate, bool dy_cm, bool x_cm, hipStream_t st,
+                                bool pacc = false, bool reduce = true);
 hipError_t launch_gemm_wgrad(const void* dY, int64_t ldy, const void* X, int64_t ldx, float* part, float* out,
                              int M, int P, int Q, bool accumulate, hipStream_t st);
 

@@ -33,6 +33,7 @@ struct SelScanArgs {
   float* part_dB; float* part_dC;                   // (B, ndg, N, L)
   float* part_dA;                                   // (B, D, N)   zero-initialised
   float* part_dD; float* part_dbias;                // (B, D)      zero-initialised
+  bool pacc;  // sequential backward only: add into part_dA / part_dD / part_dbias (deferred reduction)
 };
 
 struct SSMUpdateArgs {
@@ -54,6 +55,7 @@ hipError_t launch_selscan_bwd(const SelScanArgs& a, hipStream_t st);
 int selscan_carry_t(const SelScanArgs& a);
 // channels per backward workgroup (SelScanArgs::Kc; sizes the dB / dC partials); needs carry_t set
 int selscan_bwd_kc(const SelScanArgs& a);
+bool selscan_bwd_sequential(const SelScanArgs& a);  // the wave-per-state-group kernel runs (supports pacc)
 hipError_t launch_ssm_update(const SSMUpdateArgs& a, hipStream_t st);
 
 }  // namespace mamba_amd

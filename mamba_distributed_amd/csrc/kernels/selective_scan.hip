@@ -1317,16 +1317,24 @@ __global__ __launch_bounds__(256) void selscan_bwd_sg_k(SelScanArgs a) {
       if (dzb) *reinterpret_cast<unsigned*>(dzb + t + sr * (int)a.sdzd + 2 * sp) = pack2(o_dz[0], o_dz[1]);
     }
   }
-  *reinterpret_cast<float4*>(a.part_dA + ((int64_t)b * a.D + d) * N + 4 * w) =
-      make_float4(dA[0].x, dA[0].y, dA[1].x, dA[1].y);
+  {
+    float4* pa = reinterpret_cast<float4*>(a.part_dA + ((int64_t)b * a.D + d) * N + 4 * w);
+    float4 v = make_float4(dA[0].x, dA[0].y, dA[1].x, dA[1].y);
+    if (a.pacc) {
+      const float4 o = *pa;
+      v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+    }
+    *pa = v;
+  }
   // dD / ddelta_bias: the 4 threads of a channel are one quad
   dDp += dppf<0xB1>(0.f, dDp);
   dDp += dppf<0x4E>(0.f, dDp);
   dbp += dppf<0xB1>(0.f, dbp);
   dbp += dppf<0x4E>(0.f, dbp);
   if (sp == 0) {
-    a.part_dD[(int64_t)b * a.D + d0 + sr] = dDp;
-    a.part_dbias[(int64_t)b * a.D + d0 + sr] = dbp;
+    const int64_t o = (int64_t)b * a.D + d0 + sr;
+    a.part_dD[o] = a.pacc ? a.part_dD[o] + dDp : dDp;
+    a.part_dbias[o] = a.pacc ? a.part_dbias[o] + dbp : dbp;
   }
 }
 
@@ -1391,6 +1399,7 @@ static bool use_bwd_sg(const SelScanArgs& a) {
   return a.carry_t == SGB_T && sg_shape_ok(a) && a.vecg && a.L % SGB_T == 0 && a.nct == a.L / SGB_T && off32;
 }
 int selscan_bwd_kc(const SelScanArgs& a) { return use_bwd_sg(a) ? 64 : SB_KC; }
+bool selscan_bwd_sequential(const SelScanArgs& a) { return use_bwd_sg(a); }
 
 hipError_t launch_selscan_fwd(const SelScanArgs& a, hipStream_t st) {
   const int64_t rows = (int64_t)a.B * a.D;
@@ -1411,6 +1420,7 @@ hipError_t launch_selscan_bwd(const SelScanArgs& a, hipStream_t st) {
   if (a.Kc != selscan_bwd_kc(a) || (a.carry_t != SGB_T && a.carry_t != SB_T) ||
       a.nct != (a.L + a.carry_t - 1) / a.carry_t)
     return hipErrorInvalidValue;
+  if (a.pacc && !use_bwd_sg(a)) return hipErrorInvalidValue;  // only the sequential kernel adds into partials
   if (use_bwd_sg(a)) {
     hipLaunchKernelGGL(selscan_bwd_sg_k, dim3((unsigned)(a.B * (a.D / 64))), dim3(256), 0, st, a);
   } else {

@@ -33,6 +33,7 @@ struct SSDArgs {
   void* ddt; int ddt_dtype; int64_t sddtb, sddtl, sddth;
   bf16_t* dB; int64_t sdBb, sdBl, sdBg;
   bf16_t* dC; int64_t sdCb, sdCl, sdCg;
+  bool fuse_dbc;          // HG == H / G: ssd_chunk_bwd finishes dB / dC itself (no partials, no ssd_dbc_bwd)
   float* part_dcb;        // (b, nc, nhg, 64, 64)
   float* part_db;         // (b, nc, nhg, 64, N)
   float* part_dc;         // (b, nc, nhg, 64, N)

@@ -671,6 +671,45 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
     }
     if ((hh & 7) == 7 || hh == a.HG - 1) flush(hh & ~7, (hh & 7) + 1);
   }
+  if (a.fuse_dbc) {
+    // ---- this workgroup holds every head of group g (HG == H / G): finish dC = dC_off + dCB B and
+    // dB = dB_off + dCB^T C here (ssd_dbc_bwd's math in the same order, so bitwise the same result) instead of
+    // writing the head-group partials and re-reading them in a fourth kernel.  dCB goes to LDS as bf16 [i][j]
+    // in MsT (all 16 tiles: the 10 owned ones and the 6 zero ones), dC / dB are staged in Ss / dSs.
+    __syncthreads();  // every wave is done with MsT / Ss / dSs and the last flush
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if (k < own) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) MsT[(16 * tI[k] + 4 * lg + r) * LD64 + 16 * tJ[k] + li] = f2bf(dcbo[k][r]);
+      }
+    }
+    if (wid >= 2) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) MsT[(16 * zI + 4 * lg + r) * LD64 + 16 * zJ + li] = f2bf(0.f);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < Q / 32; ++ks) {
+      const bf16x8 Ac = frag_kc(MsT, LD64, 16 * w, 32 * ks);  // dCB rows i, k = j
+      const bf16x8 Ab = frag_tr(MsT, LD64, 32 * ks, 16 * w);  // dCB^T rows j, k = i
+#pragma unroll
+      for (int nt = 0; nt < NTH; ++nt) {
+        const int n0 = 16 * (half * NTH + nt);
+        dCa[nt] = mfma16(Ac, frag_tr(Bs, LDN, 32 * ks, n0), dCa[nt]);
+        dBa[nt] = mfma16(Ab, frag_tr(Cs, LDN, 32 * ks, n0), dBa[nt]);
+      }
+    }
+#pragma unroll
+    for (int nt = 0; nt < NTH; ++nt) {
+      acc_to_lds(Ss, LDN, 16 * w, 16 * (half * NTH + nt), dCa[nt]);
+      acc_to_lds(dSs, LDN, 16 * w, 16 * (half * NTH + nt), dBa[nt]);
+    }
+    __syncthreads();
+    store_tile<Q, N>(a.dC + (int64_t)b * a.sdCb + (int64_t)c * Q * a.sdCl + (int64_t)g * a.sdCg, a.sdCl, Ss, LDN, valid);
+    store_tile<Q, N>(a.dB + (int64_t)b * a.sdBb + (int64_t)c * Q * a.sdBl + (int64_t)g * a.sdBg, a.sdBl, dSs, LDN, valid);
+    return;
+  }
   // ---- head-group partials
   const int64_t pbase = ((int64_t)b * a.nc + c) * a.nhg + hgi;
 #pragma unroll
@@ -834,8 +873,10 @@ hipError_t launch_ssd_fwd(const SSDArgs& a, hipStream_t st) {
 hipError_t launch_ssd_bwd(const SSDArgs& a, hipStream_t st) {
   N_SWITCH(a.N, hipLaunchKernelGGL(ssd_dstate_bwd_k<NN>, dim3(a.H, a.B), dim3(256), 0, st, a));
   MAMBA_HIP_CHECK(hipGetLastError());
+  if (a.fuse_dbc && a.HG != a.H / a.G) return hipErrorInvalidValue;  // the fused finish needs the whole group
   N_SWITCH(a.N, hipLaunchKernelGGL(ssd_chunk_bwd_k<NN>, dim3(a.nc, a.nhg, a.B), dim3(512), 0, st, a));
   MAMBA_HIP_CHECK(hipGetLastError());
+  if (a.fuse_dbc) return hipSuccess;
   N_SWITCH(a.N, hipLaunchKernelGGL(ssd_dbc_bwd_k<NN>, dim3(a.nc, a.G, a.B), dim3(256), 0, st, a));
   return hipGetLastError();
 }

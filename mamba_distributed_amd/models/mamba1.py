@@ -44,6 +44,7 @@ def _flat(t: torch.Tensor) -> torch.Tensor:
 _NATIVE_XDT = os.environ.get("MAMBA_AMD_M1_NATIVE_XDT", "1") != "0"  # A/B switch: x_proj / dt_proj dW
 _NATIVE_INPROJ = os.environ.get("MAMBA_AMD_M1_NATIVE_INPROJ", "1") != "0"  # A/B switch
 _SKINNY = os.environ.get("MAMBA_AMD_SKINNY", "1") != "0"  # A/B switch: 0 = hipBLASLt for the skinny GEMMs
+_OUTPROJ_PIPE = os.environ.get("MAMBA_AMD_M1_OUTPROJ_PIPE", "1") != "0"  # A/B switch: 0 = hipBLASLt out_proj fwd
 
 
 def _mm_cm(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None, accumulate: bool = False):
@@ -137,10 +138,13 @@ def _wgrad_native(p, dY, X, dy_cm, x_cm):
 
 
 def _wgrad_native_cm(p, dY, X, dy_cm, x_cm):
-    """Default Mamba-1 weight gradient: gemm_wgrad_cm, reduced every micro-step (added in place into
-    ``p.grad`` on the no-sync micro-steps).  The deferred-slab alternative measured 0.7% slower on the
-    whole Mamba-1 280M step (180.0k vs 181.2k tok/s, profiles/r2_v5_ab_m1_defer_wgrad.txt): the skinny
-    x_proj / dt_proj products (Q = 48, P = 80) suit gemm_wgrad_cm's tiles better than the 256x256 engine."""
+    """Default Mamba-1 weight gradient: gemm_wgrad_cm (csrc/kernels/gemm.hip), whose fp32 split-K slabs persist
+    across the micro-steps of an optimizer step inside an accumulation scope (ops/grad_accum.deferred): the
+    no-sync micro-steps add into them on the weight-gradient side stream and return nothing, and the slab sum
+    (wgrad_reduce_k) runs once, on the sync micro-step.  Outside a scope (or MAMBA_AMD_DEFER_REDUCE=0) the slabs
+    are reduced every micro-step and added in place into ``p.grad`` on the no-sync micro-steps.  The 256x256
+    pipelined engine (``_wgrad_native``'s gp_mm form) measured 0.7% slower here: the skinny x_proj / dt_proj
+    products (Q = 48, P = 80) suit gemm_wgrad_cm's tiles better."""
     M = dY.shape[1] if dy_cm else dY.shape[0]
     ok = (dY.dtype == torch.bfloat16 and X.dtype == torch.bfloat16 and dY.stride(1) == 1 and X.stride(1) == 1
           and M % 64 == 0 and dY.stride(0) % 8 == 0 and X.stride(0) % 8 == 0 and dY.shape[0] % 8 == 0
@@ -148,6 +152,24 @@ def _wgrad_native_cm(p, dY, X, dy_cm, x_cm):
           and dY.data_ptr() % 16 == 0 and X.data_ptr() % 16 == 0)
     if not ok:
         return False, None
+    P = dY.shape[0] if dy_cm else dY.shape[1]
+    Q = X.shape[0] if x_cm else X.shape[1]
+    ops = _ext.ops()
+    d = grad_accum.deferred(p, "wgrad_cm", (ops.wgrad_splits(M, P, Q), P, Q), dY.device)
+    if d is not None:
+        buf, mode = d
+        if mode <= 2:  # no-sync micro-step: slabs only, beside the rest of the backward
+            side = grad_accum.side_stream(dY.device)
+            if side is None:
+                ops.gemm_wgrad_cm(dY, X, None, False, dy_cm, x_cm, buf, mode)
+            else:
+                side.wait_stream(torch.cuda.current_stream(dY.device))
+                with torch.cuda.stream(side):
+                    ops.gemm_wgrad_cm(dY, X, None, False, dy_cm, x_cm, buf, mode)
+                dY.record_stream(side)
+                X.record_stream(side)
+            return True, None
+        return True, ops.gemm_wgrad_cm(dY, X, None, False, dy_cm, x_cm, buf, mode).to(p.dtype)
     if grad_accum.accumulable(p) and p.grad.dtype == torch.float32 and p.grad.is_contiguous():
         side = grad_accum.side_stream(dY.device)
         if side is None:
@@ -173,6 +195,13 @@ class _OutProjCMFn(torch.autograd.Function):
         w = grad_accum.cached_cast(weight, cd)
         ctx.save_for_backward(y2, w)
         ctx.param = weight
+        T = y2.shape[1]
+        if (_OUTPROJ_PIPE and y2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and y2.stride(1) == 1
+                and y2.stride(0) % 8 == 0 and y2.data_ptr() % 16 == 0 and w.is_contiguous() and T % 8 == 0
+                and w.shape[1] % 8 == 0 and T >= 4096):
+            # y2 is channel-major (di, T): its transpose is the A operand as stored (k-rows of contiguous
+            # tokens) on the pipelined engine; hipBLASLt's transposed-A solution ran 154 us here
+            return _ext.ops().gp_mm(y2, w, None, 1, 0, 0, 1, 256)
         return F.linear(y2.t(), w)
 
     @staticmethod
@@ -224,6 +253,7 @@ class _Mamba1InnerFn(torch.autograd.Function):
         ctx.save_for_backward(xz, w2, conv_b, Wx, Wdt, dt_bias, A, D, conv_out, x_dbl, delta, carries)
         ctx.meta = (b, l, conv_w.shape, W_x.dtype, W_dt.dtype)
         ctx.wparams = (W_x, W_dt)  # the parameters themselves (native weight gradients accumulate into .grad)
+        ctx.pparams = (D, conv_w)  # persistent keys of the deferred partial buffers
         return _flat(y)
 
     @staticmethod
@@ -241,10 +271,18 @@ class _Mamba1InnerFn(torch.autograd.Function):
         Bm = _cm(x_dbl[R:R + N], b, l).unsqueeze(1)
         Cm = _cm(x_dbl[R + N:], b, l).unsqueeze(1)
         dx_dbl = torch.empty_like(x_dbl)
+        # A / D / dt_bias and conv tap / bias partials are reduced once per optimizer step (grad_accum.deferred,
+        # keyed on the persistent D and conv weight parameters): the no-sync micro-steps add into them and return
+        # no gradient for those parameters
+        pD, pconv = ctx.pparams
+        dev = xz.device
+        d_s = grad_accum.deferred(pD, "selscan_small", (b * di * (N + 2),), dev)
+        d_c = grad_accum.deferred(pconv, "conv_cf", (b, di, w2.shape[1] + 1), dev)
         du, ddelta, dA, dB, dC, dD, dz, ddt_bias = ops.selscan_bwd_into(
             _cm(dy2.contiguous() if dy2.stride(-1) != 1 else dy2, b, l), conv_out, _cm(delta, b, l), A,
             Bm, Cm, D, z, dt_bias, carries, True,
-            dxz3[:, di:], _cm(dx_dbl[R:R + N], b, l).unsqueeze(1), _cm(dx_dbl[R + N:], b, l).unsqueeze(1))
+            dxz3[:, di:], _cm(dx_dbl[R:R + N], b, l).unsqueeze(1), _cm(dx_dbl[R + N:], b, l).unsqueeze(1),
+            *(d_s if d_s is not None else (None, 0)))
         dd2 = _flat(ddelta)
         pWx, pWdt = ctx.wparams
         if _NATIVE_XDT:  # both operands channel-major: (di, M) . (R, M)^T on the native wgrad GEMM
@@ -262,8 +300,12 @@ class _Mamba1InnerFn(torch.autograd.Function):
             dWx = torch.mm(dx_dbl, _flat(conv_out).t()).to(wx_dtype)         # (R+2N, di)
         dco2 = _flat(du)
         _mm_cm(Wx.t(), dx_dbl, out=dco2, accumulate=True)                   # du + W_x^T dx_dbl
-        _, dw, db = ops.conv1d_cf_bwd(x, w2, conv_b, _cm(dco2, b, l), True, dxz3[:, :di])
-        return (dxz, dw.reshape(wshape).to(w2.dtype), db.to(conv_b.dtype) if conv_b is not None else None,
+        _, dw, db = ops.conv1d_cf_bwd(x, w2, conv_b, _cm(dco2, b, l), True, dxz3[:, :di],
+                                      *(d_c if d_c is not None else (None, 0)))
+        nz = lambda t: t if t.numel() else None  # noqa: E731  (empty = deferred to the sync micro-step)
+        dw, db, dA, dD, ddt_bias = nz(dw), nz(db), nz(dA), nz(dD), nz(ddt_bias)
+        return (dxz, dw.reshape(wshape).to(w2.dtype) if dw is not None else None,
+                db.to(conv_b.dtype) if (conv_b is not None and db is not None) else None,
                 dWx, dWdt, ddt_bias, dA, dD, None, None, None)
 
 

@@ -33,6 +33,11 @@ def _native_ok(dy: torch.Tensor, x: torch.Tensor) -> bool:
             and dy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0)
 
 
+import os as _os
+
+_WGRAD_DIRECT = _os.environ.get("MAMBA_AMD_WGRAD_DIRECT", "1") != "0"  # A/B: 0 = pipelined-engine slabs
+
+
 def _wgrad_native(p, dy2: torch.Tensor, x2: torch.Tensor, lb: int = 1):
     """dW = dy2^T x2 (fp32) on the native engine; None when deferred to the sync micro-step.  dy2 is token-major
     (T, P); x2 is token-major (T, Q) (lb = 1) or channel-major (Q, T) (lb = 0: the Mamba-1 out_proj input)."""
@@ -41,6 +46,14 @@ def _wgrad_native(p, dy2: torch.Tensor, x2: torch.Tensor, lb: int = 1):
     Q = x2.shape[1] if lb == 1 else x2.shape[0]
     S = ops.gp_splits(P, Q, T)
     d = grad_accum.deferred(p, "wgrad", (S, P, Q), dy2.device)
+    if d is None and lb == 1 and _WGRAD_DIRECT:
+        # not deferred (wide models, MAMBA_AMD_DEFER_REDUCE=0, outside a scope): the split-K wgrad kernel
+        # reduces its slabs itself and, on a no-sync micro-step, adds straight into p.grad (no transient dW,
+        # no queued add)
+        if grad_accum.accumulable(p) and p.grad.dtype == torch.float32 and p.grad.is_contiguous():
+            ops.gemm_wgrad(dy2, x2, p.grad, True)
+            return None
+        return ops.gemm_wgrad(dy2, x2, None, False)
     if d is None:  # outside an accumulation scope: transient slabs, reduce now
         part = ops.gp_mm(dy2, x2, None, 1, lb, 1, S, 256)
         dw = torch.empty(P, Q, device=dy2.device, dtype=torch.float32)

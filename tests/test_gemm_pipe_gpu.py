@@ -31,7 +31,7 @@ def _rel(a, b):
     return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
 
 
-@pytest.mark.parametrize("la,lb", [(0, 0), (0, 1), (1, 1)])
+@pytest.mark.parametrize("la,lb", [(0, 0), (0, 1), (1, 1), (1, 0)])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 768), (300, 264, 200), (1000, 3352, 96),
                                    (768, 520, 1544), (64, 8, 32), (512, 256, 1024)])
 def test_gp_bf16(cuda, la, lb, M, N, K):

@@ -194,6 +194,25 @@ def test_ssd_head_groups(cuda, monkeypatch, hg):
         assert rel(a, b_) < 3e-2, (hg, nm, rel(a, b_))
 
 
+@pytest.mark.parametrize("H,G", [(24, 1), (8, 2)])
+def test_ssd_fused_dbc_bitwise(cuda, monkeypatch, H, G):
+    """One head group per B/C group (HG == H / G, the 280M training shape): ssd_chunk_bwd_k finishes dB / dC
+    itself instead of writing head-group partials for ssd_dbc_bwd_k.  Same math in the same order: every
+    gradient is bitwise the unfused one (MAMBA_AMD_SSD_FUSE_DBC=0)."""
+    from mamba_distributed_amd.ops.ssd import mamba_chunk_scan_combined
+    monkeypatch.setenv("MAMBA_AMD_SSD_HG", str(H // G))
+    x, dt, A, Bm, Cm, D, dt_bias = _ssd_inputs(cuda, 2, 200, H, G, 128, seed=13)
+    grads = {}
+    for fuse in ("0", "1"):
+        monkeypatch.setenv("MAMBA_AMD_SSD_FUSE_DBC", fuse)
+        ins = [t.detach().clone().requires_grad_(True) for t in (x, dt, Bm, Cm)]
+        y = mamba_chunk_scan_combined(ins[0], ins[1], A, ins[2], ins[3], 64, D=D, dt_bias=dt_bias, dt_softplus=True)
+        y.float().square().mean().backward()
+        grads[fuse] = [t.grad for t in ins]
+    for nm, a, b_ in zip(["x", "dt", "B", "C"], grads["1"], grads["0"]):
+        assert torch.equal(a, b_), nm
+
+
 def test_ssd_initial_and_final_states(cuda):
     from mamba_distributed_amd.ops.ssd import mamba_chunk_scan_combined
     x, dt, A, Bm, Cm, D, dt_bias = _ssd_inputs(cuda, 2, 192, 4, 1, 128, seed=5)
