@@ -5,7 +5,8 @@
          --master-port P bench.py --gpus N --steps K --warmup W
 
 Config = BASELINE.json's headline: Mamba-2 280M (d_model 768, 64 layers, vocab 50304), seq 1024,
-micro-batch 32, global batch 524,288 tokens (= 512 sequences; grad-accum 16/N), bf16 autocast,
+global batch 524,288 tokens (= 512 sequences; micro-batch auto: 64 sequences per micro-step for the 280M models,
+grad-accum 8/N), bf16 autocast,
 fused AdamW, grad clip 1.0, data parallel over RCCL (native bucketed reducer; --dp-impl ddp = torch DDP).  Synthetic tokens, random init (no dataset/weights
 on the box).  A "step" is one full optimizer step (all micro-batches + all-reduce + clip + AdamW).
 W untimed warmup steps, then exactly K steps between barrier+synchronize pairs; the MAX elapsed
@@ -50,7 +51,10 @@ def main():
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--model", default="mamba2-280m")
-    p.add_argument("--B", type=int, default=32)
+    p.add_argument("--B", default="auto",
+                   help="micro-batch (sequences); auto: parallel/microbatch.py::auto_micro_batch (64 for the 280M "
+                        "models when a rank has >= 64 sequences per step, else 32) -- the global batch and the "
+                        "gradient are the same for any micro-batch")
     p.add_argument("--T", type=int, default=1024)
     p.add_argument("--global-batch-tokens", type=int, default=524288)
     p.add_argument("--bucket-cap-mb", type=float, default=100.0)
@@ -89,12 +93,17 @@ def main():
         print(f"bench.py: --gpus {a.gpus} but the job has {world} rank(s); refusing to report", file=sys.stderr)
         destroy()
         sys.exit(2)
+    cfg = preset(a.model)
+    assert a.global_batch_tokens % (a.T * world) == 0
+    if str(a.B) == "auto":
+        from mamba_distributed_amd.parallel.microbatch import auto_micro_batch
+        a.B = auto_micro_batch(cfg, a.global_batch_tokens // (a.T * world), a.T)
+    a.B = int(a.B)
     assert a.global_batch_tokens % (a.B * a.T * world) == 0
     accum = a.global_batch_tokens // (a.B * a.T * world)
     from mamba_distributed_amd.utils.gemm_tuning import enable_tuned_gemms
     tuned = False if a.no_tuned_gemms else enable_tuned_gemms()
     torch.manual_seed(1337)
-    cfg = preset(a.model)
     model = LMHeadModel(cfg, device=dev)
     if a.activation_checkpointing:
         model.set_activation_checkpointing(a.activation_checkpointing)
@@ -102,7 +111,7 @@ def main():
     opt = model.configure_optimizers(0.1, 6e-4, "cuda" if dev.startswith("cuda") else "cpu", False)
     loader = SyntheticTokens(a.B, a.T, cfg.vocab_size, info.rank, world, device=dev)
     fused = not a.no_fused_ce
-    overlap = resolve_overlap("off" if a.no_overlap else a.overlap, cfg)
+    overlap = resolve_overlap("off" if a.no_overlap else a.overlap, cfg, a.B * a.T)
 
     on_gpu = dev.startswith("cuda")
 

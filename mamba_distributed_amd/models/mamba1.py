@@ -41,9 +41,6 @@ def _flat(t: torch.Tensor) -> torch.Tensor:
     return t.permute(1, 0, 2).reshape(t.shape[1], -1)
 
 
-_NATIVE_XDT = os.environ.get("MAMBA_AMD_M1_NATIVE_XDT", "1") != "0"  # A/B switch: x_proj / dt_proj dW
-_NATIVE_INPROJ = os.environ.get("MAMBA_AMD_M1_NATIVE_INPROJ", "1") != "0"  # A/B switch
-_SKINNY = os.environ.get("MAMBA_AMD_SKINNY", "1") != "0"  # A/B switch: 0 = hipBLASLt for the skinny GEMMs
 _OUTPROJ_PIPE = os.environ.get("MAMBA_AMD_M1_OUTPROJ_PIPE", "1") != "0"  # A/B switch: 0 = hipBLASLt out_proj fwd
 
 
@@ -54,7 +51,7 @@ def _mm_cm(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,
     M = B.shape[1]
     # native only for the wide, short-K products (delta = W_dt x_dbl[:R], dconv += W_x^T dx_dbl):
     # for the long-K ones (x_dbl, dx_dbl[:R]) hipBLASLt measured faster (scripts/m1_gemms.py)
-    ok = (_SKINNY and A.shape[0] >= 256 and A.shape[1] <= 128 and A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16 and A.is_cuda and B.stride(1) == 1
+    ok = (A.shape[0] >= 256 and A.shape[1] <= 128 and A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16 and A.is_cuda and B.stride(1) == 1
           and A.shape[1] % 8 == 0 and M % 8 == 0 and B.stride(0) % 8 == 0 and B.data_ptr() % 16 == 0
           and (out is None or (out.stride(1) == 1 and out.stride(0) % 8 == 0 and out.data_ptr() % 16 == 0)))
     if ok:
@@ -63,6 +60,23 @@ def _mm_cm(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,
     if accumulate:
         return out.addmm_(A, B)
     return torch.mm(A, B, out=out) if out is not None else torch.mm(A, B)
+
+
+class _NegExpFn(torch.autograd.Function):
+    """A = -exp(A_log) (fp32), computed once per optimizer step inside an accumulation scope
+    (ops/grad_accum.cached_value) instead of two elementwise launches per layer and micro-batch."""
+
+    @staticmethod
+    def forward(ctx, A_log):
+        A = grad_accum.cached_value(A_log, "negexp", lambda t: -torch.exp(t.float()))
+        ctx.save_for_backward(A)
+        ctx.dtype = A_log.dtype
+        return A.view_as(A)
+
+    @staticmethod
+    def backward(ctx, dA):
+        (A,) = ctx.saved_tensors
+        return (dA * A).to(ctx.dtype)
 
 
 class _InProjCMFn(torch.autograd.Function):
@@ -94,57 +108,14 @@ class _InProjCMFn(torch.autograd.Function):
 
 
 def _wgrad_native(p, dY, X, dy_cm, x_cm):
-    """Weight gradient of a channel-major projection.  Default: ``_wgrad_native_cm`` (gemm_wgrad_cm,
-    reduced every micro-step).  MAMBA_AMD_M1_DEFER_WGRAD=1: dW (P, Q) = sum over tokens of dY x X on the native
-    pipelined GEMM engine (csrc/kernels/gemm_pipe.hip; k-contiguous / k-row operand layouts) with fp32
-    split-K slabs that persist across the micro-steps of an optimizer step (ops/grad_accum.deferred):
-    no-sync micro-steps add their slabs on the side stream and return nothing, the sync micro-step
-    reduces once.  Returns (handled, dw); handled is False when the layout is not supported."""
-    ops = _ext.ops()
-    P = dY.shape[0] if dy_cm else dY.shape[1]
-    Q = X.shape[0] if x_cm else X.shape[1]
-    T = dY.shape[1] if dy_cm else dY.shape[0]
-    ok = (dY.dtype == torch.bfloat16 and X.dtype == torch.bfloat16 and dY.stride(1) == 1 and X.stride(1) == 1
-          and dY.stride(0) % 8 == 0 and X.stride(0) % 8 == 0 and T % 8 == 0 and Q % 4 == 0
-          and dY.data_ptr() % 16 == 0 and X.data_ptr() % 16 == 0 and (X.shape[0] if x_cm else T) % 8 == 0
-          and (dY.shape[0] if dy_cm else T) % 8 == 0)
-    if not ok or os.environ.get("MAMBA_AMD_M1_DEFER_WGRAD", "0") != "1":
-        return _wgrad_native_cm(p, dY, X, dy_cm, x_cm)
-    la, lb = (0 if dy_cm else 1), (0 if x_cm else 1)
-    S = ops.gp_splits(P, Q, T)
-    d = grad_accum.deferred(p, "wgrad_cm", (S, P, Q), dY.device)
-    if d is None:  # outside an accumulation scope: transient slabs, reduce now
-        part = ops.gp_mm(dY, X, None, la, lb, 1, S, 256)
-        dw = torch.empty(P, Q, device=dY.device, dtype=torch.float32)
-        ops.gp_reduce(part, dw, False)
-        return True, grad_accum.defer(p, dw.to(p.dtype))
-    buf, mode = d
-    slab_mode = 1 if mode in (1, 3) else 2  # store / add
-    if mode <= 2:
-        side = grad_accum.side_stream(dY.device)
-        if side is None:
-            ops.gp_mm(dY, X, buf, la, lb, slab_mode, S, 256)
-        else:
-            side.wait_stream(torch.cuda.current_stream(dY.device))
-            with torch.cuda.stream(side):
-                ops.gp_mm(dY, X, buf, la, lb, slab_mode, S, 256)
-            dY.record_stream(side)
-            X.record_stream(side)
-        return True, None
-    ops.gp_mm(dY, X, buf, la, lb, slab_mode, S, 256)
-    dw = torch.empty(P, Q, device=dY.device, dtype=torch.float32)
-    ops.gp_reduce(buf, dw, False)
-    return True, grad_accum.defer(p, dw.to(p.dtype))
-
-
-def _wgrad_native_cm(p, dY, X, dy_cm, x_cm):
-    """Default Mamba-1 weight gradient: gemm_wgrad_cm (csrc/kernels/gemm.hip), whose fp32 split-K slabs persist
-    across the micro-steps of an optimizer step inside an accumulation scope (ops/grad_accum.deferred): the
-    no-sync micro-steps add into them on the weight-gradient side stream and return nothing, and the slab sum
-    (wgrad_reduce_k) runs once, on the sync micro-step.  Outside a scope (or MAMBA_AMD_DEFER_REDUCE=0) the slabs
-    are reduced every micro-step and added in place into ``p.grad`` on the no-sync micro-steps.  The 256x256
-    pipelined engine (``_wgrad_native``'s gp_mm form) measured 0.7% slower here: the skinny x_proj / dt_proj
-    products (Q = 48, P = 80) suit gemm_wgrad_cm's tiles better."""
+    """Weight gradient of a channel-major Mamba-1 projection: gemm_wgrad_cm (csrc/kernels/gemm.hip), its split-K
+    slabs reduced every micro-step and added in place into ``p.grad`` on the no-sync micro-steps (weight-gradient
+    side stream).  Returns (handled, dw); handled is False when the layout is not supported.
+    Measured alternatives: the 256x256 pipelined engine with slabs deferred to the sync micro-step -0.7%
+    (profiles/r2_v5_ab_m1_defer_wgrad.txt); keeping the
+    slabs across micro-steps (gemm_wgrad_cm's ``part_mode`` add-into-slabs form) made the wgrad kernels
+    read-modify-write their fp32 slabs (in_proj 190 -> 240 us, x/dt_proj 34 -> 60 us per call) for a 13 us
+    reduce saved, and halved the overlapped step (profiles/r3/ab3_mamba1_deferral.txt)."""
     M = dY.shape[1] if dy_cm else dY.shape[0]
     ok = (dY.dtype == torch.bfloat16 and X.dtype == torch.bfloat16 and dY.stride(1) == 1 and X.stride(1) == 1
           and M % 64 == 0 and dY.stride(0) % 8 == 0 and X.stride(0) % 8 == 0 and dY.shape[0] % 8 == 0
@@ -152,24 +123,6 @@ def _wgrad_native_cm(p, dY, X, dy_cm, x_cm):
           and dY.data_ptr() % 16 == 0 and X.data_ptr() % 16 == 0)
     if not ok:
         return False, None
-    P = dY.shape[0] if dy_cm else dY.shape[1]
-    Q = X.shape[0] if x_cm else X.shape[1]
-    ops = _ext.ops()
-    d = grad_accum.deferred(p, "wgrad_cm", (ops.wgrad_splits(M, P, Q), P, Q), dY.device)
-    if d is not None:
-        buf, mode = d
-        if mode <= 2:  # no-sync micro-step: slabs only, beside the rest of the backward
-            side = grad_accum.side_stream(dY.device)
-            if side is None:
-                ops.gemm_wgrad_cm(dY, X, None, False, dy_cm, x_cm, buf, mode)
-            else:
-                side.wait_stream(torch.cuda.current_stream(dY.device))
-                with torch.cuda.stream(side):
-                    ops.gemm_wgrad_cm(dY, X, None, False, dy_cm, x_cm, buf, mode)
-                dY.record_stream(side)
-                X.record_stream(side)
-            return True, None
-        return True, ops.gemm_wgrad_cm(dY, X, None, False, dy_cm, x_cm, buf, mode).to(p.dtype)
     if grad_accum.accumulable(p) and p.grad.dtype == torch.float32 and p.grad.is_contiguous():
         side = grad_accum.side_stream(dY.device)
         if side is None:
@@ -253,7 +206,6 @@ class _Mamba1InnerFn(torch.autograd.Function):
         ctx.save_for_backward(xz, w2, conv_b, Wx, Wdt, dt_bias, A, D, conv_out, x_dbl, delta, carries)
         ctx.meta = (b, l, conv_w.shape, W_x.dtype, W_dt.dtype)
         ctx.wparams = (W_x, W_dt)  # the parameters themselves (native weight gradients accumulate into .grad)
-        ctx.pparams = (D, conv_w)  # persistent keys of the deferred partial buffers
         return _flat(y)
 
     @staticmethod
@@ -271,41 +223,24 @@ class _Mamba1InnerFn(torch.autograd.Function):
         Bm = _cm(x_dbl[R:R + N], b, l).unsqueeze(1)
         Cm = _cm(x_dbl[R + N:], b, l).unsqueeze(1)
         dx_dbl = torch.empty_like(x_dbl)
-        # A / D / dt_bias and conv tap / bias partials are reduced once per optimizer step (grad_accum.deferred,
-        # keyed on the persistent D and conv weight parameters): the no-sync micro-steps add into them and return
-        # no gradient for those parameters
-        pD, pconv = ctx.pparams
-        dev = xz.device
-        d_s = grad_accum.deferred(pD, "selscan_small", (b * di * (N + 2),), dev)
-        d_c = grad_accum.deferred(pconv, "conv_cf", (b, di, w2.shape[1] + 1), dev)
         du, ddelta, dA, dB, dC, dD, dz, ddt_bias = ops.selscan_bwd_into(
             _cm(dy2.contiguous() if dy2.stride(-1) != 1 else dy2, b, l), conv_out, _cm(delta, b, l), A,
             Bm, Cm, D, z, dt_bias, carries, True,
-            dxz3[:, di:], _cm(dx_dbl[R:R + N], b, l).unsqueeze(1), _cm(dx_dbl[R + N:], b, l).unsqueeze(1),
-            *(d_s if d_s is not None else (None, 0)))
+            dxz3[:, di:], _cm(dx_dbl[R:R + N], b, l).unsqueeze(1), _cm(dx_dbl[R + N:], b, l).unsqueeze(1))
         dd2 = _flat(ddelta)
         pWx, pWdt = ctx.wparams
-        if _NATIVE_XDT:  # both operands channel-major: (di, M) . (R, M)^T on the native wgrad GEMM
-            ok_dt, dWdt = _wgrad_native(pWdt, dd2, x_dbl[:R], True, True)
-        else:
-            ok_dt = False
+        # both operands channel-major: (di, M) . (R, M)^T on the native wgrad GEMM
+        ok_dt, dWdt = _wgrad_native(pWdt, dd2, x_dbl[:R], True, True)
         if not ok_dt:
             dWdt = torch.mm(dd2, x_dbl[:R].t()).to(wdt_dtype)                # (di, R)
         _mm_cm(Wdt.t(), dd2, out=dx_dbl[:R])                                # d x_dbl[:R]
-        if _NATIVE_XDT:
-            ok_x, dWx = _wgrad_native(pWx, dx_dbl, _flat(conv_out), True, True)
-        else:
-            ok_x = False
+        ok_x, dWx = _wgrad_native(pWx, dx_dbl, _flat(conv_out), True, True)
         if not ok_x:
             dWx = torch.mm(dx_dbl, _flat(conv_out).t()).to(wx_dtype)         # (R+2N, di)
         dco2 = _flat(du)
         _mm_cm(Wx.t(), dx_dbl, out=dco2, accumulate=True)                   # du + W_x^T dx_dbl
-        _, dw, db = ops.conv1d_cf_bwd(x, w2, conv_b, _cm(dco2, b, l), True, dxz3[:, :di],
-                                      *(d_c if d_c is not None else (None, 0)))
-        nz = lambda t: t if t.numel() else None  # noqa: E731  (empty = deferred to the sync micro-step)
-        dw, db, dA, dD, ddt_bias = nz(dw), nz(db), nz(dA), nz(dD), nz(ddt_bias)
-        return (dxz, dw.reshape(wshape).to(w2.dtype) if dw is not None else None,
-                db.to(conv_b.dtype) if (conv_b is not None and db is not None) else None,
+        _, dw, db = ops.conv1d_cf_bwd(x, w2, conv_b, _cm(dco2, b, l), True, dxz3[:, :di])
+        return (dxz, dw.reshape(wshape).to(w2.dtype), db.to(conv_b.dtype) if conv_b is not None else None,
                 dWx, dWdt, ddt_bias, dA, dD, None, None, None)
 
 
@@ -377,9 +312,9 @@ class Mamba(nn.Module):
         else:
             conv_state = ssm_state = None
         cd = torch.get_autocast_dtype("cuda") if (hidden_states.is_cuda and torch.is_autocast_enabled("cuda")) else hidden_states.dtype
-        A = -torch.exp(self.A_log.float())
+        A = _NegExpFn.apply(self.A_log) if self.A_log.requires_grad else -torch.exp(self.A_log.float())
         h2 = hidden_states.reshape(b * l, -1).to(cd)
-        if _NATIVE_INPROJ and _ext.use_native(h2) and self.in_proj.weight.requires_grad:
+        if _ext.use_native(h2) and self.in_proj.weight.requires_grad:
             xz = _InProjCMFn.apply(h2, self.in_proj.weight, cd)            # (2di, b*l)
         else:
             xz = torch.mm(self.in_proj.weight.to(cd), h2.t())              # (2di, b*l)

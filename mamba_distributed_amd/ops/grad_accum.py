@@ -170,6 +170,21 @@ def cached_cast(w: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     return t
 
 
+def cached_value(w: torch.Tensor, tag: str, fn):
+    """``fn(w)`` (a function of a parameter only, e.g. A = -exp(A_log)), computed once per scope like
+    ``cached_cast``; outside a scope it is computed every call."""
+    if _scope_depth == 0:
+        return fn(w)
+    key = (id(w), tag)
+    ent = _wcache.get(key)
+    if ent is not None and ent[0] is w:
+        return ent[1]
+    with torch.no_grad():
+        t = fn(w)
+    _wcache[key] = (w, t)
+    return t
+
+
 def cached_transpose(w: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     """``w.to(dtype).t().contiguous()`` (the input-gradient GEMM's k-contiguous B operand), reused across
     the micro-steps of the current scope like ``cached_cast``."""

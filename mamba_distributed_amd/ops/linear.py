@@ -33,11 +33,6 @@ def _native_ok(dy: torch.Tensor, x: torch.Tensor) -> bool:
             and dy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0)
 
 
-import os as _os
-
-_WGRAD_DIRECT = _os.environ.get("MAMBA_AMD_WGRAD_DIRECT", "1") != "0"  # A/B: 0 = pipelined-engine slabs
-
-
 def _wgrad_native(p, dy2: torch.Tensor, x2: torch.Tensor, lb: int = 1):
     """dW = dy2^T x2 (fp32) on the native engine; None when deferred to the sync micro-step.  dy2 is token-major
     (T, P); x2 is token-major (T, Q) (lb = 1) or channel-major (Q, T) (lb = 0: the Mamba-1 out_proj input)."""
@@ -46,15 +41,22 @@ def _wgrad_native(p, dy2: torch.Tensor, x2: torch.Tensor, lb: int = 1):
     Q = x2.shape[1] if lb == 1 else x2.shape[0]
     S = ops.gp_splits(P, Q, T)
     d = grad_accum.deferred(p, "wgrad", (S, P, Q), dy2.device)
-    if d is None and lb == 1 and _WGRAD_DIRECT:
-        # not deferred (wide models, MAMBA_AMD_DEFER_REDUCE=0, outside a scope): the split-K wgrad kernel
-        # reduces its slabs itself and, on a no-sync micro-step, adds straight into p.grad (no transient dW,
-        # no queued add)
-        if grad_accum.accumulable(p) and p.grad.dtype == torch.float32 and p.grad.is_contiguous():
+    if d is None and lb == 1 and grad_accum.accumulable(p) and p.grad.dtype == torch.float32 and p.grad.is_contiguous():
+        # not deferred (wide models: auto_defer_reduce) on a no-sync micro-step: the split-K wgrad kernel adds
+        # its fixed-order slab sum straight into p.grad on the weight-gradient side stream, beside the rest of
+        # the backward (the round-1 path; running it on the main stream cost Mamba-2 1.4B 89k -> 84k tok/s,
+        # profiles/r3/ab4_mamba2_1.4b_bisect.txt)
+        side = grad_accum.side_stream(dy2.device)
+        if side is None:
             ops.gemm_wgrad(dy2, x2, p.grad, True)
-            return None
-        return ops.gemm_wgrad(dy2, x2, None, False)
-    if d is None:  # outside an accumulation scope: transient slabs, reduce now
+        else:
+            side.wait_stream(torch.cuda.current_stream(dy2.device))
+            with torch.cuda.stream(side):
+                ops.gemm_wgrad(dy2, x2, p.grad, True)
+            dy2.record_stream(side)
+            x2.record_stream(side)
+        return None
+    if d is None:  # outside an accumulation scope / sync micro-step: transient slabs, reduce now
         part = ops.gp_mm(dy2, x2, None, 1, lb, 1, S, 256)
         dw = torch.empty(P, Q, device=dy2.device, dtype=torch.float32)
         ops.gp_reduce(part, dw, False)
@@ -82,28 +84,36 @@ def _wgrad_native(p, dy2: torch.Tensor, x2: torch.Tensor, lb: int = 1):
 
 def _proj_engine() -> str:
     """Forward / input-gradient projection GEMM: "pk" (the persistent native engine, gemm_pk_k, for every shape
-    it takes), "auto" (pk only for the short-K shapes where it measured faster than the library) or "lib"
-    (hipBLASLt).  MAMBA_AMD_PROJ_GEMM selects."""
+    it takes), "auto" (pk only for the short-K shapes where it measured faster than the library), "lib"
+    (hipBLASLt), or a comma list of roles on pk: fwd / dgrad, each optionally suffixed _short (K <= 1024) or
+    _long (K > 1024), e.g. "fwd_short,dgrad".  MAMBA_AMD_PROJ_GEMM selects."""
     import os
     return os.environ.get("MAMBA_AMD_PROJ_GEMM", "lib")
 
 
-def _pk_wins(m: int, n_out: int, k: int) -> bool:
-    """Engine choice for an (m, n_out, k) product.  Isolated timings at the 280M shapes
-    (profiles/r3/pk*_vs_hipblaslt.log): pk wins at K = 768 with moderate outputs (in_proj fwd 143 vs 166 us,
-    out_proj dgrad 61 vs 66 us) and loses at K >= 1536 and on the 50k-wide lm_head."""
+def _pk_wins(m: int, n_out: int, k: int, role: str = "fwd") -> bool:
+    """Engine choice for an (m, n_out, k) product of one role ("fwd" / "dgrad").  Isolated timings at the 280M
+    shapes (profiles/r3/pk*_vs_hipblaslt.log): pk wins at K = 768 with moderate outputs (in_proj fwd 143 vs
+    166 us, out_proj dgrad 61 vs 66 us) and loses at K >= 1536 and on the 50k-wide lm_head."""
     e = _proj_engine()
     if e == "lib":
         return False
-    return e == "pk" or (k <= 1024 and m * n_out <= (1 << 28))
+    if e == "pk":
+        return True
+    if e == "auto":
+        return k <= 1024 and m * n_out <= (1 << 28)
+    if m * n_out > (1 << 28):  # never the lm_head
+        return False
+    roles = set(e.split(","))
+    return role in roles or f"{role}_{'short' if k <= 1024 else 'long'}" in roles
 
 
-def _pk_ok(a2: torch.Tensor, n_out: int, k: int) -> bool:
+def _pk_ok(a2: torch.Tensor, n_out: int, k: int, role: str = "fwd") -> bool:
     """The native persistent GEMM for a forward or input-gradient projection: a2 (T, k) token-major bf16 times a
     k-contiguous (n_out, k) weight image (csrc/kernels/gemm_pipe.hip)."""
     return (a2.is_cuda and a2.dtype == torch.bfloat16 and a2.dim() == 2 and a2.stride(-1) == 1
             and a2.stride(0) % 8 == 0 and a2.data_ptr() % 16 == 0 and a2.shape[0] >= 4096 and k > 192
-            and k % 8 == 0 and n_out % 8 == 0 and _pk_wins(a2.shape[0], n_out, k))
+            and k % 8 == 0 and n_out % 8 == 0 and _pk_wins(a2.shape[0], n_out, k, role))
 
 
 def _pk_mm(a2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
@@ -147,7 +157,7 @@ class _ProjFn(torch.autograd.Function):
             dy2 = dy2.contiguous()
         dx = None
         if ctx.needs_input_grad[0]:
-            if _pk_ok(dy2, w.shape[1], w.shape[0]):
+            if _pk_ok(dy2, w.shape[1], w.shape[0], "dgrad"):
                 # dX = dY W as a KC . KC product against W^T, transposed once per optimizer step
                 dx = _pk_mm(dy2, grad_accum.cached_transpose(ctx.param, w.dtype))
             else:

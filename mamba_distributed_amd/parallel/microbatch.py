@@ -48,13 +48,29 @@ def _reducer(model):
     return model.reducer if isinstance(model, ReducedModule) else None
 
 
-def auto_overlap(cfg) -> bool:
+def auto_micro_batch(cfg, seqs_per_rank: int, seq_len: int) -> int:
+    """Micro-batch (sequences) for a rank that processes ``seqs_per_rank`` sequences per optimizer step; the
+    global batch and the gradient are the same for any choice (the loss is averaged over all micro-batches).
+    Measured on one MI355X at Mamba-2 280M, T = 1024 (profiles/r3/ab5_micro_batch.txt): 64 sequences
+    without the overlap match 32 with it at grad-accum 16 (289.6k vs 289.5k tok/s, same 128 GB peak) and
+    beat it in the 8-GPU per-rank regime (65,536 tokens per rank: one micro-batch of 64 at 282k vs two of 32
+    at 264k, which leaves the second backward with nothing to overlap).  Wider models keep 32 (their
+    activations at 64 would not fit next to a second micro-batch, and the 1.4B GEMMs already fill the chip)."""
+    best = 64 if getattr(cfg, "d_model", 0) <= 1024 and seq_len <= 1024 else 32
+    while best > 1 and (best > seqs_per_rank or seqs_per_rank % best):
+        best //= 2
+    return max(1, best)
+
+
+def auto_overlap(cfg, micro_tokens: int = 32768) -> bool:
     """Default for the two-stream micro-batch overlap, by model width.  Measured on one MI355X
     (interleaved runs, native wgrad side stream on): Mamba-2 280M 262k -> 275k tok/s with overlap,
     Mamba-1 280M / 370M +0.4% / +1.3%, but Mamba-2 1.4B (d_model 2048) 91k -> 67k: its GEMMs already
     fill the chip, and a second forward stream beside the backward and its side-stream weight-gradient
-    GEMMs only thrashes the caches.  So: on for d_model <= 1024."""
-    return getattr(cfg, "d_model", 0) <= 1024
+    GEMMs only thrashes the caches.  So: on for d_model <= 1024, and only up to 32k-token micro-batches: two
+    micro-batches of 64 x 1024 in flight peak at 241 GB and run at 109k tok/s (allocator pressure) against
+    290k for one at a time (profiles/r3/ab5_micro_batch.txt)."""
+    return getattr(cfg, "d_model", 0) <= 1024 and micro_tokens <= 32768
 
 
 def auto_defer_reduce(cfg) -> bool:
@@ -62,17 +78,19 @@ def auto_defer_reduce(cfg) -> bool:
     Measured on one MI355X (interleaved runs): Mamba-2 280M 272k -> 283k tok/s with deferral, but
     Mamba-2 1.4B (d_model 2048, overlap off) 88k -> 41k: there the deferred projection slabs are
     full-size K-split GEMMs on the weight-gradient side stream, and next to the main stream's
-    chip-filling GEMMs they serialise.  So: on for d_model <= 1024 (same crossover as overlap)."""
-    return getattr(cfg, "d_model", 0) <= 1024
+    chip-filling GEMMs they serialise.  So: on for d_model <= 1024 (same crossover as overlap).  Mamba-1 keeps
+    them off: its channel-major projections reduce their own split-K slabs, and with the deferred norm /
+    out_proj partials the 280M step measured 208k against 214-218k without (profiles/r3/ab3_mamba1_deferral.txt)."""
+    return getattr(cfg, "d_model", 0) <= 1024 and getattr(cfg, "layer_type", "Mamba2") != "Mamba1"
 
 
-def resolve_overlap(mode, cfg) -> bool:
+def resolve_overlap(mode, cfg, micro_tokens: int = 32768) -> bool:
     """``mode``: "auto" (auto_overlap), "on"/"off", or a bool."""
     if isinstance(mode, bool):
         return mode
     mode = str(mode).lower()
     if mode == "auto":
-        return auto_overlap(cfg)
+        return auto_overlap(cfg, micro_tokens)
     if mode in ("on", "true", "1", "yes"):
         return True
     if mode in ("off", "false", "0", "no"):

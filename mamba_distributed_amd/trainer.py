@@ -266,8 +266,8 @@ class Trainer:
 
         # overlap micro-batch k+1's forward with k's backward on a second stream (parallel/microbatch.py);
         # not under TP/CP, whose per-layer collectives must be issued on one stream per communicator
-        overlap = (resolve_overlap(self.a.overlap_microbatches, self.raw_model.config) and self.device_type == "cuda"
-                   and not self.parallel)
+        overlap = (resolve_overlap(self.a.overlap_microbatches, self.raw_model.config, self.a.B * self.a.T)
+                   and self.device_type == "cuda" and not self.parallel)
         with grad_accum.accumulation_scope(defer_reduce=auto_defer_reduce(self.raw_model.config)):  # weights are frozen until optimizer.step()
             loss_accum = run_micro_batches(self.model, lambda: self._batch(self.train_loader), self.grad_accum_steps,
                                            compute_loss, overlap=overlap)

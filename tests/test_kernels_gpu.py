@@ -882,32 +882,6 @@ def test_selective_scan_sequential_backward(cuda, monkeypatch, b, d, L, G, with_
             assert rel(a_, b_) < 1e-2, (nm, rel(a_, b_))
 
 
-def test_mamba1_deferred_wgrad_matches_default(cuda, monkeypatch):
-    """MAMBA_AMD_M1_DEFER_WGRAD=1 (gemm_pipe slabs reduced once per optimizer step) gives the same
-    parameter gradients as the default per-micro-step path over a 3-micro-step accumulation."""
-    from mamba_distributed_amd import LMHeadModel, MambaConfig
-    from mamba_distributed_amd.ops import grad_accum
-    torch.manual_seed(0)
-    cfg = MambaConfig(d_model=256, n_layer=2, vocab_size=1024, ssm_cfg={"layer": "Mamba1"})
-    m = LMHeadModel(cfg, device=cuda)
-    xs = [torch.randint(0, 1024, (2, 256), device=cuda) for _ in range(3)]
-    grads = {}
-    for v in ("0", "1"):
-        monkeypatch.setenv("MAMBA_AMD_M1_DEFER_WGRAD", v)
-        grad_accum.release_buffers()
-        m.zero_grad(set_to_none=True)
-        with grad_accum.accumulation_scope():
-            for k, x in enumerate(xs):
-                grad_accum.set_direct(k != len(xs) - 1)
-                with torch.autocast("cuda", dtype=torch.bfloat16):
-                    _, loss = m(x, x)
-                loss.backward()
-        torch.cuda.synchronize()
-        grads[v] = {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
-    for n in grads["0"]:
-        assert rel(grads["1"][n], grads["0"][n]) < 1e-2, n
-
-
 @pytest.mark.parametrize("b,L,H,G,N,with_init", [(2, 200, 8, 1, 128, True), (1, 64, 4, 2, 64, False),
                                                  (3, 1030, 24, 1, 128, False)])
 def test_ssd_fp32_native_forward(cuda, b, L, H, G, N, with_init):
