@@ -33,6 +33,8 @@
 //    share the A panel / the K slab in one XCD's L2.
 //  * K tails: chunks with k >= K are DMA'd from a 16-B zero page (per-lane source), rows / columns past
 //    M / N are clamped on load and never stored.
+#include <cstdlib>
+
 #include "mfma.h"
 #include "launchers.h"
 
@@ -90,12 +92,17 @@ __device__ __forceinline__ void pin() {
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
     __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
   }
+  if constexpr (NREADS % 2) {  // odd read count (3-column-tile waves): the last read gets its own MFMA
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+  }
 #pragma unroll
   for (int k = 0; k < NVMEM; ++k) {
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
     __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read (LDS-DMA)
   }
-  __builtin_amdgcn_sched_group_barrier(0x008, NMFMA - NREADS / 2 - NVMEM, 0);
+  static_assert(NMFMA >= (NREADS + 1) / 2 + NVMEM, "pin: more reads / DMAs than MFMA slots");
+  __builtin_amdgcn_sched_group_barrier(0x008, NMFMA - (NREADS + 1) / 2 - NVMEM, 0);
   __builtin_amdgcn_sched_barrier(0);
 }
 
@@ -364,12 +371,12 @@ struct GemmPkArgs {
 
 __device__ __attribute__((aligned(64))) uint4 g_pk_sink[64];  // epilogue stores of lanes outside C
 
-template <int MI, bool RS, bool TAIL>
+template <int MI, int NJ, bool RS, bool TAIL>
 __global__ __launch_bounds__(512) void gemm_pk_k(GemmPkArgs a) {
-  constexpr int NT = 512, NJ = 4, WN = 4, MH = MI / 2;
-  constexpr int BM = 32 * MI, BN = 256;
+  constexpr int NT = 512, WN = 4, MH = MI / 2;
+  constexpr int BM = 32 * MI, BN = 64 * NJ;  // NJ = 4: 256-wide tiles; NJ = 3: 192-wide (d_model = 768 outputs)
   constexpr int SA = BM * 128, SB = BN * 128, SS = SA + SB;
-  constexpr int GA = BM / 64, GB = 4, G = GA + GB;
+  constexpr int GA = BM / 64, GB = BN / 64, G = GA + GB;
   constexpr int STG = 8 * 2048;
   constexpr int NST = 2 * MI;  // epilogue store instructions per wave
   __shared__ __attribute__((aligned(1024))) char smem[2 * SS + STG + 64];
@@ -518,8 +525,8 @@ __global__ __launch_bounds__(512) void gemm_pk_k(GemmPkArgs a) {
       tile_mn(tile, m0, n0);
       char* stg = smem + 2 * SS + ew * 2048;
       const int r = el & 15, q = el >> 4;
-      const int rr = el >> 3, cc = el & 7;
-      const int n = n0 + ebn0 + 8 * cc;
+      // staged row = 2 NJ 16-B chunks; store h covers chunk slots el + 64 h (slots past 16 rows go to the sink)
+      constexpr int CH = 2 * NJ;
       float rs[MI];
       if constexpr (RS) {
 #pragma unroll
@@ -539,10 +546,13 @@ __global__ __launch_bounds__(512) void gemm_pk_k(GemmPkArgs a) {
         }
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          const int row = rr + 8 * h;
-          const uint4 v = *reinterpret_cast<const uint4*>(stg + row * 128 + ((cc ^ (row & 7)) << 4));
-          const int m = m0 + eam0 + 16 * i + row;
-          uint4* dst = (m < a.M && n < a.N) ? reinterpret_cast<uint4*>(a.C + (int64_t)m * a.ldc + n) : &g_pk_sink[el];
+          const int sl = el + 64 * h;
+          const int row = CH == 8 ? sl >> 3 : sl / CH, cc = CH == 8 ? sl & 7 : sl % CH;
+          const int rowc = row < 16 ? row : 15;
+          const uint4 v = *reinterpret_cast<const uint4*>(stg + rowc * 128 + ((cc ^ (rowc & 7)) << 4));
+          const int m = m0 + eam0 + 16 * i + row, n = n0 + ebn0 + 8 * cc;
+          uint4* dst = (row < 16 && m < a.M && n < a.N) ? reinterpret_cast<uint4*>(a.C + (int64_t)m * a.ldc + n)
+                                                       : &g_pk_sink[el];
           *dst = v;
         }
       }
@@ -624,6 +634,11 @@ hipError_t launch_gemm_pipe(int la, int lb, const void* A, int64_t lda, const vo
   return hipGetLastError();
 }
 
+static int getenv_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return v && *v ? std::atoi(v) : dflt;
+}
+
 static int cu_count() {
   static int n = 0;
   if (n == 0) {
@@ -677,22 +692,31 @@ hipError_t launch_gemm_pk(int la, int lb, const void* A, int64_t lda, const void
   a.M = M; a.N = N; a.K = K;
   a.kte = ((K + 63) / 64 + 1) / 2 * 2;
   const int ncu = cu_count();
-  // tile height: 256 unless 128-row tiles fill the rounds better (e.g. N = 768 outputs: 384 tiles of 256 rows
-  // are 1.5 rounds of 256 CUs, 768 of 128 rows are 3 full rounds; a 128-row tile costs ~0.55 of a 256-row one)
-  const int t256 = ((M + 255) / 256) * ((N + 255) / 256), t128 = ((M + 127) / 128) * ((N + 255) / 256);
-  const double c256 = (double)((t256 + ncu - 1) / ncu), c128 = 0.55 * ((t128 + ncu - 1) / ncu);
-  const int bm = c128 < c256 ? 128 : 256;
-  a.tm = (M + bm - 1) / bm; a.tn = (N + 255) / 256;
+  // tile shape: 256 x 256 unless a smaller tile fills the rounds of ncu workgroups better.  Relative tile costs:
+  // 128 x 256 ~0.55, 256 x 192 ~0.78 of a 256 x 256 tile.  E.g. N = 768 outputs (out_proj fwd, in_proj / lm_head
+  // dgrad at d_model 768): 384 tiles of 256 x 256 are 1.5 rounds of 256 CUs, 768 of 128 x 256 are 3 rounds
+  // (1.65), 512 of 256 x 192 are exactly 2 rounds (1.56) at full-height operand reuse.
+  auto rounds = [&](int bm_, int bn_) {
+    const int t = ((M + bm_ - 1) / bm_) * ((N + bn_ - 1) / bn_);
+    return (double)((t + ncu - 1) / ncu);
+  };
+  const double c256 = rounds(256, 256), c128 = 0.55 * rounds(128, 256), c192 = 0.78 * rounds(256, 192);
+  int bm = 256, bn = 256;
+  if (c192 < c256 && c192 <= c128 && getenv_int("MAMBA_AMD_PK_BN192", 1)) bn = 192;
+  else if (c128 < c256) bm = 128;
+  a.tm = (M + bm - 1) / bm; a.tn = (N + bn - 1) / bn;
   a.ntiles = a.tm * a.tn;
   const bool tail = K % 64 != 0 || a.kte * 64 != K;
   const int nwg = std::min(a.ntiles, ncu);
-#define PK_L(MI_, RS_)                                                                                  \
-  if (tail) hipLaunchKernelGGL((gemm_pk_k<MI_, RS_, true>), dim3(nwg), dim3(512), 0, st, a);            \
-  else hipLaunchKernelGGL((gemm_pk_k<MI_, RS_, false>), dim3(nwg), dim3(512), 0, st, a)
-  if (bm == 256) {
-    if (rowscale) { PK_L(8, true); } else { PK_L(8, false); }
+#define PK_L(MI_, NJ_, RS_)                                                                              \
+  if (tail) hipLaunchKernelGGL((gemm_pk_k<MI_, NJ_, RS_, true>), dim3(nwg), dim3(512), 0, st, a);          \
+  else hipLaunchKernelGGL((gemm_pk_k<MI_, NJ_, RS_, false>), dim3(nwg), dim3(512), 0, st, a)
+  if (bn == 192) {
+    if (rowscale) { PK_L(8, 3, true); } else { PK_L(8, 3, false); }
+  } else if (bm == 256) {
+    if (rowscale) { PK_L(8, 4, true); } else { PK_L(8, 4, false); }
   } else {
-    if (rowscale) { PK_L(4, true); } else { PK_L(4, false); }
+    if (rowscale) { PK_L(4, 4, true); } else { PK_L(4, 4, false); }
   }
 #undef PK_L
   return hipGetLastError();

@@ -3,13 +3,14 @@
 Parameter names, shapes and init follow upstream ``mamba_ssm/modules/mamba2.py::Mamba2``
  so checkpoints interchange.  Training forward:
 
-    zxbcdt = in_proj(u)                      hipBLASLt fwd / dgrad, native wgrad; token-major
+    zxbcdt = in_proj(u)                      native persistent GEMM fwd into 64-aligned padded rows,
+                                             hipBLASLt dgrad (K = padded width), native split-K wgrad
     y      = mamba2_inner_fn(zxbcdt, ...)    HIP: conv1d(xBC)+SiLU -> SSD -> gated RMSNorm
-    out    = out_proj(y)                     hipBLASLt fwd / dgrad, native wgrad
-(projection routing: ops/linear.py)
+    out    = out_proj(y)                     hipBLASLt fwd, native persistent dgrad, native wgrad
+(projection routing: ops/linear.py, MAMBA_AMD_PROJ_GEMM)
 
 The conv, SSD and norm kernels read their operands straight out of the strided zxbcdt buffer
-and the backward writes d(zxbcdt) as one buffer (ops/ssd.py).
+and the backward writes d(zxbcdt) as one buffer in the same padded layout (ops/ssd.py).
 """
 from __future__ import annotations
 
@@ -99,7 +100,9 @@ class Mamba2(nn.Module):
             if inference_params.seqlen_offset > 0:
                 out, _, _ = self.step(u, conv_state, ssm_state)
                 return out
-        zxbcdt = linear(u, self.in_proj)
+        fused = not self._general and self.cp_group is None and conv_state is None
+        # the fused chain writes d(zxbcdt) into the padded layout itself (ops/linear.py: padded output rows)
+        zxbcdt = linear(u, self.in_proj, pad=fused)
         if seq_idx is None and cu_seqlens is not None:
             seq_idx = seq_idx_from_cu_seqlens(cu_seqlens, l, u.device).expand(b, l)
         if self._general:

@@ -2,8 +2,9 @@
 
 Forward and input-gradient GEMMs run on the persistent engine (``gp_pk``: one workgroup per CU walks the
 output tiles; the next tile's operands stream into LDS while the previous tile's bf16 epilogue drains as
-whole-row stores), the input gradient as dY . (W^T)^T against a transposed weight cached per optimizer step;
-shapes it does not take (short K, small token counts) fall back to hipBLASLt.  The weight
+whole-row stores), the input gradient as dY . (W^T)^T against a transposed weight cached per optimizer step,
+for the shapes where it measured faster than hipBLASLt (``_pk_wins``: short K, moderate outputs); the long-K
+and lm_head products stay on the library with a tuned solution table.  The weight
 gradient dW = dY^T X reduces over all B*T tokens into a small output (3352 x 768 for in_proj), where the
 library leaves most CUs idle: the native engine (csrc/kernels/gemm_pipe.hip, ``gp_mm`` with both operands
 token-major) splits the tokens into S K-slices written as fp32 slabs.  Inside an accumulation scope the
@@ -88,13 +89,14 @@ def _proj_engine() -> str:
     (hipBLASLt), or a comma list of roles on pk: fwd / dgrad, each optionally suffixed _short (K <= 1024) or
     _long (K > 1024), e.g. "fwd_short,dgrad".  MAMBA_AMD_PROJ_GEMM selects."""
     import os
-    return os.environ.get("MAMBA_AMD_PROJ_GEMM", "lib")
+    return os.environ.get("MAMBA_AMD_PROJ_GEMM", "auto")
 
 
 def _pk_wins(m: int, n_out: int, k: int, role: str = "fwd") -> bool:
     """Engine choice for an (m, n_out, k) product of one role ("fwd" / "dgrad").  Isolated timings at the 280M
-    shapes (profiles/r3/pk*_vs_hipblaslt.log): pk wins at K = 768 with moderate outputs (in_proj fwd 143 vs
-    166 us, out_proj dgrad 61 vs 66 us) and loses at K >= 1536 and on the 50k-wide lm_head."""
+    shapes (profiles/r3/pk*_vs_hipblaslt.log, pk5_inproj_padded_width.log): pk wins at K = 768 with moderate
+    outputs (padded in_proj fwd 316 vs 334 us, out_proj dgrad 135 vs 132 us at 64k tokens) and loses at K >= 1536
+    and on the 50k-wide lm_head, which stay on hipBLASLt under the default "auto"."""
     e = _proj_engine()
     if e == "lib":
         return False
@@ -132,11 +134,60 @@ def mm_nt(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     return _pk_mm(a, b) if ok else torch.mm(a, b.t())
 
 
+# ---- padded output rows --------------------------------------------------------------------------------------
+# An output width that is not a multiple of 64 elements (the Mamba-2 in_proj: 3352 = 2 d_inner + 2 N + H at the
+# 280M shape) makes every row of the product start off a 128-B line, and the input gradient then reads a
+# K = 3352 operand whose K-tiles straddle two lines each.  The padded layout computes the output into a
+# (T, Np) buffer (Np = width rounded up to 64) against a weight copy with zero rows appended (made once per
+# optimizer step) and hands the consumer the (T, width) column view.  A consumer that writes the output's
+# gradient into the same padded layout with zeroed pad columns registers it (register_zero_padded_grad); the
+# backward then runs the input gradient as a K = Np product (zero rows of W^T meet zero columns of dY):
+# in_proj dgrad 290 -> 252 us and forward 342 -> 316 us per layer at 64 x 1024 tokens
+# (profiles/r3/pk5_inproj_padded_width.log).  Any other gradient layout takes the unpadded product.
+_ZERO_PADDED: dict = {}
+
+
+def pad_width(n: int) -> int:
+    return (n + 63) // 64 * 64
+
+
+def register_zero_padded_grad(full: torch.Tensor) -> None:
+    """``full`` (T, Np) [or (b, l, Np)] is a gradient buffer whose columns past the consumer's width are zero;
+    the view handed back as the gradient of a padded projection output starts at its first element."""
+    for k in [k for k, (ref, _) in _ZERO_PADDED.items() if ref() is None]:
+        del _ZERO_PADDED[k]
+    import weakref
+    _ZERO_PADDED[full.data_ptr()] = (weakref.ref(full), full._version)
+
+
+def _zero_padded_full(dy2: torch.Tensor, np_: int):
+    """The registered (T, Np) buffer behind the gradient view dy2 (T, width), or None."""
+    ent = _ZERO_PADDED.get(dy2.data_ptr())
+    if ent is None or dy2.stride(0) != np_ or dy2.stride(1) != 1:
+        return None
+    full = ent[0]()
+    if full is None or full._version != ent[1] or full.data_ptr() != dy2.data_ptr() or full.shape[-1] != np_:
+        return None
+    del _ZERO_PADDED[dy2.data_ptr()]
+    return full.reshape(-1, np_)
+
+
+def _pad_rows(w: torch.Tensor, cd: torch.dtype, np_: int) -> torch.Tensor:
+    wp = torch.zeros(np_, w.shape[1], device=w.device, dtype=cd)
+    wp[:w.shape[0]].copy_(w)
+    return wp
+
+
 class _ProjFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, cd):
+    def forward(ctx, x, weight, cd, pad):
         x2 = x.reshape(-1, x.shape[-1]).to(cd)
-        w = grad_accum.cached_cast(weight, cd)
+        n = weight.shape[0]
+        np_ = pad_width(n) if pad else n
+        if np_ != n:
+            w = grad_accum.cached_value(weight, ("pad_rows", cd, np_), lambda t: _pad_rows(t, cd, np_))
+        else:
+            w = grad_accum.cached_cast(weight, cd)
         if _pk_ok(x2, w.shape[0], w.shape[1]) and w.is_contiguous():
             y = _pk_mm(x2, w)
         else:
@@ -145,23 +196,31 @@ class _ProjFn(torch.autograd.Function):
         ctx.param = weight
         ctx.wdtype = weight.dtype
         ctx.xshape = x.shape
-        return y.view(*x.shape[:-1], w.shape[0])
+        ctx.n = n
+        return y[:, :n].view(*x.shape[:-1], n) if np_ != n else y.view(*x.shape[:-1], n)
 
     @staticmethod
     def backward(ctx, dy):
         x2, w = ctx.saved_tensors
+        n = ctx.n
+        np_ = w.shape[0]
         dy2 = dy.reshape(-1, dy.shape[-1])
         if dy2.dtype != w.dtype:
             dy2 = dy2.to(w.dtype)
-        if not dy2.is_contiguous():
+        full = _zero_padded_full(dy2, np_) if np_ != n else None
+        if full is None and not dy2.is_contiguous():
             dy2 = dy2.contiguous()
         dx = None
         if ctx.needs_input_grad[0]:
-            if _pk_ok(dy2, w.shape[1], w.shape[0], "dgrad"):
+            if full is not None:
+                # K = Np: the zero pad columns of dY meet the zero pad rows of W
+                dx = _pk_mm(full, grad_accum.cached_transpose(w, w.dtype)) if _pk_ok(full, w.shape[1], np_, "dgrad") \
+                    else torch.mm(full, w)
+            elif _pk_ok(dy2, w.shape[1], n, "dgrad"):
                 # dX = dY W as a KC . KC product against W^T, transposed once per optimizer step
                 dx = _pk_mm(dy2, grad_accum.cached_transpose(ctx.param, w.dtype))
             else:
-                dx = torch.mm(dy2, w)
+                dx = torch.mm(dy2, w[:n])
         dw = None
         if ctx.needs_input_grad[1]:
             p = ctx.param
@@ -171,11 +230,18 @@ class _ProjFn(torch.autograd.Function):
                     dw = grad_accum.defer(p, dw.to(ctx.wdtype))
             else:
                 dw = grad_accum.defer(p, torch.mm(dy2.t(), x2).to(ctx.wdtype))
-        return (dx.view(ctx.xshape) if dx is not None else None), dw, None
+        return (dx.view(ctx.xshape) if dx is not None else None), dw, None, None
 
 
-def linear(x: torch.Tensor, layer: torch.nn.Linear) -> torch.Tensor:
-    """``layer(x)`` for a bias-free nn.Linear, native weight gradient on the GPU."""
+def _pad_enabled() -> bool:
+    import os
+    return os.environ.get("MAMBA_AMD_PAD_PROJ", "1") != "0"
+
+
+def linear(x: torch.Tensor, layer: torch.nn.Linear, pad: bool = False) -> torch.Tensor:
+    """``layer(x)`` for a bias-free nn.Linear, native weight gradient on the GPU.  ``pad``: compute into rows
+    padded to a multiple of 64 and return the column view (see register_zero_padded_grad)."""
     if layer.bias is None and _ext.use_native(x):
-        return _ProjFn.apply(x, layer.weight, _compute_dtype(x))
+        pad = pad and _pad_enabled() and layer.weight.shape[0] % 64 != 0
+        return _ProjFn.apply(x, layer.weight, _compute_dtype(x), pad)
     return layer(x)

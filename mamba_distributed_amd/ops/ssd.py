@@ -182,7 +182,16 @@ class _Mamba2InnerFn(torch.autograd.Function):
         di = H * headdim
         gn = ngroups * d_state
         conv_dim = di + 2 * gn
-        dz_all = torch.empty_like(zxbcdt)
+        rs = zxbcdt.stride(-2)
+        if rs > dproj and rs % 64 == 0 and zxbcdt.stride(0) == l * rs:
+            # zxbcdt is the column view of a padded in_proj output (ops/linear.py): write d(zxbcdt) into the
+            # same layout with zero pad columns, so the in_proj input gradient runs on 128-B aligned rows
+            dz_full = torch.empty(b, l, rs, device=zxbcdt.device, dtype=zxbcdt.dtype)
+            dz_full[..., dproj:].zero_()
+            dz_all = dz_full[..., :dproj]
+        else:
+            dz_full = None
+            dz_all = torch.empty_like(zxbcdt)
         z = zxbcdt[..., :di]
         pw, pb, pdtb, pA, pD, pn = ctx.params
         dev = zxbcdt.device
@@ -219,6 +228,9 @@ class _Mamba2InnerFn(torch.autograd.Function):
         d = grad_accum.defer
         nz = lambda t: t if t.numel() else None  # noqa: E731  (empty = deferred to the sync micro-step)
         dw = nz(dw)
+        if dz_full is not None:
+            from .linear import register_zero_padded_grad
+            register_zero_padded_grad(dz_full)
         return (dz_all, d(pw, dw.reshape(ctx.wshape).to(w2.dtype)) if dw is not None else None,
                 d(pb, nz(db).to(conv_b.dtype)) if (conv_b is not None and db.numel()) else None,
                 d(pdtb, nz(ddt_bias)), d(pA, nz(dA)), d(pD, nz(dD)), d(pn, nz(dnorm_w)),

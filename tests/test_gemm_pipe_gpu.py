@@ -173,17 +173,18 @@ def test_gp_pk_strided_out_and_unsupported(cuda, eng):
 
 
 @pytest.mark.parametrize("eng", ["pk"])
-@pytest.mark.parametrize("which", ["in_fwd", "in_dgrad", "out_fwd", "out_dgrad", "lm_fwd"])
+@pytest.mark.parametrize("which", ["in_fwd", "in_dgrad", "out_fwd", "out_dgrad", "lm_fwd", "lm_dgrad"])
 def test_gp_pk_headline_shapes(cuda, eng, which):
     """The persistent engine at the Mamba-2 280M bench micro-batch (32 x 1024 tokens), input gradients through
-    the transposed weight (KC . KC), vs fp32."""
+    the transposed weight (KC . KC), vs fp32.  The d_model-wide outputs (in_dgrad, out_fwd, lm_dgrad) take the
+    256 x 192 tiles."""
     ops = _ops()
     g = torch.Generator(device=cuda).manual_seed(3)
     T, d, dp, di = 32768, 768, 3352, 1536
     rnd = lambda *s: (torch.randn(*s, device=cuda, generator=g) * 0.5).to(torch.bfloat16)  # noqa: E731
     A, B = {"in_fwd": lambda: (rnd(T, d), rnd(dp, d)), "in_dgrad": lambda: (rnd(T, dp), rnd(d, dp)),
             "out_fwd": lambda: (rnd(T, di), rnd(d, di)), "out_dgrad": lambda: (rnd(T, d), rnd(di, d)),
-            "lm_fwd": lambda: (rnd(8192, d), rnd(50304, d))}[which]()
+            "lm_fwd": lambda: (rnd(8192, d), rnd(50304, d)), "lm_dgrad": lambda: (rnd(4096, 50304), rnd(d, 50304))}[which]()
     C = _pmm(ops, eng, A, B)
     assert _rel(C, A.float() @ B.float().t()) < 8e-3
 
@@ -207,3 +208,19 @@ def test_gp_pk_concurrent_streams(cuda):
     torch.cuda.synchronize()
     for o1, o2 in outs:
         assert torch.equal(o1, r1) and torch.equal(o2, r2)
+
+
+@pytest.mark.parametrize("M,N,K", [(32768, 768, 1536), (768, 520, 1544), (4096, 392, 3352)])
+def test_gp_pk_bn192_matches_bn256(cuda, M, N, K, monkeypatch):
+    """The 256 x 192 tile walk (chosen for d_model-wide outputs) against the 256 x 256 one on the same operands:
+    both within bf16 rounding of fp32, and the fp32 K-sums agree to bf16 output rounding."""
+    ops = _ops()
+    g = torch.Generator(device=cuda).manual_seed(M + N + K)
+    A, B = _mk(M, K, 0, cuda, g), _mk(N, K, 0, cuda, g)
+    monkeypatch.setenv("MAMBA_AMD_PK_BN192", "1")
+    c192 = ops.gp_pk(A, B)
+    monkeypatch.setenv("MAMBA_AMD_PK_BN192", "0")
+    c256 = ops.gp_pk(A, B)
+    ref = _ref(A, B, 0, 0)
+    assert _rel(c192, ref) < 8e-3 and _rel(c256, ref) < 8e-3
+    assert _rel(c192, c256) < 8e-3
