@@ -545,9 +545,7 @@ std::vector<Tensor> ssd_bwd(Tensor dy, Tensor x, Tensor dt, Tensor A, Tensor Bm,
   a.dB = (mamba_amd::bf16_t*)dB.data_ptr(); a.sdBb = dB.stride(0); a.sdBl = dB.stride(1); a.sdBg = dB.stride(2);
   a.dC = (mamba_amd::bf16_t*)dC.data_ptr(); a.sdCb = dC.stride(0); a.sdCl = dC.stride(1); a.sdCg = dC.stride(2);
   // one head group per B/C group: the chunk kernel finishes dB / dC itself (no head-group partials)
-  a.fuse_dbc = std::getenv("MAMBA_AMD_SSD_FUSE_DBC") ? std::atoi(std::getenv("MAMBA_AMD_SSD_FUSE_DBC")) != 0 &&
-                                                         a.HG == a.H / a.G
-                                                     : a.HG == a.H / a.G;
+  a.fuse_dbc = a.HG == a.H / a.G;
   const int64_t pn = a.fuse_dbc ? 0 : 1;
   auto part_dcb = at::empty({pn * a.B, a.nc, a.nhg, 64, 64}, fo);
   auto part_db = at::empty({pn * a.B, a.nc, a.nhg, 64, a.N}, fo);

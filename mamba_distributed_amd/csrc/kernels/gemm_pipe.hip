@@ -634,11 +634,6 @@ hipError_t launch_gemm_pipe(int la, int lb, const void* A, int64_t lda, const vo
   return hipGetLastError();
 }
 
-static int getenv_int(const char* name, int dflt) {
-  const char* v = std::getenv(name);
-  return v && *v ? std::atoi(v) : dflt;
-}
-
 static int cu_count() {
   static int n = 0;
   if (n == 0) {
@@ -702,7 +697,7 @@ hipError_t launch_gemm_pk(int la, int lb, const void* A, int64_t lda, const void
   };
   const double c256 = rounds(256, 256), c128 = 0.55 * rounds(128, 256), c192 = 0.78 * rounds(256, 192);
   int bm = 256, bn = 256;
-  if (c192 < c256 && c192 <= c128 && getenv_int("MAMBA_AMD_PK_BN192", 1)) bn = 192;
+  if (c192 < c256 && c192 <= c128) bn = 192;
   else if (c128 < c256) bm = 128;
   a.tm = (M + bm - 1) / bm; a.tn = (N + bn - 1) / bn;
   a.ntiles = a.tm * a.tn;

@@ -271,8 +271,8 @@ typedef float ss_f2 __attribute__((ext_vector_type(2)));
 // nothing per lane but dt and dt*u (staged once per tile in LDS for the 4 waves).  Per step and lane:
 // 2 v_pk_mul (dt A), 4 exp, 2 v_pk_mul (dt u B), 2 v_pk_fma (h), 2 v_pk_fma (C h).  The 4 waves' partial
 // y meet in LDS at the end of the tile; (y + D u) silu(z) leaves as coalesced rows.
-constexpr int SG_T = 16, SG_D = 4;  // tile length, tiles of u / delta / z in flight
-__global__ __launch_bounds__(256) void selscan_fwd_sg_k(SelScanArgs a) {
+constexpr int SG_T = 16, SG_D = 3;  // tile length, tiles of u / delta / z in flight
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void selscan_fwd_sg_k(SelScanArgs a) {
   constexpr int N = 16;
   __shared__ __attribute__((aligned(16))) float dlS[64][SG_T + 4], duS[64][SG_T + 4];
   __shared__ __attribute__((aligned(16))) float yS[4][64][SG_T + 4];

@@ -17,7 +17,6 @@ materialisation), like upstream's MambaInnerFn.
 from __future__ import annotations
 
 import math
-import os
 from typing import Optional
 
 import torch
@@ -39,9 +38,6 @@ def _cm(t2d: torch.Tensor, b: int, l: int) -> torch.Tensor:
 def _flat(t: torch.Tensor) -> torch.Tensor:
     """logical (b, d, l) stored (d, b, l) -> (d, b*l) view."""
     return t.permute(1, 0, 2).reshape(t.shape[1], -1)
-
-
-_OUTPROJ_PIPE = os.environ.get("MAMBA_AMD_M1_OUTPROJ_PIPE", "1") != "0"  # A/B switch: 0 = hipBLASLt out_proj fwd
 
 
 def _mm_cm(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None, accumulate: bool = False):
@@ -149,7 +145,7 @@ class _OutProjCMFn(torch.autograd.Function):
         ctx.save_for_backward(y2, w)
         ctx.param = weight
         T = y2.shape[1]
-        if (_OUTPROJ_PIPE and y2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and y2.stride(1) == 1
+        if (y2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and y2.stride(1) == 1
                 and y2.stride(0) % 8 == 0 and y2.data_ptr() % 16 == 0 and w.is_contiguous() and T % 8 == 0
                 and w.shape[1] % 8 == 0 and T >= 4096):
             # y2 is channel-major (di, T): its transpose is the A operand as stored (k-rows of contiguous

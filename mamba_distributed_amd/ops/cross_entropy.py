@@ -9,8 +9,8 @@ d(loss)/d(logits) = (softmax - onehot) / n_valid as bf16 in the same pass.
 
 Two entry points:
   * ``cross_entropy(logits, targets)``            — drop-in loss, logits preserved, bf16 grad buffer.
-  * ``fused_linear_cross_entropy(h, W, targets)`` — lm_head GEMM + CE in one autograd node; the
-    gradient overwrites the logits buffer in place, so the (B*T, V) tensor exists once.
+  * ``fused_linear_cross_entropy(h, W, targets)`` — lm_head GEMMs + CE in one autograd node over row chunks
+    of the logits (the whole (B*T, V) tensor never exists; dh and dW are produced in the forward pass).
 """
 from __future__ import annotations
 
@@ -18,7 +18,6 @@ import torch
 import torch.nn.functional as F
 
 from . import _ext, grad_accum
-from .linear import _pk_wins, mm_nt
 
 
 def _inv_count(targets, ignore_index):
@@ -54,42 +53,108 @@ def cross_entropy(logits, targets, ignore_index=-100):
 
 
 class _FusedLinearCEFn(torch.autograd.Function):
-    """loss = CE(h @ W^T, targets); the CE kernel turns the logits buffer into dlogits in place."""
+    """loss = CE(h @ W^T, targets), with both gradients produced in the forward pass.
+
+    The tokens are processed in row chunks (``_row_chunk``: <= 16384 rows, i.e. a 1.65 GB bf16 logits tile at
+    V = 50304).  Per chunk:
+      logits_c = h_c W^T                         hipBLASLt (tuned table)  | native: gp_pk
+      loss_c, dlogits_c (in place, / n_valid)    ce_fwd (one read of the tile)
+      dh_c     = dlogits_c W                     gp_pk (persistent MFMA engine) against W^T cached per optimizer step
+      dW      += dlogits_c^T h_c                 hipBLASLt + fp32 add     | native: gp_mm, fp32 accumulation
+    so the (B*T, V) logits never exist whole (6.6 GB at 64 x 1024 tokens) and nothing of the lm_head is kept
+    for the backward but dh and dW, which the backward scales by d(loss).  Engine per product (``_lm_engines``,
+    MAMBA_AMD_LMHEAD=auto|native|lib): measured at one 16384-row chunk, fwd pk 1211 / lib 1116 us, dh pk 1041 /
+    lib 1063 us, dW gp_mm 1529 / lib 1321 us (profiles/r3/lm_head_chunk_products.log) -> auto = lib, pk, lib.
+    The reference materialises the full fp32 logits (model.py:44-46)."""
 
     @staticmethod
-    def forward(ctx, h, weight, targets, ignore_index, compute_dtype):
+    def forward(ctx, h, weight, targets, ignore_index, compute_dtype, row_chunk):
         h2 = h.reshape(-1, h.shape[-1]).to(compute_dtype)
         w = grad_accum.cached_cast(weight, compute_dtype)        # once per optimizer step
         t = targets.reshape(-1)
-        logits = mm_nt(h2, w)                                    # persistent native GEMM or hipBLASLt
+        M, K = h2.shape
+        V = w.shape[0]
         inv = _inv_count(t, ignore_index)
-        need_grad = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
-        losses = _ext.ops().ce_fwd(logits, t, ignore_index, inv, logits if need_grad else None)
+        need_h, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        nat_f, nat_h, nat_w = _lm_engines(h2, w)
+        R = _row_chunk(M, V, row_chunk)
+        buf = torch.empty(min(R, M), V, device=h2.device, dtype=compute_dtype)
+        losses = torch.empty(M, device=h2.device, dtype=torch.float32)
+        dh = torch.empty(M, K, device=h2.device, dtype=compute_dtype) if need_h else None
+        dw = torch.empty(1, V, K, device=h2.device, dtype=torch.float32) if need_w else None
+        wt = grad_accum.cached_transpose(weight, compute_dtype) if (need_h and nat_h) else None
+        ops = _ext.ops()
+        for r0 in range(0, M, R):
+            r1 = min(M, r0 + R)
+            hc, lg = h2[r0:r1], buf[:r1 - r0]
+            if nat_f:
+                ops.gp_pk(hc, w, lg)
+            else:
+                torch.mm(hc, w.t(), out=lg)
+            losses[r0:r1] = ops.ce_fwd(lg, t[r0:r1], ignore_index, inv, lg if (need_h or need_w) else None)
+            if need_h:
+                if nat_h:
+                    ops.gp_pk(lg, wt, dh[r0:r1])
+                else:
+                    torch.mm(lg, w, out=dh[r0:r1])
+            if need_w:
+                if nat_w:
+                    ops.gp_mm(lg, hc, dw, 1, 1, 1 if r0 == 0 else 2, 1, 256)
+                elif r0 == 0:
+                    dw[0].copy_(lg.t() @ hc)
+                else:
+                    dw[0].add_(lg.t() @ hc)
+        del buf
         loss = losses.sum() * inv
-        if need_grad:
-            ctx.save_for_backward(h2, w, logits)               # logits now hold dlogits
+        ctx.save_for_backward(dh, dw)
         ctx.hshape, ctx.hdtype, ctx.wdtype = h.shape, h.dtype, weight.dtype
-        ctx.param = weight
         return loss
 
     @staticmethod
     def backward(ctx, gloss):
-        h2, w, dlogits = ctx.saved_tensors
+        dh_, dw_ = ctx.saved_tensors
         g = gloss.to(torch.float32)
         dh = dw = None
         if ctx.needs_input_grad[0]:
-            # dh = dlogits W: a K-contiguous product against W^T (cached once per optimizer step)
-            wt = (grad_accum.cached_transpose(ctx.param, w.dtype)
-                  if _pk_wins(dlogits.shape[0], w.shape[1], w.shape[0]) else None)
-            dh = (mm_nt(dlogits, wt) if wt is not None else torch.mm(dlogits, w)).mul_(g).view(ctx.hshape).to(ctx.hdtype)
+            dh = dh_.mul_(g.to(dh_.dtype)).view(ctx.hshape).to(ctx.hdtype)
         if ctx.needs_input_grad[1]:
-            dw = torch.mm(dlogits.t(), h2).to(ctx.wdtype).mul_(g)
-        return dh, dw, None, None, None
+            dw = dw_[0].mul_(g).to(ctx.wdtype)
+        return dh, dw, None, None, None, None
 
 
-def fused_linear_cross_entropy(h, weight, targets, ignore_index=-100, compute_dtype=torch.bfloat16):
+def _lm_native(h2: torch.Tensor, w: torch.Tensor) -> bool:
+    """The shapes suit the native engines (persistent GEMM: K > 192, 8-aligned, 16-B aligned rows)."""
+    return (h2.is_cuda and h2.dtype == torch.bfloat16 and h2.stride(-1) == 1 and h2.stride(0) % 8 == 0
+            and h2.data_ptr() % 16 == 0 and h2.shape[1] > 192 and h2.shape[1] % 8 == 0 and w.shape[0] % 8 == 0
+            and w.is_contiguous())
+
+
+def _lm_engines(h2: torch.Tensor, w: torch.Tensor):
+    """(logits, dh, dW) on the native engines?  MAMBA_AMD_LMHEAD: auto (the measured-fastest per product: dh
+    native), native (all three), lib (none)."""
+    import os
+    mode = os.environ.get("MAMBA_AMD_LMHEAD", "auto")
+    if mode == "lib" or not _lm_native(h2, w):
+        return False, False, False
+    if mode == "native":
+        return True, True, True
+    return False, True, False
+
+
+def _row_chunk(M: int, V: int, row_chunk=None) -> int:
+    """Rows per logits tile: at most 16384 (a 1.65 GB bf16 tile at V = 50304, under the persistent GEMM's 4 GB
+    operand limit), balanced over the chunks and rounded up to whole 256-row GEMM tiles."""
+    if row_chunk:
+        return min(M, int(row_chunk))
+    cap = max(256, min(16384, (1 << 31) // max(1, 2 * V) // 256 * 256))
+    n = -(-M // cap)
+    per = -(-M // n)
+    return min(M, -(-per // 256) * 256)
+
+
+def fused_linear_cross_entropy(h, weight, targets, ignore_index=-100, compute_dtype=torch.bfloat16, row_chunk=None):
     if _ext.use_native(h):
-        return _FusedLinearCEFn.apply(h, weight, targets, ignore_index, compute_dtype)
+        return _FusedLinearCEFn.apply(h, weight, targets, ignore_index, compute_dtype, row_chunk)
     logits = F.linear(h, weight.to(h.dtype))
     return F.cross_entropy(logits.float().view(-1, logits.size(-1)), targets.view(-1),
                            ignore_index=ignore_index)

@@ -1,5 +1,5 @@
 """lm_head GEMMs at the 280M training shape (32768 x 768 hidden, vocab 50304) with the tuned table, and
-the fused lm_head + CE node end to end.   python scripts/lmhead_bench.py"""
+the fused lm_head + CE node end to end (native row-chunked engines vs hipBLASLt).   python scripts/lmhead_bench.py"""
 import os
 import sys
 
@@ -16,7 +16,7 @@ def main():
     assert _ext.load(), _ext.error()
     print("tuned:", enable_tuned_gemms())
     dev = "cuda"
-    T, d, V = 32768, 768, 50304
+    T, d, V = int(os.environ.get("LM_T", 65536)), 768, 50304
     h = torch.randn(T, d, device=dev).to(torch.bfloat16)
     W = (torch.randn(V, d, device=dev) * 0.02).to(torch.bfloat16)
     g = torch.randn(T, V, device=dev).to(torch.bfloat16)
@@ -27,6 +27,19 @@ def main():
                      ("wgrad g^T.h", lambda: torch.mm(g.t(), h))]:
         t = timeit(fn, 10)
         print(f"{name:20s} {t * 1e3:9.1f} us  {fl / t / 1e9:7.0f} TF/s", flush=True)
+    # the row-chunked node's three products at one 16384-row chunk: native engines vs hipBLASLt
+    R = 16384
+    ops = torch.ops.mamba_amd
+    hc, gc = h[:R], g[:R]
+    Wt = W.t().contiguous()
+    dwb = torch.zeros(1, V, d, device=dev)
+    fc = 2 * R * d * V
+    for name, fn in [("chunk fwd  pk", lambda: ops.gp_pk(hc, W)), ("chunk fwd  lib", lambda: torch.mm(hc, W.t())),
+                     ("chunk dh   pk", lambda: ops.gp_pk(gc, Wt)), ("chunk dh   lib", lambda: torch.mm(gc, W)),
+                     ("chunk dW   gp_mm+=", lambda: ops.gp_mm(gc, hc, dwb, 1, 1, 2, 1, 256)),
+                     ("chunk dW   lib", lambda: torch.mm(gc.t(), hc))]:
+        t = timeit(fn, 10)
+        print(f"{name:20s} {t * 1e3:9.1f} us  {fc / t / 1e9:7.0f} TF/s", flush=True)
     Wp = (torch.randn(V, d, device=dev) * 0.02).requires_grad_(True)
     hh = h.clone().requires_grad_(True)
     tg = torch.randint(0, V, (T,), device=dev)
@@ -35,8 +48,16 @@ def main():
         with torch.autocast("cuda", dtype=torch.bfloat16):
             loss = fused_linear_cross_entropy(hh, Wp, tg)
         loss.backward()
-    t = timeit(node, 5)
-    print(f"fused lm_head+CE fwd+bwd {t * 1e3:9.1f} us")
+    for eng in ("native", "lib"):
+        os.environ["MAMBA_AMD_LMHEAD"] = eng
+        node()
+        torch.cuda.synchronize()
+        torch.cuda.reset_peak_memory_stats()
+        base = torch.cuda.memory_allocated()
+        t = timeit(node, 5)
+        peak = (torch.cuda.max_memory_allocated() - base) / 2**30
+        print(f"fused lm_head+CE fwd+bwd [{eng}] {t * 1e3:9.1f} us  ({3 * fl / t / 1e9:6.0f} TF/s over the 3 GEMMs)"
+              f"  transient peak {peak:.2f} GB", flush=True)
 
 
 if __name__ == "__main__":

@@ -129,6 +129,34 @@ def test_cross_entropy(cuda):
     assert rel(gn[0], gr[0]) < 3e-2 and rel(gn[1], gr[1]) < 3e-2
 
 
+@pytest.mark.parametrize("engine", ["auto", "native"])
+@pytest.mark.parametrize("row_chunk", [None, 2048])
+def test_fused_lm_head_ce_native(cuda, row_chunk, engine, monkeypatch):
+    """The row-chunked lm_head + CE at the 280M head shape (d 768, V 50304) against fp32 math: loss, dh and dW
+    (row_chunk 2048: three chunks, the last one 404 rows, dW accumulated across them); engine "native": all three
+    products on the native MFMA engines, "auto": the default per-product choice (dh native)."""
+    import importlib
+    monkeypatch.setenv("MAMBA_AMD_LMHEAD", engine)
+    ce = importlib.import_module("mamba_distributed_amd.ops.cross_entropy")
+    torch.manual_seed(4)
+    M, d, V = 4500, 768, 50304
+    h = torch.randn(M, d, device=cuda, dtype=torch.bfloat16)
+    W = torch.randn(V, d, device=cuda) * 0.05
+    t = torch.randint(0, V, (M,), device=cuda)
+    t[::5] = -100
+    assert ce._lm_native(h, W.to(torch.bfloat16))
+    hn, Wn = leaf(h), leaf(W)
+    loss = ce.fused_linear_cross_entropy(hn, Wn, t, row_chunk=row_chunk)
+    (loss * 1.7).backward()
+    hr, Wr = leaf(h.float()), leaf(W.to(torch.bfloat16).float())
+    lr = F.cross_entropy(hr @ Wr.t(), t, ignore_index=-100)
+    (lr * 1.7).backward()
+    assert abs(loss.item() - lr.item()) < 2e-3 * abs(lr.item())
+    assert rel(hn.grad, hr.grad) < 2e-2, rel(hn.grad, hr.grad)
+    assert rel(Wn.grad, Wr.grad) < 2e-2, rel(Wn.grad, Wr.grad)
+    assert hn.grad.dtype == torch.bfloat16 and Wn.grad.dtype == torch.float32
+
+
 def _ssd_inputs(cuda, b, L, H, G, N, seed=0, strided=True):
     g = torch.Generator(device=cuda).manual_seed(seed)
     P = 64
