@@ -57,14 +57,15 @@ class _FusedLinearCEFn(torch.autograd.Function):
 
     The tokens are processed in row chunks (``_row_chunk``: <= 16384 rows, i.e. a 1.65 GB bf16 logits tile at
     V = 50304).  Per chunk:
-      logits_c = h_c W^T                         hipBLASLt (tuned table)  | native: gp_pk
+      logits_c = h_c W^T                         hipBLASLt (tuned table)           | native: gp_pk
       loss_c, dlogits_c (in place, / n_valid)    ce_fwd (one read of the tile)
-      dh_c     = dlogits_c W                     gp_pk (persistent MFMA engine) against W^T cached per optimizer step
-      dW      += dlogits_c^T h_c                 hipBLASLt + fp32 add     | native: gp_mm, fp32 accumulation
+      dh_c     = dlogits_c W                     hipBLASLt                         | native: gp_pk against W^T
+      dW      += dlogits_c^T h_c                 hipBLASLt, fp32 output + accumulate | native: gp_mm, fp32 slab
     so the (B*T, V) logits never exist whole (6.6 GB at 64 x 1024 tokens) and nothing of the lm_head is kept
-    for the backward but dh and dW, which the backward scales by d(loss).  Engine per product (``_lm_engines``,
-    MAMBA_AMD_LMHEAD=auto|native|lib): measured at one 16384-row chunk, fwd pk 1211 / lib 1116 us, dh pk 1041 /
-    lib 1063 us, dW gp_mm 1529 / lib 1321 us (profiles/r3/lm_head_chunk_products.log) -> auto = lib, pk, lib.
+    for the backward but dh and dW, which the backward scales by d(loss).  Engines (MAMBA_AMD_LMHEAD=lib|native):
+    the whole node at 64k tokens measured 17.0 ms on hipBLASLt, 17.5 with dh native, 19.0 all native (per chunk
+    the native fwd / dW products are 10-17% slower, the native dh 2% faster in isolation;
+    profiles/r3/lm_head_chunk_products.log), so the library is the default.
     The reference materialises the full fp32 logits (model.py:44-46)."""
 
     @staticmethod
@@ -100,10 +101,8 @@ class _FusedLinearCEFn(torch.autograd.Function):
             if need_w:
                 if nat_w:
                     ops.gp_mm(lg, hc, dw, 1, 1, 1 if r0 == 0 else 2, 1, 256)
-                elif r0 == 0:
-                    dw[0].copy_(lg.t() @ hc)
                 else:
-                    dw[0].add_(lg.t() @ hc)
+                    _lib_wgrad_acc(dw[0], lg, hc, r0 == 0)
         del buf
         loss = losses.sum() * inv
         ctx.save_for_backward(dh, dw)
@@ -122,6 +121,29 @@ class _FusedLinearCEFn(torch.autograd.Function):
         return dh, dw, None, None, None, None
 
 
+_F32_OUT = [None]  # hipBLASLt bf16 x bf16 -> fp32 products (aten::mm.dtype / addmm.dtype) usable here
+
+
+def _lib_wgrad_acc(dw: torch.Tensor, g: torch.Tensor, h: torch.Tensor, first: bool) -> None:
+    """dw (fp32) (+)= g^T h on the library: fp32 output straight from the GEMM where torch exposes it (no bf16
+    rounding of the chunk's product and no separate add), else a bf16 product added in fp32."""
+    if _F32_OUT[0] is None:
+        try:
+            torch.mm(g[:8].t(), h[:8], out_dtype=torch.float32)
+            _F32_OUT[0] = True
+        except (RuntimeError, TypeError):
+            _F32_OUT[0] = False
+    if _F32_OUT[0]:
+        if first:
+            torch.mm(g.t(), h, out_dtype=torch.float32, out=dw)
+        else:
+            torch.addmm(dw, g.t(), h, out_dtype=torch.float32, out=dw)
+    elif first:
+        dw.copy_(g.t() @ h)
+    else:
+        dw.add_(g.t() @ h)
+
+
 def _lm_native(h2: torch.Tensor, w: torch.Tensor) -> bool:
     """The shapes suit the native engines (persistent GEMM: K > 192, 8-aligned, 16-B aligned rows)."""
     return (h2.is_cuda and h2.dtype == torch.bfloat16 and h2.stride(-1) == 1 and h2.stride(0) % 8 == 0
@@ -130,15 +152,13 @@ def _lm_native(h2: torch.Tensor, w: torch.Tensor) -> bool:
 
 
 def _lm_engines(h2: torch.Tensor, w: torch.Tensor):
-    """(logits, dh, dW) on the native engines?  MAMBA_AMD_LMHEAD: auto (the measured-fastest per product: dh
-    native), native (all three), lib (none)."""
+    """(logits, dh, dW) on the native engines?  MAMBA_AMD_LMHEAD=native: all three; lib (default): none."""
     import os
-    mode = os.environ.get("MAMBA_AMD_LMHEAD", "auto")
-    if mode == "lib" or not _lm_native(h2, w):
-        return False, False, False
-    if mode == "native":
-        return True, True, True
-    return False, True, False
+    nat = os.environ.get("MAMBA_AMD_LMHEAD", "lib") == "native" and _lm_native(h2, w)
+    return nat, nat, nat
+
+
+_ROW_CAP = 16384
 
 
 def _row_chunk(M: int, V: int, row_chunk=None) -> int:
@@ -146,7 +166,7 @@ def _row_chunk(M: int, V: int, row_chunk=None) -> int:
     operand limit), balanced over the chunks and rounded up to whole 256-row GEMM tiles."""
     if row_chunk:
         return min(M, int(row_chunk))
-    cap = max(256, min(16384, (1 << 31) // max(1, 2 * V) // 256 * 256))
+    cap = max(256, min(_ROW_CAP, (1 << 31) // max(1, 2 * V) // 256 * 256))
     n = -(-M // cap)
     per = -(-M // n)
     return min(M, -(-per // 256) * 256)

@@ -48,17 +48,20 @@ def main():
         with torch.autocast("cuda", dtype=torch.bfloat16):
             loss = fused_linear_cross_entropy(hh, Wp, tg)
         loss.backward()
-    for eng in ("native", "lib"):
+    import importlib
+    ce = importlib.import_module("mamba_distributed_amd.ops.cross_entropy")
+    for eng, cap, f32 in (("lib", 16384, True), ("lib", 32768, True), ("lib", 16384, False), ("native", 16384, True)):
         os.environ["MAMBA_AMD_LMHEAD"] = eng
+        ce._ROW_CAP = cap
+        ce._F32_OUT[0] = None if f32 else False
         node()
         torch.cuda.synchronize()
         torch.cuda.reset_peak_memory_stats()
         base = torch.cuda.memory_allocated()
         t = timeit(node, 5)
         peak = (torch.cuda.max_memory_allocated() - base) / 2**30
-        print(f"fused lm_head+CE fwd+bwd [{eng}] {t * 1e3:9.1f} us  ({3 * fl / t / 1e9:6.0f} TF/s over the 3 GEMMs)"
-              f"  transient peak {peak:.2f} GB", flush=True)
-
+        print(f"fused lm_head+CE fwd+bwd [{eng} rows<={cap} dW-f32-out={ce._F32_OUT[0]}] {t * 1e3:9.1f} us"
+              f"  ({3 * fl / t / 1e9:6.0f} TF/s over the 3 GEMMs)  transient peak {peak:.2f} GB", flush=True)
 
 if __name__ == "__main__":
     main()

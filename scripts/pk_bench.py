@@ -80,10 +80,6 @@ def main():
             for _ in range(a.rounds):
                 t["pk"].append(timeit(lambda: ops.gp_pk(A, B), a.reps))
                 t["lib"].append(timeit(lambda: torch.nn.functional.linear(A, B), a.reps))
-                if N % 192 == 0 and N <= 1536:  # the 256 x 256 walk for the shapes that now take 256 x 192 tiles
-                    os.environ["MAMBA_AMD_PK_BN192"] = "0"
-                    t.setdefault("pk256", []).append(timeit(lambda: ops.gp_pk(A, B), a.reps))
-                    os.environ["MAMBA_AMD_PK_BN192"] = "1"
                 if name in ("in_fwd", "out_fwd"):
                     t["gp_mm"].append(timeit(lambda: ops.gp_mm(A, B, None, 0, 0, 0, 1, 256), a.reps))
             for k, v in t.items():
