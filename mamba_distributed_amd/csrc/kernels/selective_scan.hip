@@ -277,6 +277,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
   __shared__ __attribute__((aligned(16))) float dlS[64][SG_T + 4], duS[64][SG_T + 4];
   __shared__ __attribute__((aligned(16))) float yS[4][64][SG_T + 4];
   __shared__ __attribute__((aligned(16))) bf16_t uS[64][SG_T];
+  // this tile's B / C in fp32, per step t: wave w's 4 states of B then C at [t][8 w .. 8 w + 7]; a 36-float
+  // row stride puts the 64 lanes' staging writes (steps 2j / 2j+1, state n, B or C) on 64 distinct banks
+  __shared__ __attribute__((aligned(16))) float bcS[SG_T][36];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int wgs_per_b = a.D / 64;
   const int b = blockIdx.x / wgs_per_b, d0 = (blockIdx.x % wgs_per_b) * 64;
@@ -336,14 +339,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
       *reinterpret_cast<uint2*>(&uS[sr][sc]) = r.u;
     }
     const uint2 zc = r.z;
-    uint32_t Bq[4][SG_T / 2], Cq[4][SG_T / 2];
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-      for (int j = 0; j < SG_T / 2; ++j) {
-        Bq[n][j] = __builtin_amdgcn_readlane(bc, 16 * n + j);
-        Cq[n][j] = __builtin_amdgcn_readlane(bc, 16 * n + 8 + j);
-      }
+    // B / C of the tile: this lane holds steps 2 bl_j, 2 bl_j + 1 of state 4 w + bl_n (B or C); the wave stages
+    // them in its own slots (no barrier needed: same-wave LDS order) and the step loop reads them back as
+    // wave-uniform float4 broadcasts -- LDS-pipe work instead of 64 v_readlane + SALU unpacking per tile
+    bcS[2 * bl_j][8 * w + 4 * bl_m + bl_n] = __uint_as_float(bc << 16);
+    bcS[2 * bl_j + 1][8 * w + 4 * bl_m + bl_n] = __uint_as_float(bc & 0xffff0000u);
     __syncthreads();
     fetch(r, min(tile + SG_D, ntile - 1));
     fetch_bc(min(tile + 1, ntile - 1));
@@ -359,16 +359,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int t = t4 + k;
-        const int j = t >> 1;
-        const bool hi = t & 1;
+        const float4 Bv = *reinterpret_cast<const float4*>(&bcS[t][8 * w]);
+        const float4 Cv = *reinterpret_cast<const float4*>(&bcS[t][8 * w + 4]);
         ss_f2 y2 = ss_f2{0.f, 0.f};
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
-          const uint32_t b0 = Bq[2 * p][j], b1 = Bq[2 * p + 1][j], c0 = Cq[2 * p][j], c1 = Cq[2 * p + 1][j];
-          const ss_f2 Bp = ss_f2{__uint_as_float(hi ? (b0 & 0xffff0000u) : (b0 << 16)),
-                                 __uint_as_float(hi ? (b1 & 0xffff0000u) : (b1 << 16))};
-          const ss_f2 Cp = ss_f2{__uint_as_float(hi ? (c0 & 0xffff0000u) : (c0 << 16)),
-                                 __uint_as_float(hi ? (c1 & 0xffff0000u) : (c1 << 16))};
+          const ss_f2 Bp = p ? ss_f2{Bv.z, Bv.w} : ss_f2{Bv.x, Bv.y};
+          const ss_f2 Cp = p ? ss_f2{Cv.z, Cv.w} : ss_f2{Cv.x, Cv.y};
           const ss_f2 e = A2[p] * dlv[k];
           const ss_f2 av = ss_f2{__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
           h[p] = __builtin_elementwise_fma(av, h[p], Bp * duv[k]);
