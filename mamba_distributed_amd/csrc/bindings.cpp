@@ -506,7 +506,8 @@ std::vector<Tensor> ssd_bwd(Tensor dy, Tensor x, Tensor dt, Tensor A, Tensor Bm,
                             optional<Tensor> dt_bias, optional<Tensor> init, Tensor cum, Tensor dtp, Tensor states,
                             optional<Tensor> dfinal, int64_t chunk, bool softplus, double dt_min, double dt_max,
                             optional<Tensor> dx_out, optional<Tensor> ddt_out, optional<Tensor> dB_out,
-                            optional<Tensor> dC_out, bool A_is_log, optional<Tensor> part_buf, int64_t part_mode_) {
+                            optional<Tensor> dC_out, bool A_is_log, optional<Tensor> part_buf, int64_t part_mode_,
+                            int64_t ddt_zero_pad) {
   check_cuda(x, "x");
   at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   mamba_amd::SSDArgs a{};
@@ -542,6 +543,15 @@ std::vector<Tensor> ssd_bwd(Tensor dy, Tensor x, Tensor dt, Tensor A, Tensor Bm,
   a.dx = (mamba_amd::bf16_t*)dx.data_ptr(); a.sdxb = dx.stride(0); a.sdxl = dx.stride(1); a.sdxh = dx.stride(2);
   a.ddt = ddt.data_ptr(); a.ddt_dtype = dcode(ddt.scalar_type());
   a.sddtb = ddt.stride(0); a.sddtl = ddt.stride(1); a.sddth = ddt.stride(2);
+  if (ddt_zero_pad > 0) {
+    // the pad columns [H, H + pad) of every ddt row are part of the same allocation (the caller's padded row);
+    // zeroed with 16-B stores: bf16, unit column stride, pad a multiple of 8, 16-B aligned pad start and rows
+    TORCH_CHECK(ddt.scalar_type() == at::kBFloat16 && ddt.stride(2) == 1 && ddt_zero_pad % 8 == 0 &&
+                ddt.stride(1) >= a.H + ddt_zero_pad && ddt.stride(1) % 8 == 0 && ddt.stride(0) % 8 == 0 &&
+                ((uintptr_t)ddt.data_ptr() + 2 * (uintptr_t)a.H) % 16 == 0,
+                "ssd_bwd: ddt_zero_pad needs bf16 rows with 16-B aligned pad columns");
+    a.ddt_zero_pad = (int)ddt_zero_pad;
+  }
   a.dB = (mamba_amd::bf16_t*)dB.data_ptr(); a.sdBb = dB.stride(0); a.sdBl = dB.stride(1); a.sdBg = dB.stride(2);
   a.dC = (mamba_amd::bf16_t*)dC.data_ptr(); a.sdCb = dC.stride(0); a.sdCl = dC.stride(1); a.sdCg = dC.stride(2);
   // one head group per B/C group: the chunk kernel finishes dB / dC itself (no head-group partials)
@@ -1059,7 +1069,7 @@ TORCH_LIBRARY(mamba_amd, m) {
   m.def("ssd_bwd(Tensor dy, Tensor x, Tensor dt, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? dt_bias, "
         "Tensor? init, Tensor cum, Tensor dtp, Tensor states, Tensor? dfinal, int chunk, bool softplus, float dt_min, "
         "float dt_max, Tensor(a!)? dx_out, Tensor(b!)? ddt_out, Tensor(c!)? dB_out, Tensor(d!)? dC_out, "
-        "bool A_is_log=False, Tensor(z!)? part_buf=None, int part_mode=0) -> Tensor[]");
+        "bool A_is_log=False, Tensor(z!)? part_buf=None, int part_mode=0, int ddt_zero_pad=0) -> Tensor[]");
   m.def("selscan_fwd(Tensor u, Tensor delta, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? z, Tensor? delta_bias, "
         "bool softplus) -> (Tensor, Tensor, Tensor)");
   m.def("selscan_bwd(Tensor dout, Tensor u, Tensor delta, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? z, "

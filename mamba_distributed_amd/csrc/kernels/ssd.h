@@ -31,6 +31,8 @@ struct SSDArgs {
   float* dinit;           // or null
   bf16_t* dx; int64_t sdxb, sdxl, sdxh;
   void* ddt; int ddt_dtype; int64_t sddtb, sddtl, sddth;
+  int ddt_zero_pad;       // bf16 ddt rows (sddth == 1): zero this many columns after the H dt columns (the padded
+                          // in_proj gradient's pad, ops/linear.py), written by the chunk kernel's first head flush
   bf16_t* dB; int64_t sdBb, sdBl, sdBg;
   bf16_t* dC; int64_t sdCb, sdCl, sdCg;
   bool fuse_dbc;          // HG == H / G: ssd_chunk_bwd finishes dB / dC itself (no partials, no ssd_dbc_bwd)

@@ -52,35 +52,52 @@ __device__ __forceinline__ void st_any(void* p, int dt, int64_t i, float v) {
 }
 
 // ============================== K0: dt transform + cumsum ====================================
+// One 256-thread workgroup per (b, chunk) stages the chunk's dt rows (64 steps x H heads, each step's heads
+// contiguous in the in_proj output) through LDS with the threads walking the rows in order, then every wave scans
+// heads w, w+4, ... (lane = step) and writes dt / cumsum rows (b, h, Lp) contiguously.  (A wave per (b, h, chunk)
+// read its 64 dt values 64 row strides apart: one 128-B line per element, ~20 us per layer at 64k tokens.)
+constexpr int CS_HMAX = 32;  // heads staged per pass
 __global__ __launch_bounds__(256) void ssd_cumsum_k(SSDArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (wid >= (int64_t)a.B * a.H * a.nc) return;
-  const int c = wid % a.nc, h = (wid / a.nc) % a.H, b = wid / ((int64_t)a.nc * a.H);
+  __shared__ float raw_s[Q][CS_HMAX + 1];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x % a.nc, b = blockIdx.x / a.nc;
   const int t = c * Q + lane;
-  float v = 0.f;
-  if (t < a.L) {
-    float raw = ld_any(a.dt, a.dt_dtype, (int64_t)b * a.sdtb + (int64_t)t * a.sdtl + (int64_t)h * a.sdth);
-    if (a.dt_bias) raw += a.dt_bias[h];
-    v = a.softplus ? softplusf_(raw) : raw;
-    v = fminf(fmaxf(v, a.dt_min), a.dt_max);
-  }
-  float x = v * (a.a_log ? -__expf(a.A[h]) : a.A[h]);
   // seq_idx: a sequence start is a decay to zero.  Adding kSeqBreak to the in-chunk cumsum makes every
   // e^{cum_i - cum_j} across the break (intra-chunk L, the decay of the carried state, the state inputs
   // of earlier tokens) underflow to exactly 0 in fp32, i.e. upstream's seq_idx masks, with no change to
   // any other term or to the backward (the offset is a constant: d cum / d dt is unchanged).
-  if (a.seq && t > 0 && t < a.L &&
-      a.seq[(int64_t)b * a.sqb + (int64_t)t * a.sql] != a.seq[(int64_t)b * a.sqb + (int64_t)(t - 1) * a.sql])
-    x += kSeqBreak;
+  const bool brk = a.seq && t > 0 && t < a.L &&
+                   a.seq[(int64_t)b * a.sqb + (int64_t)t * a.sql] != a.seq[(int64_t)b * a.sqb + (int64_t)(t - 1) * a.sql];
+  for (int h0 = 0; h0 < a.H; h0 += CS_HMAX) {
+    const int nh = min(CS_HMAX, a.H - h0);
+    if (h0 > 0) __syncthreads();  // the previous pass's readers are done
+    for (int e = threadIdx.x; e < Q * nh; e += 256) {
+      const int r = e / nh, hh = e - r * nh, tr = c * Q + r;
+      raw_s[r][hh] = tr < a.L ? ld_any(a.dt, a.dt_dtype, (int64_t)b * a.sdtb + (int64_t)tr * a.sdtl + (int64_t)(h0 + hh) * a.sdth)
+                              : 0.f;
+    }
+    __syncthreads();
+    for (int hh = w; hh < nh; hh += 4) {
+      const int h = h0 + hh;
+      float v = 0.f;
+      if (t < a.L) {
+        float raw = raw_s[lane][hh];
+        if (a.dt_bias) raw += a.dt_bias[h];
+        v = a.softplus ? softplusf_(raw) : raw;
+        v = fminf(fmaxf(v, a.dt_min), a.dt_max);
+      }
+      float x = v * (a.a_log ? -__expf(a.A[h]) : a.A[h]);
+      if (brk) x += kSeqBreak;
 #pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const float y = __shfl_up(x, off, 64);
-    if (lane >= off) x += y;
+      for (int off = 1; off < 64; off <<= 1) {
+        const float y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+      }
+      const int64_t o = ((int64_t)b * a.H + h) * a.Lp + t;
+      a.dtp[o] = v;
+      a.cum[o] = x;
+    }
   }
-  const int64_t o = ((int64_t)b * a.H + h) * a.Lp + t;
-  a.dtp[o] = v;
-  a.cum[o] = x;
 }
 
 // ---- register-staged tile loads (issue early, write to LDS late: latency hides under the MFMAs) ----
@@ -492,6 +509,10 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
         const bool inside = (v >= a.dt_min) && (v <= a.dt_max);
         gdt = inside ? ddt * (a.softplus ? sigmoidf_(raw) : 1.f) : 0.f;
         st_any(a.ddt, a.ddt_dtype, (int64_t)b * a.sddtb + (int64_t)t * a.sddtl + (int64_t)h * a.sddth, gdt);
+        if (a.ddt_zero_pad && h == 0) {  // the row's pad columns past the H dt columns: 16-B stores (host-checked)
+          bf16_t* pr = reinterpret_cast<bf16_t*>(a.ddt) + (int64_t)b * a.sddtb + (int64_t)t * a.sddtl + a.H;
+          for (int k = 0; k < a.ddt_zero_pad; k += 8) *reinterpret_cast<uint4*>(pr + k) = make_uint4(0u, 0u, 0u, 0u);
+        }
       }
       const float dbp = wave_sum(gdt);
       if (l == 0) {
@@ -863,8 +884,7 @@ hipError_t launch_ssd_fwd_f32(const SSDF32Args& a, hipStream_t st) {
 }
 
 hipError_t launch_ssd_fwd(const SSDArgs& a, hipStream_t st) {
-  const int64_t waves = (int64_t)a.B * a.H * a.nc;
-  hipLaunchKernelGGL(ssd_cumsum_k, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(ssd_cumsum_k, dim3((unsigned)((int64_t)a.B * a.nc)), dim3(256), 0, st, a);
   MAMBA_HIP_CHECK(hipGetLastError());
   N_SWITCH(a.N, hipLaunchKernelGGL(ssd_fused_fwd_k<NN>, dim3(a.H, a.B), dim3(256), 0, st, a));
   return hipGetLastError();

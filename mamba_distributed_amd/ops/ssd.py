@@ -186,8 +186,8 @@ class _Mamba2InnerFn(torch.autograd.Function):
         if rs > dproj and rs % 64 == 0 and zxbcdt.stride(0) == l * rs:
             # zxbcdt is the column view of a padded in_proj output (ops/linear.py): write d(zxbcdt) into the
             # same layout with zero pad columns, so the in_proj input gradient runs on 128-B aligned rows
+            # (the pad columns are zeroed by the SSD chunk backward, beside the dt gradient it writes: ddt_zero_pad)
             dz_full = torch.empty(b, l, rs, device=zxbcdt.device, dtype=zxbcdt.dtype)
-            dz_full[..., dproj:].zero_()
             dz_all = dz_full[..., :dproj]
         else:
             dz_full = None
@@ -216,7 +216,8 @@ class _Mamba2InnerFn(torch.autograd.Function):
                         dxBC_c[..., :di].unflatten(-1, (H, headdim)),
                         dz_all[..., di + conv_dim:],
                         dxBC_c[..., di:di + gn].unflatten(-1, (ngroups, d_state)),
-                        dxBC_c[..., di + gn:].unflatten(-1, (ngroups, d_state)), a_log, *(d_s or (None, 0)))
+                        dxBC_c[..., di + gn:].unflatten(-1, (ngroups, d_state)), a_log, *(d_s or (None, 0)),
+                        (rs - dproj) if dz_full is not None else 0)
         _, _, dA, _, _, dD, ddt_bias, dinit = g
         xBC = zxbcdt[..., di:di + conv_dim]
         if seq_idx is None:

@@ -426,6 +426,51 @@ def test_mamba2_padded_inproj_vs_reference(cuda, monkeypatch, engine, pad):
     assert not bad, bad
 
 
+def test_padded_inproj_grad_pad_columns_zeroed_by_ssd_bwd(cuda, monkeypatch):
+    """The padded in_proj gradient buffer's pad columns are written (zeros) by the SSD chunk backward
+    (ddt_zero_pad), not by a separate fill: with the buffer allocated NaN-filled, the pad comes back exactly 0 and
+    the d(zxbcdt) view equals the unpadded run's."""
+    import importlib
+    ssd_mod = importlib.import_module("mamba_distributed_amd.ops.ssd")
+    lin = importlib.import_module("mamba_distributed_amd.ops.linear")
+    torch.manual_seed(5)
+    b, l, H, P, N = 2, 256, 24, 64, 128
+    di = H * P
+    dproj = 2 * di + 2 * N + H
+    rs = (dproj + 63) // 64 * 64
+    full = (torch.randn(b, l, rs, device=cuda) * 0.5).to(torch.bfloat16)
+    zx_pad = full[..., :dproj]
+    zx = zx_pad.contiguous()
+    conv_w = torch.randn(di + 2 * N, 1, 4, device=cuda) * 0.3
+    conv_b = torch.randn(di + 2 * N, device=cuda) * 0.1
+    dt_bias = torch.randn(H, device=cuda) * 0.3
+    A = -torch.rand(H, device=cuda) * 4 - 0.5
+    D = torch.randn(H, device=cuda)
+    nw = torch.rand(di, device=cuda) + 0.5
+    seen = []
+    monkeypatch.setattr(lin, "register_zero_padded_grad", lambda t: seen.append(t))
+
+    class _NanEmpty:  # ssd.py's torch, with empty() NaN-filled
+        def __getattr__(self, n):
+            return getattr(torch, n)
+
+        def empty(self, *size, **kw):
+            return torch.full(size, float("nan"), **kw)
+    monkeypatch.setattr(ssd_mod, "torch", _NanEmpty())
+    grads = []
+    for z in (zx_pad, zx):
+        zl = z.detach().requires_grad_(True)
+        y = ssd_mod.mamba2_inner_fn(zl, conv_w, conv_b, dt_bias, A, D, nw, 1e-5, P, 1, N)
+        g = torch.randn(y.shape, device=cuda, generator=torch.Generator(device=cuda).manual_seed(1)).to(y.dtype)
+        y.backward(g)
+        grads.append(zl.grad)
+    assert len(seen) == 1, len(seen)
+    pad = seen[0][..., dproj:]
+    assert pad.shape[-1] == rs - dproj and (pad == 0).all()
+    assert torch.isfinite(grads[0].float()).all()
+    assert torch.equal(grads[0], grads[1])
+
+
 def test_decode_update_ops(cuda):
     from mamba_distributed_amd.ops.conv1d import causal_conv1d_update
     from mamba_distributed_amd.ops.selective_scan import selective_state_update
