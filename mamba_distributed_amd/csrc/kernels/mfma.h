@@ -111,6 +111,23 @@ __device__ __forceinline__ void acc_to_lds(bf16_t* lds, int ld, int r0, int c0, 
   for (int r = 0; r < 4; ++r) lds[(r0 + 4 * (l >> 4) + r) * ld + c0 + (l & 15)] = f2bf(a[r]);
 }
 
+// Same tile as 4-byte column pairs: lanes li and li^1 swap two values (DPP quad_perm [1,0,3,2]) so the even lane
+// writes rows 4g, 4g+1 and the odd lane rows 4g+2, 4g+3 at columns (li & ~1, li | 1): 2 ds_write_b32 per lane
+// instead of 4 ds_write_b16, and no dword is shared by two lanes.  With a row pitch of 4 mod 16 dwords (e.g.
+// 136 or 72 bf16) the 32 lanes of each half hit 32 distinct banks.
+__device__ __forceinline__ void acc_to_lds_pk(bf16_t* lds, int ld, int r0, int c0, f32x4 a) {
+  const int l = threadIdx.x & 63, li = l & 15, g = l >> 4;
+  const bool odd = li & 1;
+  const float s0 = odd ? a[0] : a[2], s1 = odd ? a[1] : a[3];
+  const float p0 = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, s0), 0xB1, 0xF, 0xF, false));
+  const float p1 = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, s1), 0xB1, 0xF, 0xF, false));
+  const int ra = r0 + 4 * g + (odd ? 2 : 0), col = c0 + (li & ~1);
+  const float e0 = odd ? p0 : a[0], e1 = odd ? a[2] : p0;  // row ra
+  const float f0 = odd ? p1 : a[1], f1 = odd ? a[3] : p1;  // row ra + 1
+  *reinterpret_cast<uint32_t*>(lds + ra * ld + col) = pack2(e0, e1);
+  *reinterpret_cast<uint32_t*>(lds + (ra + 1) * ld + col) = pack2(f0, f1);
+}
+
 // LDS [R][ld] bf16 -> global rows (row stride gs), rows >= valid skipped
 template <int R, int Cn>
 __device__ __forceinline__ void store_tile(bf16_t* g, int64_t gs, const bf16_t* lds, int ld, int valid) {

@@ -167,8 +167,9 @@ __global__ __launch_bounds__(256) void ssd_fused_fwd_k(SSDArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t Cs[Q * LDN];
   __shared__ __attribute__((aligned(16))) bf16_t Bs[Q * LDN];
   __shared__ __attribute__((aligned(16))) bf16_t Ss[P * LDN];
+  constexpr int LDY = P + 8;  // Y staging: written as column pairs (acc_to_lds_pk), read as 16-B rows only
   __shared__ __attribute__((aligned(16))) bf16_t Xs[Q * LD64];
-  __shared__ __attribute__((aligned(16))) bf16_t Os[Q * LD64];
+  __shared__ __attribute__((aligned(16))) bf16_t Os[Q * LDY];
   __shared__ __attribute__((aligned(16))) float cumr[Q], dtr[Q], wjr[Q];  // wjr = e^{cl-cum_j} dt_j
   const int h = blockIdx.x, b = blockIdx.y;
   const int g = h / (a.H / a.G);
@@ -209,8 +210,8 @@ __global__ __launch_bounds__(256) void ssd_fused_fwd_k(SSDArgs a) {
     const int row = 16 * w + (l >> 2), col = 16 * (l & 3);
     if (row < min(Q, a.L - cc * Q)) {
       bf16_t* yg = a.y + (int64_t)b * a.syb + (int64_t)(cc * Q + row) * a.syl + (int64_t)h * a.syh + col;
-      *reinterpret_cast<uint4*>(yg) = *reinterpret_cast<const uint4*>(Os + row * LD64 + col);
-      *reinterpret_cast<uint4*>(yg + 8) = *reinterpret_cast<const uint4*>(Os + row * LD64 + col + 8);
+      *reinterpret_cast<uint4*>(yg) = *reinterpret_cast<const uint4*>(Os + row * LDY + col);
+      *reinterpret_cast<uint4*>(yg + 8) = *reinterpret_cast<const uint4*>(Os + row * LDY + col + 8);
     }
   };
   prefetch(0);
@@ -294,9 +295,10 @@ __global__ __launch_bounds__(256) void ssd_fused_fwd_k(SSDArgs a) {
 #pragma unroll
     for (int pt = 0; pt < 4; ++pt) {
       const bf16x4 xr = acc_rows4(Xs, LD64, 16 * w, 16 * pt);
+      f32x4 yv;
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        Os[(16 * w + 4 * lg + r) * LD64 + 16 * pt + li] = f2bf(acc[pt][r] + Dh * (float)xr[r]);
+      for (int r = 0; r < 4; ++r) yv[r] = acc[pt][r] + Dh * (float)xr[r];
+      acc_to_lds_pk(Os, LDY, 16 * w, 16 * pt, yv);
     }
     // ---- S_{c+1} = e^{cl} S_c + (X o w)^T B
     const float decay = __expf(cl);
@@ -330,10 +332,11 @@ __global__ __launch_bounds__(256) void ssd_fused_fwd_k(SSDArgs a) {
 template <int N>
 __global__ __launch_bounds__(256) void ssd_dstate_bwd_k(SSDArgs a) {
   constexpr int LDN = N + 16;
+  constexpr int LDO = N + 8;  // dS staging: written as column pairs (acc_to_lds_pk), read as 16-B rows only
   constexpr int NTS = N / 16;
   __shared__ __attribute__((aligned(16))) bf16_t Ys[Q * LD64];
   __shared__ __attribute__((aligned(16))) bf16_t Cs[Q * LDN];
-  __shared__ __attribute__((aligned(16))) bf16_t Os[P * LDN];
+  __shared__ __attribute__((aligned(16))) bf16_t Os[P * LDO];
   __shared__ float er[Q];
   const int h = blockIdx.x, b = blockIdx.y;
   const int g = h / (a.H / a.G);
@@ -367,7 +370,7 @@ __global__ __launch_bounds__(256) void ssd_dstate_bwd_k(SSDArgs a) {
   prefetch(a.nc - 1);
   for (int c = a.nc - 1; c >= 0; --c) {
 #pragma unroll
-    for (int nt = 0; nt < NTS; ++nt) acc_to_lds(Os, LDN, 16 * w, 16 * nt, acc[nt]);
+    for (int nt = 0; nt < NTS; ++nt) acc_to_lds_pk(Os, LDO, 16 * w, 16 * nt, acc[nt]);
     if (threadIdx.x < Q) er[threadIdx.x] = __expf(pe);
     const float decay = __expf(pl);
     __syncthreads();
@@ -375,7 +378,7 @@ __global__ __launch_bounds__(256) void ssd_dstate_bwd_k(SSDArgs a) {
     // loads: vmcnt completes in order, so stores issued before a wait would be waited for too
     py.store(Ys, LD64, er);
     pcs.store(Cs, LDN);
-    store_tile<P, N>(a.dstates + ((((int64_t)b * a.nc + c) * a.H + h) * P) * N, N, Os, LDN, P);
+    store_tile<P, N>(a.dstates + ((((int64_t)b * a.nc + c) * a.H + h) * P) * N, N, Os, LDO, P);
     if (c > 0) prefetch(c - 1);
     __syncthreads();
 #pragma unroll
