@@ -128,6 +128,10 @@ def _lib_wgrad_acc(dw: torch.Tensor, g: torch.Tensor, h: torch.Tensor, first: bo
     """dw (fp32) (+)= g^T h on the library: fp32 output straight from the GEMM where torch exposes it (no bf16
     rounding of the chunk's product and no separate add), else a bf16 product added in fp32."""
     if _F32_OUT[0] is None:
+        import os
+        if os.environ.get("MAMBA_AMD_LM_DW_F32", "1") == "0":
+            _F32_OUT[0] = False
+            return _lib_wgrad_acc(dw, g, h, first)
         try:
             torch.mm(g[:8].t(), h[:8], out_dtype=torch.float32)
             _F32_OUT[0] = True

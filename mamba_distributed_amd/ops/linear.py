@@ -42,7 +42,8 @@ def _wgrad_native(p, dy2: torch.Tensor, x2: torch.Tensor, lb: int = 1):
     Q = x2.shape[1] if lb == 1 else x2.shape[0]
     S = ops.gp_splits(P, Q, T)
     d = grad_accum.deferred(p, "wgrad", (S, P, Q), dy2.device)
-    if d is None and lb == 1 and grad_accum.accumulable(p) and p.grad.dtype == torch.float32 and p.grad.is_contiguous():
+    if (d is None and lb == 1 and _wgrad_inplace(dy2.device) and grad_accum.accumulable(p) and p.grad.dtype == torch.float32
+            and p.grad.is_contiguous()):
         # not deferred (wide models: auto_defer_reduce) on a no-sync micro-step: the split-K wgrad kernel adds
         # its fixed-order slab sum straight into p.grad on the weight-gradient side stream, beside the rest of
         # the backward (the round-1 path; running it on the main stream cost Mamba-2 1.4B 89k -> 84k tok/s,
@@ -81,6 +82,33 @@ def _wgrad_native(p, dy2: torch.Tensor, x2: torch.Tensor, lb: int = 1):
     dw = torch.empty(P, Q, device=dy2.device, dtype=torch.float32)
     ops.gp_reduce(buf, dw, False)
     return dw
+
+
+_INPLACE_STATE: dict = {}   # device index -> [calls until the next re-check, decision, device bytes]
+
+
+def _wgrad_inplace(dev) -> bool:
+    """Non-deferred no-sync micro-steps: the split-K wgrad adds into p.grad in place on the side stream, or (False)
+    transient fp32 slabs on the persistent engine, reduced on the main stream. MAMBA_AMD_WGRAD_INPLACE=1/0 forces
+    either; auto takes the side stream while the allocated peak stays under 70% of the device and the caching
+    allocator has never had to retry (re-checked every 64 calls: memory_stats() is not free). The side-stream form
+    keeps dy/x alive (record_stream) past the main stream's frees; near capacity that turns into allocator
+    retries, which synchronise the device: Mamba-2 2.8B @ 8192 (222 GiB peak) ran 29.6k tok/s with it (17
+    retries) vs 46.8k without, while 1.4B @ 1024 (130 GiB) gains ~8% from it (profiles/r3/ab15_*)."""
+    import os
+    env = os.environ.get("MAMBA_AMD_WGRAD_INPLACE", "auto")
+    if env in ("0", "1"):
+        return env == "1"
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    st = _INPLACE_STATE.get(key)
+    if st is None:
+        st = _INPLACE_STATE[key] = [0, True, torch.cuda.get_device_properties(key).total_memory]
+    if st[0] <= 0:
+        s = torch.cuda.memory_stats(key)
+        st[1] = (s.get("allocated_bytes.all.peak", 0) < 0.7 * st[2]) and s.get("num_alloc_retries", 0) == 0
+        st[0] = 64
+    st[0] -= 1
+    return st[1]
 
 
 def _proj_engine() -> str:
