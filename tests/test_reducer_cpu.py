@@ -48,3 +48,31 @@ def test_reducer_flat_views_and_clip_match_torch(world1):
         torch.testing.assert_close(n1, n0, rtol=1e-5, atol=1e-6)
         for (k, p), q in zip(m.named_parameters(), ref.parameters()):
             torch.testing.assert_close(p.grad, q.grad, rtol=1e-5, atol=1e-7, msg=k)
+
+
+def test_wgrad_inplace_policy_follows_allocator_headroom(monkeypatch):
+    """ops/linear.py::_wgrad_inplace (auto): the side-stream in-place weight gradient only while the allocated
+    peak is < 70% of the device and the allocator never retried; re-checked every 64 calls; env forces either
+    (profiles/r3/ab15_2.8b_regression_fix.txt). The CUDA queries are faked, so this runs on CPU."""
+    import types
+    from mamba_distributed_amd.ops import linear
+    stats = {"allocated_bytes.all.peak": 100, "num_alloc_retries": 0}
+    monkeypatch.setattr(torch.cuda, "get_device_properties", lambda i: types.SimpleNamespace(total_memory=1000))
+    monkeypatch.setattr(torch.cuda, "memory_stats", lambda i: dict(stats))
+    monkeypatch.setattr(linear, "_INPLACE_STATE", {})
+    monkeypatch.delenv("MAMBA_AMD_WGRAD_INPLACE", raising=False)
+    dev = torch.device("cuda", 0)
+    assert linear._wgrad_inplace(dev)
+    stats["allocated_bytes.all.peak"] = 800       # 80% of the device: slabs, but only after the re-check
+    assert all(linear._wgrad_inplace(dev) for _ in range(63))
+    assert not linear._wgrad_inplace(dev)
+    monkeypatch.setattr(linear, "_INPLACE_STATE", {})
+    stats["allocated_bytes.all.peak"] = 100
+    stats["num_alloc_retries"] = 3                # any allocator retry turns it off
+    assert not linear._wgrad_inplace(dev)
+    monkeypatch.setenv("MAMBA_AMD_WGRAD_INPLACE", "1")
+    assert linear._wgrad_inplace(dev)
+    monkeypatch.setenv("MAMBA_AMD_WGRAD_INPLACE", "0")
+    stats["num_alloc_retries"] = 0
+    monkeypatch.setattr(linear, "_INPLACE_STATE", {})
+    assert not linear._wgrad_inplace(dev)
