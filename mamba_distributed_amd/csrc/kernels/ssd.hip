@@ -623,6 +623,7 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
       yr[q] = acc_rows4(dYs, LD64, 16 * w, 16 * (2 * half + q));
     }
     float dDp = 0.f, usum = 0.f;
+    f32x4 ov[2];  // dX tile values, staged to Os as 4-byte column pairs after the row loop
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int j = 16 * w + 4 * lg + r;
@@ -633,10 +634,9 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
       float ddp = 0.f, up = 0.f, yp = 0.f;
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        const int p = 16 * (2 * half + q) + li;
         const float xv = (float)xr[q][r];
         const float dyv = (float)yr[q][r];
-        Os[j * LD64 + p] = f2bf(dt_ * dxd[q][r] + wj * bds[q][r] + Dh * dyv);
+        ov[q][r] = dt_ * dxd[q][r] + wj * bds[q][r] + Dh * dyv;
         ddp += xv * (dxd[q][r] + ej * bds[q][r]);
         up += xv * bds[q][r];
         yp += yo[q][r] * dyv;
@@ -651,6 +651,8 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
       }
       usum += up;
     }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) acc_to_lds_pk(Os, LD64, 16 * w, 16 * (2 * half + q), ov[q]);
     usum = rows_sum4(usum);  // the wave's U total over its 16 rows (x its p-half)
     if (l == 0) dcw[hh & 7][wid][Q - 1] += usum;
     dDp = wave_sum(dDp);
