@@ -59,61 +59,81 @@ __device__ __forceinline__ float multi_wave_sum(float (&v)[M], int lane, int& id
 
 // ---------------------------------------------------------------------------------------------
 // Shared GEMV core: out[r][o] = sum_k W[o][k] x[r][k] for the RPW rows o of this wave, every batch row r
-// (x staged in LDS as bf16).  The wave's first weight chunk of every row is loaded before the caller
-// stages x, so the HBM latency of the weight stream overlaps the staging.
+// (x staged in LDS as bf16).  The wave's weight chunks are loaded before the caller stages x, so the HBM latency
+// of the weight stream overlaps the staging.
 typedef __bf16 bf2v __attribute__((ext_vector_type(2)));
 
 template <int RPW, int MB>
 struct GemvRows {
-  uint4 w0[RPW];
+  // The first KC 512-element chunks of every row (K <= 2048 at 280M-2.8B widths) are all loaded before the caller
+  // stages x: one HBM round trip per kernel instead of one per chunk (a decode step streams ~560 MB of cold
+  // weights; with one wave per SIMD nothing else hides a per-chunk wait).  Chunks past KC load in the loop.
+  static constexpr int KC = 4;
+  uint4 w0[KC][RPW];
   __device__ __forceinline__ void prefetch(const bf16_t* W, int o0, int n_out, int K, int lane) {
 #pragma unroll
-    for (int q = 0; q < RPW; ++q)
-      w0[q] = (o0 + q < n_out && lane * 8 < K) ? *reinterpret_cast<const uint4*>(W + (int64_t)(o0 + q) * K + lane * 8)
-                                              : make_uint4(0, 0, 0, 0);
+    for (int c = 0; c < KC; ++c)
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) {
+        const int k = lane * 8 + 512 * c;
+        w0[c][q] = (o0 + q < n_out && k < K) ? *reinterpret_cast<const uint4*>(W + (int64_t)(o0 + q) * K + k)
+                                             : make_uint4(0, 0, 0, 0);
+      }
   }
   // acc[q * MB + r]: row o0 + q, batch row r (rows r >= b stay zero).  bf16 pairs go straight into
   // v_dot2c_f32_bf16 (2 products per instruction, no unpacking of weights or activations).
+  __device__ __forceinline__ void chunk(const uint4 (&u)[RPW], int k, int K, const bf16_t* xs, int b,
+                                        float (&acc)[RPW * MB]) {
+    bf2v wv[RPW][4];
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      wv[q][0] = __builtin_bit_cast(bf2v, u[q].x);
+      wv[q][1] = __builtin_bit_cast(bf2v, u[q].y);
+      wv[q][2] = __builtin_bit_cast(bf2v, u[q].z);
+      wv[q][3] = __builtin_bit_cast(bf2v, u[q].w);
+    }
+#pragma unroll
+    for (int r = 0; r < MB; ++r) {
+      if (r < b) {
+        const uint4 xu = *reinterpret_cast<const uint4*>(xs + r * K + k);
+        const bf2v x0 = __builtin_bit_cast(bf2v, xu.x), x1 = __builtin_bit_cast(bf2v, xu.y);
+        const bf2v x2 = __builtin_bit_cast(bf2v, xu.z), x3 = __builtin_bit_cast(bf2v, xu.w);
+#pragma unroll
+        for (int q = 0; q < RPW; ++q) {
+          float a = acc[q * MB + r];
+          a = __builtin_amdgcn_fdot2_f32_bf16(wv[q][0], x0, a, false);
+          a = __builtin_amdgcn_fdot2_f32_bf16(wv[q][1], x1, a, false);
+          a = __builtin_amdgcn_fdot2_f32_bf16(wv[q][2], x2, a, false);
+          a = __builtin_amdgcn_fdot2_f32_bf16(wv[q][3], x3, a, false);
+          acc[q * MB + r] = a;
+        }
+      }
+    }
+  }
   __device__ __forceinline__ void run(const bf16_t* W, int o0, int n_out, int K, int lane, const bf16_t* xs, int b,
                                       float (&acc)[RPW * MB]) {
 #pragma unroll
     for (int i = 0; i < RPW * MB; ++i) acc[i] = 0.f;
-    for (int k = lane * 8, c = 0; k < K; k += 512, ++c) {  // K % 8 == 0
-      bf2v wv[RPW][4];
 #pragma unroll
-      for (int q = 0; q < RPW; ++q) {
-        const uint4 u = (c == 0) ? w0[q]
-                                 : ((o0 + q < n_out) ? *reinterpret_cast<const uint4*>(W + (int64_t)(o0 + q) * K + k)
-                                                     : make_uint4(0, 0, 0, 0));
-        wv[q][0] = __builtin_bit_cast(bf2v, u.x);
-        wv[q][1] = __builtin_bit_cast(bf2v, u.y);
-        wv[q][2] = __builtin_bit_cast(bf2v, u.z);
-        wv[q][3] = __builtin_bit_cast(bf2v, u.w);
-      }
+    for (int c = 0; c < KC; ++c) {  // K % 8 == 0
+      const int k = lane * 8 + 512 * c;
+      if (k < K) chunk(w0[c], k, K, xs, b, acc);
+    }
+    for (int k = lane * 8 + 512 * KC; k < K; k += 512) {
+      uint4 u[RPW];
 #pragma unroll
-      for (int r = 0; r < MB; ++r) {
-        if (r < b) {
-          const uint4 xu = *reinterpret_cast<const uint4*>(xs + r * K + k);
-          const bf2v x0 = __builtin_bit_cast(bf2v, xu.x), x1 = __builtin_bit_cast(bf2v, xu.y);
-          const bf2v x2 = __builtin_bit_cast(bf2v, xu.z), x3 = __builtin_bit_cast(bf2v, xu.w);
-#pragma unroll
-          for (int q = 0; q < RPW; ++q) {
-            float a = acc[q * MB + r];
-            a = __builtin_amdgcn_fdot2_f32_bf16(wv[q][0], x0, a, false);
-            a = __builtin_amdgcn_fdot2_f32_bf16(wv[q][1], x1, a, false);
-            a = __builtin_amdgcn_fdot2_f32_bf16(wv[q][2], x2, a, false);
-            a = __builtin_amdgcn_fdot2_f32_bf16(wv[q][3], x3, a, false);
-            acc[q * MB + r] = a;
-          }
-        }
-      }
+      for (int q = 0; q < RPW; ++q)
+        u[q] = (o0 + q < n_out) ? *reinterpret_cast<const uint4*>(W + (int64_t)(o0 + q) * K + k) : make_uint4(0, 0, 0, 0);
+      chunk(u, k, K, xs, b, acc);
     }
   }
 };
 
 // K1.  hn (b, d) bf16 = RMSNorm(residual + h) * w from the add+RMSNorm kernel; grid ceil(n_out / (4 RPW)).
 // LDS: hn staged (b * d * 2 <= 64 KiB, host-checked).
-constexpr int K1_RPW = 4;
+// Output rows per wave: 4, or 2 at 16 batch rows -- 4 x 16 accumulators went to scratch (272 B per lane) and a
+// narrower wave also doubles the grid (3392 in_proj rows: 212 -> 424 workgroups for 256 CUs).
+constexpr int k1_rpw(int mb) { return mb >= 16 ? 2 : 4; }
 template <int MB>  // batch-row capacity (1, 4 or 16); the transpose-reduce leaves one (row, batch) per lane
 __global__ __launch_bounds__(256) void dec_inproj_k(const bf16_t* __restrict__ hn, const bf16_t* __restrict__ W,
                                                     int n_out, int d, int b, float* __restrict__ zxbcdt, int conv_lo,
@@ -123,6 +143,7 @@ __global__ __launch_bounds__(256) void dec_inproj_k(const bf16_t* __restrict__ h
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* xs = reinterpret_cast<bf16_t*>(smem);  // [b][d]
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  constexpr int K1_RPW = k1_rpw(MB);
   const int o0 = (blockIdx.x * 4 + wave) * K1_RPW;
   GemvRows<K1_RPW, MB> gv;
   gv.prefetch(W, o0, n_out, d, lane);
@@ -219,7 +240,8 @@ __global__ __launch_bounds__(256) void dec_ssm_k(const float* __restrict__ zxbcd
 
 // ---------------------------------------------------------------------------------------------
 // K3.  grid: ceil(d_model / (4 RPW)) workgroups; LDS xn[b][di] bf16 (host-checked <= 64 KiB).
-constexpr int K3_RPW = 2;
+// Output rows per wave: 2, or 1 at 16 batch rows (d_model 768: 96 -> 192 workgroups for 256 CUs).
+constexpr int k3_rpw(int mb) { return mb >= 16 ? 1 : 2; }
 // The gate-norm weight is folded into the weight on the host (W' = W diag(w), static during decode)
 // and rstd is a per-row scalar, so the GEMV runs on g as produced by K2 and the epilogue scales by
 // rstd:  out = rstd * (g W'^T)  ==  (g * rstd * w) W^T.
@@ -231,6 +253,7 @@ __global__ __launch_bounds__(256) void dec_outproj_k(const bf16_t* __restrict__ 
   bf16_t* xs = reinterpret_cast<bf16_t*>(smem);
   __shared__ float rstd_s[DEC_MAXB];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  constexpr int K3_RPW = k3_rpw(MB);
   const int o0 = (blockIdx.x * 4 + wave) * K3_RPW;
   GemvRows<K3_RPW, MB> gv;
   gv.prefetch(W, o0, d_out, di, lane);
@@ -273,10 +296,8 @@ hipError_t launch_decode_inproj(const void* hn, const void* W, int n_out, int d,
                                 int conv_hi, void* conv_state, int64_t csb, int64_t csc, int SL, const float* cw,
                                 const float* cb, int Wd, hipStream_t st) {
   if (b < 1 || b > DEC_MAXB || d % 8 || (size_t)b * d * 2 > 65536 || SL < Wd - 1) return hipErrorInvalidValue;
-  const int rows_per_wg = 4 * K1_RPW;
-  const dim3 grid((n_out + rows_per_wg - 1) / rows_per_wg);
   const size_t lds = (size_t)b * d * 2;
-#define DEC_K1(MB) hipLaunchKernelGGL(dec_inproj_k<MB>, grid, dim3(256), lds, st, (const bf16_t*)hn, (const bf16_t*)W, \
+#define DEC_K1(MB) hipLaunchKernelGGL(dec_inproj_k<MB>, dim3((n_out + 4 * k1_rpw(MB) - 1) / (4 * k1_rpw(MB))), dim3(256), lds, st, (const bf16_t*)hn, (const bf16_t*)W, \
                                       n_out, d, b, zxbcdt, conv_lo, conv_hi, (bf16_t*)conv_state, csb, csc, SL, cw, cb, Wd)
   if (b == 1) DEC_K1(1);
   else if (b <= 4) DEC_K1(4);
@@ -303,10 +324,8 @@ hipError_t launch_decode_ssm(const float* zxbcdt, int n_out, float* state, const
 hipError_t launch_decode_outproj(const void* g, const float* part, int nparts, float eps, const void* W, int d_out,
                                  int di, int b, void* out, hipStream_t st) {
   if (b < 1 || b > DEC_MAXB || di % 8 || (size_t)b * di * 2 > 65536) return hipErrorInvalidValue;
-  const int rows_per_wg = 4 * K3_RPW;
-  const dim3 grid((d_out + rows_per_wg - 1) / rows_per_wg);
   const size_t lds = (size_t)b * di * 2;
-#define DEC_K3(MB) hipLaunchKernelGGL(dec_outproj_k<MB>, grid, dim3(256), lds, st, (const bf16_t*)g, part, nparts, \
+#define DEC_K3(MB) hipLaunchKernelGGL(dec_outproj_k<MB>, dim3((d_out + 4 * k3_rpw(MB) - 1) / (4 * k3_rpw(MB))), dim3(256), lds, st, (const bf16_t*)g, part, nparts, \
                                       eps, (const bf16_t*)W, d_out, di, b, (bf16_t*)out)
   if (b == 1) DEC_K3(1);
   else if (b <= 4) DEC_K3(4);

@@ -522,7 +522,7 @@ def test_graphed_decode_matches_eager(cuda, layer):
     assert rel(lg, full) < 1e-3
 
 
-@pytest.mark.parametrize("batch", [1, 3])
+@pytest.mark.parametrize("batch", [1, 3, 9, 16])
 def test_fused_decode_matches_unfused(cuda, batch):
     """The fused 3-kernel Mamba-2 decode layer (csrc/kernels/decode.hip), HIP-graph replayed, tracks the
     unfused cached step of a bf16 model (logits and SSM states) and the full bf16 recompute."""
