@@ -946,6 +946,17 @@ Tensor gp_pk(Tensor A, Tensor B, optional<Tensor> out, int64_t la, int64_t lb, i
   return C;
 }
 
+// GEMM engine workgroup shape (8 or 4 waves): which = 0 the persistent engine, 1 the split-K engine;
+// w <= 0 only reads it
+int64_t gp_pk_waves(int64_t w, int64_t which) {
+  if (which == 1) {
+    if (w > 0) mamba_amd::set_gemm_pipe_waves((int)w);
+    return mamba_amd::gemm_pipe_waves();
+  }
+  if (w > 0) mamba_amd::set_gemm_pk_waves((int)w);
+  return mamba_amd::gemm_pk_waves();
+}
+
 int64_t wgrad_splits(int64_t M, int64_t P, int64_t Q) { return mamba_amd::gemm_wgrad_splits((int)M, (int)P, (int)Q); }
 int64_t gp_splits(int64_t M, int64_t N, int64_t K) { return mamba_amd::gemm_pipe_splits((int)M, (int)N, (int)K); }
 
@@ -1084,6 +1095,7 @@ TORCH_LIBRARY(mamba_amd, m) {
   m.def("wgrad_splits(int M, int P, int Q) -> int", &wgrad_splits);
   m.def("gp_mm(Tensor A, Tensor B, Tensor(a!)? out=None, int la=0, int lb=0, int mode=0, int splits=1, int bm=256) -> Tensor");
   m.def("gp_pk(Tensor A, Tensor B, Tensor(a!)? out=None, int la=0, int lb=0, int mode=0, Tensor? rowscale=None) -> Tensor");
+  m.def("gp_pk_waves(int w=0, int which=0) -> int", &gp_pk_waves);
   m.def("gp_splits(int M, int N, int K) -> int", &gp_splits);
   m.def("part_rows(str kind, int a, int b=0) -> int", &part_rows);
   m.def("gp_reduce(Tensor part, Tensor(a!) out, bool accumulate=False) -> ()");

@@ -126,11 +126,12 @@ struct GemmPipeArgs {
 // four LDS-DMAs or an MFMA waiting on a fragment read issued fewer than 16 MFMAs earlier.
 // (A persistent variant that streams the next output tile's K-tiles behind this one's was measured slower:
 // the dynamic buffer parity and tile bookkeeping cost more in the K-loop than the hidden epilogue gained.)
-template <int LA, int LB, int EPI>
-__global__ __launch_bounds__(512) void gemm_pipe_k(GemmPipeArgs a) {
-  // 8 waves as 2 x 4, each 128 x 64 of the 256 x 256 tile
-  constexpr int MI = 8, WN = 4, NT = 512;
-  constexpr int NJ = 4;  // 16-col tiles per wave
+// WN = 4: 8 waves as 2 x 4, each 128 x 64 of the 256 x 256 tile (two per SIMD); WN = 2: 4 waves of 128 x 128
+// (one per SIMD, 256 accumulator registers): half the LDS fragment reads per MFMA
+template <int LA, int LB, int EPI, int WN = 4>
+__global__ __launch_bounds__(128 * WN) void gemm_pipe_k(GemmPipeArgs a) {
+  constexpr int MI = 8, NT = 128 * WN;
+  constexpr int NJ = 16 / WN;  // 16-col tiles per wave
   constexpr int BM = 32 * MI, BN = 16 * NJ * WN;
   constexpr int SA = BM * 128, SB = BN * 128;  // bytes per K-tile image
   constexpr int SS = SA + SB;
@@ -371,14 +372,23 @@ struct GemmPkArgs {
 
 __device__ __attribute__((aligned(64))) uint4 g_pk_sink[64];  // epilogue stores of lanes outside C
 
-template <int MI, int NJ, bool RS, bool TAIL>
-__global__ __launch_bounds__(512) void gemm_pk_k(GemmPkArgs a) {
-  constexpr int NT = 512, WN = 4, MH = MI / 2;
-  constexpr int BM = 32 * MI, BN = 64 * NJ;  // NJ = 4: 256-wide tiles; NJ = 3: 192-wide (d_model = 768 outputs)
+// WN: waves along N (2 x WN waves).  WN = 4: 8 waves of (16 MI) x (16 NJ), two per SIMD; WN = 2: 4 waves of
+// 128 x 128 (MI = NJ = 8), one per SIMD with 256 accumulator registers each -- half the LDS fragment reads per
+// MFMA of the 8-wave form (16 reads per 64 MFMAs instead of 12 per 32).
+template <int MI, int NJ, bool RS, bool TAIL, int WN = 4>
+__global__ __launch_bounds__(128 * WN) void gemm_pk_k(GemmPkArgs a) {
+  constexpr int NT = 128 * WN, MH = MI / 2, NW = 2 * WN;
+  constexpr int BM = 32 * MI, BN = 16 * WN * NJ;  // WN 4: NJ = 4: 256-wide tiles; NJ = 3: 192-wide (d_model = 768 outputs)
   constexpr int SA = BM * 128, SB = BN * 128, SS = SA + SB;
-  constexpr int GA = BM / 64, GB = BN / 64, G = GA + GB;
-  constexpr int STG = 8 * 2048;
-  constexpr int NST = 2 * MI;  // epilogue store instructions per wave
+  constexpr int RPI = NT / 8;  // tile rows per DMA instruction (8 lanes per 128-B row)
+  constexpr int GA = BM / RPI, GB = BN / RPI, G = GA + GB;
+  constexpr int CH = 2 * NJ;              // 16-B chunks per staged accumulator row (16 NJ columns)
+  constexpr int PCH = (CH + 7) / 8 * 8;    // staged row pitch in chunks (the XOR swizzle permutes groups of 8)
+  constexpr int STW = 16 * PCH * 16;      // staging bytes per wave (16 rows)
+  constexpr int STG = NW * STW;
+  constexpr int SPI = (16 * CH + 63) / 64;  // epilogue store instructions per 16-row block
+  constexpr int NST = SPI * MI;             // epilogue store instructions per wave
+  static_assert(NST <= 63, "vmcnt range");
   __shared__ __attribute__((aligned(1024))) char smem[2 * SS + STG + 64];
   int* const claim = reinterpret_cast<int*>(smem + 2 * SS + STG);  // the claimed next tile, LDS-broadcast
 
@@ -392,8 +402,8 @@ __global__ __launch_bounds__(512) void gemm_pk_k(GemmPkArgs a) {
 
   const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, (short)0, (int)a.nbA, 0x00020000);
   const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)a.B, (short)0, (int)a.nbB, 0x00020000);
-  // KC operands: DMA instruction ii moves rows 64 ii + (tid >> 3) at 16-B chunk (tid & 7) ^ (row & 7)
-  // (64 ii does not change row & 7), so the lane part of every offset is one VGPR per operand
+  // KC operands: DMA instruction ii moves rows RPI ii + (tid >> 3) at 16-B chunk (tid & 7) ^ (row & 7)
+  // (RPI ii, a multiple of 32, does not change row & 7), so the lane part of every offset is one VGPR per operand
   const int lrow = tid >> 3, lch = (tid & 7) ^ (lrow & 7);
   const unsigned loA = (unsigned)(((int64_t)lrow * a.lda + 8 * lch) * 2);
   const unsigned loB = (unsigned)(((int64_t)lrow * a.ldb + 8 * lch) * 2);
@@ -417,7 +427,7 @@ __global__ __launch_bounds__(512) void gemm_pk_k(GemmPkArgs a) {
       const bool isA = i < GA;
       if ((part == 0 && !isA) || (part == 1 && isA)) continue;
       const int ii = isA ? i : i - GA;
-      unsigned v = isA ? loA + ba + (unsigned)(64 * ii * a.lda * 2) : loB + bb + (unsigned)(64 * ii * a.ldb * 2);
+      unsigned v = isA ? loA + ba + (unsigned)(RPI * ii * a.lda * 2) : loB + bb + (unsigned)(RPI * ii * a.ldb * 2);
       if (dead) v = 0xFFFFFFF0u;
       lds_void* dst = (lds_void*)(buf + (isA ? 0 : SA) + (ii * NT + wu * 64) * 16);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rA : rB, dst, 16, v, 0, 0, 0);
@@ -523,10 +533,9 @@ __global__ __launch_bounds__(512) void gemm_pk_k(GemmPkArgs a) {
       const int eam0 = (ew / WN) * (BM / 2), ebn0 = (ew % WN) * (BN / WN);
       int m0, n0;
       tile_mn(tile, m0, n0);
-      char* stg = smem + 2 * SS + ew * 2048;
+      char* stg = smem + 2 * SS + ew * STW;
       const int r = el & 15, q = el >> 4;
-      // staged row = 2 NJ 16-B chunks; store h covers chunk slots el + 64 h (slots past 16 rows go to the sink)
-      constexpr int CH = 2 * NJ;
+      // staged row = CH 16-B chunks; store h covers chunk slots el + 64 h (slots past 16 rows go to the sink)
       float rs[MI];
       if constexpr (RS) {
 #pragma unroll
@@ -539,17 +548,17 @@ __global__ __launch_bounds__(512) void gemm_pk_k(GemmPkArgs a) {
       for (int i = 0; i < MI; ++i) {
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
-          const int off = r * 128 + (((2 * j + (q >> 1)) ^ (r & 7)) << 4) + ((q & 1) << 3);
+          const int off = r * (PCH * 16) + (((2 * j + (q >> 1)) ^ (r & 7)) << 4) + ((q & 1) << 3);
           f32x4 v = acc[i][j];
           if constexpr (RS) v = v * rs[i];
           *reinterpret_cast<uint2*>(stg + off) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
         }
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < SPI; ++h) {
           const int sl = el + 64 * h;
-          const int row = CH == 8 ? sl >> 3 : sl / CH, cc = CH == 8 ? sl & 7 : sl % CH;
+          const int row = sl / CH, cc = sl % CH;
           const int rowc = row < 16 ? row : 15;
-          const uint4 v = *reinterpret_cast<const uint4*>(stg + rowc * 128 + ((cc ^ (rowc & 7)) << 4));
+          const uint4 v = *reinterpret_cast<const uint4*>(stg + rowc * (PCH * 16) + ((cc ^ (rowc & 7)) << 4));
           const int m = m0 + eam0 + 16 * i + row, n = n0 + ebn0 + 8 * cc;
           uint4* dst = (row < 16 && m < a.M && n < a.N) ? reinterpret_cast<uint4*>(a.C + (int64_t)m * a.ldc + n)
                                                        : &g_pk_sink[el];
@@ -586,6 +595,28 @@ __global__ void gp_reduce_k(const float* __restrict__ part, int S, int64_t strid
   *reinterpret_cast<float4*>(out + i) = s;
 }
 
+// waves per workgroup of the persistent engine: 8 (two per SIMD, 128 x 64 wave tiles) or 4 (one per SIMD, 128 x 128);
+// MAMBA_AMD_PK_WAVES sets the process default, set_gemm_pk_waves overrides it (A/B in one process)
+static int g_pk_waves = 0;
+int gemm_pk_waves() {
+  if (g_pk_waves == 0) {
+    const char* e = getenv("MAMBA_AMD_PK_WAVES");
+    g_pk_waves = (e && atoi(e) == 4) ? 4 : 8;
+  }
+  return g_pk_waves;
+}
+void set_gemm_pk_waves(int w) { g_pk_waves = (w == 4) ? 4 : 8; }
+// the same choice for the split-K / non-persistent engine (gemm_pipe_k: weight gradients), MAMBA_AMD_PIPE_WAVES
+static int g_pipe_waves = 0;
+int gemm_pipe_waves() {
+  if (g_pipe_waves == 0) {
+    const char* e = getenv("MAMBA_AMD_PIPE_WAVES");
+    g_pipe_waves = (e && atoi(e) == 4) ? 4 : 8;
+  }
+  return g_pipe_waves;
+}
+void set_gemm_pipe_waves(int w) { g_pipe_waves = (w == 4) ? 4 : 8; }
+
 bool gemm_pipe_supported(int la, int lb, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc) {
   if (M <= 0 || N <= 0 || K <= 0) return false;
   if (lda % 8 || ldb % 8 || ldc % 4 || N % 4) return false;
@@ -620,10 +651,18 @@ hipError_t launch_gemm_pipe(int la, int lb, const void* A, int64_t lda, const vo
   a.kslice = ((K + splits - 1) / splits + GP_BK - 1) / GP_BK * GP_BK;
   const int nwg = ((M + 255) / 256) * ((N + 255) / 256) * splits;
 #define GP_EPI(LA_, LB_)                                                                       \
-  switch (epi) {                                                                               \
-    case 0: hipLaunchKernelGGL((gemm_pipe_k<LA_, LB_, 0>), dim3(nwg), dim3(GP_NT), 0, st, a); break; \
-    case 1: hipLaunchKernelGGL((gemm_pipe_k<LA_, LB_, 1>), dim3(nwg), dim3(GP_NT), 0, st, a); break; \
-    default: hipLaunchKernelGGL((gemm_pipe_k<LA_, LB_, 2>), dim3(nwg), dim3(GP_NT), 0, st, a); break; \
+  if (gemm_pipe_waves() == 4) {                                                                \
+    switch (epi) {                                                                             \
+      case 0: hipLaunchKernelGGL((gemm_pipe_k<LA_, LB_, 0, 2>), dim3(nwg), dim3(256), 0, st, a); break; \
+      case 1: hipLaunchKernelGGL((gemm_pipe_k<LA_, LB_, 1, 2>), dim3(nwg), dim3(256), 0, st, a); break; \
+      default: hipLaunchKernelGGL((gemm_pipe_k<LA_, LB_, 2, 2>), dim3(nwg), dim3(256), 0, st, a); break; \
+    }                                                                                          \
+  } else {                                                                                     \
+    switch (epi) {                                                                             \
+      case 0: hipLaunchKernelGGL((gemm_pipe_k<LA_, LB_, 0>), dim3(nwg), dim3(GP_NT), 0, st, a); break; \
+      case 1: hipLaunchKernelGGL((gemm_pipe_k<LA_, LB_, 1>), dim3(nwg), dim3(GP_NT), 0, st, a); break; \
+      default: hipLaunchKernelGGL((gemm_pipe_k<LA_, LB_, 2>), dim3(nwg), dim3(GP_NT), 0, st, a); break; \
+    }                                                                                          \
   }
   if (la == 0 && lb == 0) { GP_EPI(0, 0) }
   else if (la == 0 && lb == 1) { GP_EPI(0, 1) }
@@ -644,6 +683,8 @@ static int cu_count() {
   return n;
 }
 
+
+
 bool gemm_pk_supported(int la, int lb, int epi, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc) {
   if (M <= 0 || N <= 0 || K <= 192) return false;  // >= 4 K-tiles
   if (la != 0 || lb != 0 || epi != 0) return false;  // instantiated: KC . KC, bf16 output
@@ -651,37 +692,49 @@ bool gemm_pk_supported(int la, int lb, int epi, int M, int N, int K, int64_t lda
   // every DMA byte offset, including the overhang of partial tiles, must stay below the out-of-range sentinel
   const int64_t kt = ((K + 63) / 64 + 1) / 2 * 2;
   const int64_t lim = ((int64_t)1 << 32) - 64;
-  const int64_t Mp = (M + 255) / 256 * 256, Np = (N + 255) / 256 * 256;
+  const int64_t Mp = (M + 255) / 256 * 256 + 256, Np = (N + 255) / 256 * 256 + 256;  // any tile shape's overhang
   return (Mp * lda + kt * 64) * 2 < lim && (Np * ldb + kt * 64) * 2 < lim;
 }
 
 // per-launch tile-claim counters: a ring of zeroed {next, done} pairs, each re-armed by its launch's last
-// workgroup; launches in flight at once (two micro-batch streams) never share a pair
-static int* pk_counters(int dev, int& slot) {
-  constexpr int R = 16384;
+// workgroup; launches in flight at once (two micro-batch streams) never share a pair.  Launches recorded into a
+// HIP graph take pairs from a separate, never-recycled range (a replayed graph keeps its baked pair, which an
+// eager launch must never reuse).  The buffer is allocated on the device's first eager launch; a first launch
+// inside stream capture fails loudly (run one eager launch, e.g. the warm-up step, before capturing).
+static int* pk_counters(int dev, hipStream_t st) {
+  constexpr int R = 16384, RC = 8192;  // eager ring, graph-captured range
   static int* bufs[16] = {};
   static unsigned seq[16] = {};
+  static unsigned cap[16] = {};
   if (dev < 0 || dev >= 16) return nullptr;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess) return nullptr;
+  const bool capturing = cs != hipStreamCaptureStatusNone;
   if (!bufs[dev]) {
+    if (capturing) return nullptr;
     void* p = nullptr;
-    if (hipMalloc(&p, R * 2 * sizeof(int)) != hipSuccess || hipMemset(p, 0, R * 2 * sizeof(int)) != hipSuccess)
+    if (hipMalloc(&p, (R + RC) * 2 * sizeof(int)) != hipSuccess || hipMemset(p, 0, (R + RC) * 2 * sizeof(int)) != hipSuccess)
       return nullptr;
     bufs[dev] = (int*)p;
   }
-  slot = (int)(seq[dev]++ % R);
+  if (capturing) {
+    if (cap[dev] >= (unsigned)RC) return nullptr;
+    return bufs[dev] + 2 * (R + (int)cap[dev]++);
+  }
+  const int slot = (int)(seq[dev]++ % R);
   return bufs[dev] + 2 * slot;
 }
 
 hipError_t launch_gemm_pk(int la, int lb, const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
                           int64_t ldc, int M, int N, int K, int epi, const float* rowscale, hipStream_t st) {
   if (!gemm_pk_supported(la, lb, epi, M, N, K, lda, ldb, ldc)) return hipErrorInvalidValue;
-  int dev = 0, slot = 0;
+  int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidValue;
   GemmPkArgs a;
   a.A = (const bf16_t*)A; a.lda = lda; a.B = (const bf16_t*)B; a.ldb = ldb;
   a.C = (bf16_t*)C; a.ldc = ldc; a.rowscale = rowscale;
-  a.ctr = pk_counters(dev, slot);
-  if (!a.ctr) return hipErrorOutOfMemory;
+  a.ctr = pk_counters(dev, st);
+  if (!a.ctr) return hipErrorNotReady;  // no counter pair: first launch under capture, or the captured range is spent
   a.nbA = (unsigned)(((int64_t)(M - 1) * lda + K) * 2);
   a.nbB = (unsigned)(((int64_t)(N - 1) * ldb + K) * 2);
   a.M = M; a.N = N; a.K = K;
@@ -702,11 +755,32 @@ hipError_t launch_gemm_pk(int la, int lb, const void* A, int64_t lda, const void
   a.tm = (M + bm - 1) / bm; a.tn = (N + bn - 1) / bn;
   a.ntiles = a.tm * a.tn;
   const bool tail = K % 64 != 0 || a.kte * 64 != K;
-  const int nwg = std::min(a.ntiles, ncu);
+  int nwg = std::min(a.ntiles, ncu);
 #define PK_L(MI_, NJ_, RS_)                                                                              \
   if (tail) hipLaunchKernelGGL((gemm_pk_k<MI_, NJ_, RS_, true>), dim3(nwg), dim3(512), 0, st, a);          \
   else hipLaunchKernelGGL((gemm_pk_k<MI_, NJ_, RS_, false>), dim3(nwg), dim3(512), 0, st, a)
-  if (bn == 192) {
+#define PK_L4(MI_, NJ_, RS_)                                                                              \
+  if (tail) hipLaunchKernelGGL((gemm_pk_k<MI_, NJ_, RS_, true, 2>), dim3(nwg), dim3(256), 0, st, a);       \
+  else hipLaunchKernelGGL((gemm_pk_k<MI_, NJ_, RS_, false, 2>), dim3(nwg), dim3(256), 0, st, a)
+  if (gemm_pk_waves() == 4) {
+    // 4-wave tiles (MAMBA_AMD_PK4_TILE): 0 = 256 x 256 (256 accumulators: hipcc shuffles AGPRs), 1 = 192 x 256,
+    // 2 = 256 x 224, 3 = 256 x 192
+    static int shape = -1;
+    if (shape < 0) { const char* e = getenv("MAMBA_AMD_PK4_TILE"); shape = e ? atoi(e) : 1; }
+    const int bm4 = shape == 1 ? 192 : 256, bn4 = shape == 2 ? 224 : shape == 3 ? 192 : 256;
+    a.tm = (M + bm4 - 1) / bm4; a.tn = (N + bn4 - 1) / bn4;
+    a.ntiles = a.tm * a.tn;
+    nwg = std::min(a.ntiles, ncu);
+    if (shape == 1) {
+      if (rowscale) { PK_L4(6, 8, true); } else { PK_L4(6, 8, false); }
+    } else if (shape == 2) {
+      if (rowscale) { PK_L4(8, 7, true); } else { PK_L4(8, 7, false); }
+    } else if (shape == 3) {
+      if (rowscale) { PK_L4(8, 6, true); } else { PK_L4(8, 6, false); }
+    } else {
+      if (rowscale) { PK_L4(8, 8, true); } else { PK_L4(8, 8, false); }
+    }
+  } else if (bn == 192) {
     if (rowscale) { PK_L(8, 3, true); } else { PK_L(8, 3, false); }
   } else if (bm == 256) {
     if (rowscale) { PK_L(8, 4, true); } else { PK_L(8, 4, false); }
@@ -714,6 +788,7 @@ hipError_t launch_gemm_pk(int la, int lb, const void* A, int64_t lda, const void
     if (rowscale) { PK_L(4, 4, true); } else { PK_L(4, 4, false); }
   }
 #undef PK_L
+#undef PK_L4
   return hipGetLastError();
 }
 

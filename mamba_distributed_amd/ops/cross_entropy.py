@@ -69,14 +69,16 @@ class _FusedLinearCEFn(torch.autograd.Function):
     The reference materialises the full fp32 logits (model.py:44-46)."""
 
     @staticmethod
-    def forward(ctx, h, weight, targets, ignore_index, compute_dtype, row_chunk):
+    def forward(ctx, h, weight, targets, ignore_index, compute_dtype, row_chunk, grad_enabled):
         h2 = h.reshape(-1, h.shape[-1]).to(compute_dtype)
         w = grad_accum.cached_cast(weight, compute_dtype)        # once per optimizer step
         t = targets.reshape(-1)
         M, K = h2.shape
         V = w.shape[0]
         inv = _inv_count(t, ignore_index)
-        need_h, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        # needs_input_grad reflects requires_grad even under no_grad (validation): skip the dh / dW products then
+        need_h = ctx.needs_input_grad[0] and grad_enabled
+        need_w = ctx.needs_input_grad[1] and grad_enabled
         nat_f, nat_h, nat_w = _lm_engines(h2, w)
         R = _row_chunk(M, V, row_chunk)
         buf = torch.empty(min(R, M), V, device=h2.device, dtype=compute_dtype)
@@ -114,11 +116,12 @@ class _FusedLinearCEFn(torch.autograd.Function):
         dh_, dw_ = ctx.saved_tensors
         g = gloss.to(torch.float32)
         dh = dw = None
-        if ctx.needs_input_grad[0]:
-            dh = dh_.mul_(g.to(dh_.dtype)).view(ctx.hshape).to(ctx.hdtype)
-        if ctx.needs_input_grad[1]:
-            dw = dw_[0].mul_(g).to(ctx.wdtype)
-        return dh, dw, None, None, None, None
+        # out of place: a second backward through the graph (retain_graph) must not scale the saved products twice
+        if ctx.needs_input_grad[0] and dh_ is not None:
+            dh = (dh_ * g.to(dh_.dtype)).view(ctx.hshape).to(ctx.hdtype)
+        if ctx.needs_input_grad[1] and dw_ is not None:
+            dw = (dw_[0] * g).to(ctx.wdtype)
+        return dh, dw, None, None, None, None, None
 
 
 _F32_OUT = [None]  # hipBLASLt bf16 x bf16 -> fp32 products (aten::mm.dtype / addmm.dtype) usable here
@@ -178,7 +181,8 @@ def _row_chunk(M: int, V: int, row_chunk=None) -> int:
 
 def fused_linear_cross_entropy(h, weight, targets, ignore_index=-100, compute_dtype=torch.bfloat16, row_chunk=None):
     if _ext.use_native(h):
-        return _FusedLinearCEFn.apply(h, weight, targets, ignore_index, compute_dtype, row_chunk)
+        return _FusedLinearCEFn.apply(h, weight, targets, ignore_index, compute_dtype, row_chunk,
+                                      torch.is_grad_enabled())
     logits = F.linear(h, weight.to(h.dtype))
     return F.cross_entropy(logits.float().view(-1, logits.size(-1)), targets.view(-1),
                            ignore_index=ignore_index)

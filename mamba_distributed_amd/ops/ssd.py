@@ -138,8 +138,12 @@ class _Mamba2InnerFn(torch.autograd.Function):
         di = H * headdim
         conv_dim = di + 2 * ngroups * d_state
         assert dproj == 2 * di + 2 * ngroups * d_state + H, "only d_mlp == 0 layouts are supported"
-        if zxbcdt.stride(-1) != 1:
-            zxbcdt = zxbcdt.contiguous()
+        if zxbcdt.stride(-1) != 1 or zxbcdt.stride(-2) % 8 or zxbcdt.stride(0) != l * zxbcdt.stride(-2):
+            # the native conv / SSD / norm kernels want 16-B aligned rows: an odd width (nheads % 8 != 0 without
+            # the padded in_proj) is copied into rows of a multiple of 8 columns
+            full = torch.empty(b, l, (dproj + 7) // 8 * 8, device=zxbcdt.device, dtype=zxbcdt.dtype)
+            full[..., :dproj].copy_(zxbcdt)
+            zxbcdt = full[..., :dproj]
         z = zxbcdt[..., :di]
         xBC = zxbcdt[..., di:di + conv_dim]
         dt = zxbcdt[..., di + conv_dim:]
@@ -183,7 +187,9 @@ class _Mamba2InnerFn(torch.autograd.Function):
         gn = ngroups * d_state
         conv_dim = di + 2 * gn
         rs = zxbcdt.stride(-2)
-        if rs > dproj and rs % 64 == 0 and zxbcdt.stride(0) == l * rs:
+        # (the pad must start 16-B aligned and span whole 8-column groups for the chunk backward's zero fill:
+        # dproj % 8 == 0, i.e. nheads % 8 == 0 at the default layout; other widths take the unpadded gradient)
+        if rs > dproj and rs % 64 == 0 and dproj % 8 == 0 and zxbcdt.stride(0) == l * rs:
             # zxbcdt is the column view of a padded in_proj output (ops/linear.py): write d(zxbcdt) into the
             # same layout with zero pad columns, so the in_proj input gradient runs on 128-B aligned rows
             # (the pad columns are zeroed by the SSD chunk backward, beside the dt gradient it writes: ddt_zero_pad)
@@ -191,7 +197,8 @@ class _Mamba2InnerFn(torch.autograd.Function):
             dz_all = dz_full[..., :dproj]
         else:
             dz_full = None
-            dz_all = torch.empty_like(zxbcdt)
+            # rows of a multiple of 8 columns (16-B aligned) for the gated-norm / SSD / conv gradient writers
+            dz_all = torch.empty(b, l, (dproj + 7) // 8 * 8, device=zxbcdt.device, dtype=zxbcdt.dtype)[..., :dproj]
         z = zxbcdt[..., :di]
         pw, pb, pdtb, pA, pD, pn = ctx.params
         dev = zxbcdt.device

@@ -13,7 +13,6 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import Optional, Tuple
 
-import weakref
 
 import torch
 
@@ -74,7 +73,21 @@ def sample(logits: torch.Tensor, top_k: int = 1, top_p: float = 0.0, min_p: floa
     return torch.multinomial(torch.softmax(work, dim=-1), num_samples=1).squeeze(-1)
 
 
-_DECODERS: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()  # model -> {(b, max_length, cg, dev): decoder}
+def _param_signature(model) -> tuple:
+    """Storage pointers and dtypes of every parameter: a captured graph reads these addresses, so a decoder is
+    only reused while none of them changed (``.to(dtype)``, ``.cuda()``, ``load_state_dict(assign=True)``)."""
+    return tuple((p.data_ptr(), p.dtype) for p in model.parameters())
+
+
+def _decoder_cache(model) -> dict:
+    """The model's decoder cache {(b, max_length, cg, dev): (signature, decoder)}, kept as a plain attribute of
+    the model itself: the model -> cache -> decoder -> model cycle is collected with the model (a module-level
+    WeakKeyDictionary whose values hold the model strongly never released it)."""
+    cache = model.__dict__.get("_amd_decoders")
+    if cache is None:
+        cache = {}
+        object.__setattr__(model, "_amd_decoders", cache)
+    return cache
 
 
 @torch.no_grad()
@@ -91,12 +104,16 @@ def decode(input_ids: torch.Tensor, model, max_length: int, top_k: int = 1, top_
     dev = input_ids.device
     # one decoder (caches + captured graph) per (batch, max_length, cg), kept on the model like upstream's
     # graph cache; reused calls reset the states and re-derive the fused step's weight copies
-    cache = _DECODERS.setdefault(model, {})
+    cache = _decoder_cache(model)
     key = (b, max_length, bool(cg), dev)
-    dec = cache.get(key)
-    if dec is None:
-        dec = cache[key] = GraphedDecoder(model, batch_size=b, max_seqlen=max_length, use_graph=None if cg else False)
+    sig = _param_signature(model)
+    ent = cache.get(key)
+    if ent is None or ent[0] != sig:
+        cache.pop(key, None)  # parameters moved or changed dtype: the captured graph reads stale addresses
+        dec = GraphedDecoder(model, batch_size=b, max_seqlen=max_length, use_graph=None if cg else False)
+        cache[key] = (sig, dec)
     else:
+        dec = ent[1]
         dec.refresh()
     seqs = [input_ids]
     scores = []

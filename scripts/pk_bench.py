@@ -69,16 +69,27 @@ def main():
         if name == "lm_dgrad" and m * K * 2 >= (1 << 32):  # operand past the engine's 4 GB offset range
             print(json.dumps({"case": name, "M": m, "skipped": "operand >= 4 GB"}), flush=True)
             continue
-        y = ops.gp_pk(A, B)
-        err = rel(y, ref)
-        # row scale (the gated-norm rstd folded out of the out_proj operand)
         rs = torch.rand(m, device=dev, generator=g) + 0.5
-        err_rs = rel(ops.gp_pk(A, B, None, 0, 0, 0, rs), ref.float() * rs[:, None])
-        res = {"case": name, "M": m, "N": N, "K": K, "rel_err": float(f"{err:.2e}"), "rel_err_rowscale": float(f"{err_rs:.2e}")}
+        res = {"case": name, "M": m, "N": N, "K": K}
+        err = err_rs = 0.0
+        for w in (8, 4):
+            ops.gp_pk_waves(w)
+            y = ops.gp_pk(A, B)
+            e1 = rel(y, ref)
+            # row scale (the gated-norm rstd folded out of the out_proj operand)
+            e2 = rel(ops.gp_pk(A, B, None, 0, 0, 0, rs), ref.float() * rs[:, None])
+            res[f"rel_err_w{w}"] = float(f"{e1:.2e}")
+            res[f"rel_err_rs_w{w}"] = float(f"{e2:.2e}")
+            err, err_rs = max(err, e1), max(err_rs, e2)
+        ops.gp_pk_waves(8)
         if name != "odd" and not (name == "lm_dgrad" and m * K * 2 >= (1 << 32)):
-            t = {"pk": [], "lib": [], "gp_mm": []}
+            t = {"pk": [], "pk4": [], "lib": [], "gp_mm": []}
             for _ in range(a.rounds):
+                ops.gp_pk_waves(8)
                 t["pk"].append(timeit(lambda: ops.gp_pk(A, B), a.reps))
+                ops.gp_pk_waves(4)
+                t["pk4"].append(timeit(lambda: ops.gp_pk(A, B), a.reps))
+                ops.gp_pk_waves(8)
                 t["lib"].append(timeit(lambda: torch.nn.functional.linear(A, B), a.reps))
                 if name in ("in_fwd", "out_fwd"):
                     t["gp_mm"].append(timeit(lambda: ops.gp_mm(A, B, None, 0, 0, 0, 1, 256), a.reps))

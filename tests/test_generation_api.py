@@ -89,3 +89,23 @@ def test_layernorm_config_with_fused_add_norm(layer):
         for _ in range(6):
             seq = torch.cat([seq, m(seq).logits[:, -1].argmax(-1, keepdim=True)], 1)
     assert torch.equal(out, seq)
+
+
+def test_decoder_cache_released_with_model_and_rebuilt_on_new_storage():
+    """The per-model decoder cache dies with the model (no module-level strong reference), and a parameter
+    storage change (dtype cast) builds a fresh decoder instead of replaying one that reads the old buffers."""
+    import gc
+    import weakref
+    m = _tiny("Mamba2")
+    prompt = torch.randint(0, 256, (1, 4))
+    a = m.generate(prompt, max_length=8)
+    dec0 = m._amd_decoders[(1, 8, False, prompt.device)][1]
+    assert torch.equal(m.generate(prompt, max_length=8), a)
+    assert m._amd_decoders[(1, 8, False, prompt.device)][1] is dec0  # reused while the storage is unchanged
+    m.double()
+    b = m.generate(prompt, max_length=8)
+    assert m._amd_decoders[(1, 8, False, prompt.device)][1] is not dec0 and torch.equal(a, b)
+    ref = weakref.ref(m)
+    del m, dec0
+    gc.collect()
+    assert ref() is None
