@@ -946,15 +946,20 @@ Tensor gp_pk(Tensor A, Tensor B, optional<Tensor> out, int64_t la, int64_t lb, i
   return C;
 }
 
-// GEMM engine workgroup shape (8 or 4 waves): which = 0 the persistent engine, 1 the split-K engine;
-// w <= 0 only reads it
-int64_t gp_pk_waves(int64_t w, int64_t which) {
-  if (which == 1) {
-    if (w > 0) mamba_amd::set_gemm_pipe_waves((int)w);
-    return mamba_amd::gemm_pipe_waves();
+// diagnostic SSD phase timing: a contiguous uint64 (int64) buffer, or None to switch it off (kernels/ssd.hip)
+void ssd_stamps(optional<Tensor> buf) {
+  if (buf.has_value() && buf->defined()) {
+    TORCH_CHECK(buf->is_cuda() && buf->scalar_type() == at::kLong && buf->is_contiguous(), "ssd_stamps: int64 buffer");
+    mamba_amd::set_ssd_stamps(buf->data_ptr());
+  } else {
+    mamba_amd::set_ssd_stamps(nullptr);
   }
-  if (w > 0) mamba_amd::set_gemm_pk_waves((int)w);
-  return mamba_amd::gemm_pk_waves();
+}
+
+// split-K GEMM engine workgroup shape (8 or 4 waves); w <= 0 only reads it
+int64_t gp_waves(int64_t w) {
+  if (w > 0) mamba_amd::set_gemm_pipe_waves((int)w);
+  return mamba_amd::gemm_pipe_waves();
 }
 
 int64_t wgrad_splits(int64_t M, int64_t P, int64_t Q) { return mamba_amd::gemm_wgrad_splits((int)M, (int)P, (int)Q); }
@@ -1095,7 +1100,8 @@ TORCH_LIBRARY(mamba_amd, m) {
   m.def("wgrad_splits(int M, int P, int Q) -> int", &wgrad_splits);
   m.def("gp_mm(Tensor A, Tensor B, Tensor(a!)? out=None, int la=0, int lb=0, int mode=0, int splits=1, int bm=256) -> Tensor");
   m.def("gp_pk(Tensor A, Tensor B, Tensor(a!)? out=None, int la=0, int lb=0, int mode=0, Tensor? rowscale=None) -> Tensor");
-  m.def("gp_pk_waves(int w=0, int which=0) -> int", &gp_pk_waves);
+  m.def("gp_waves(int w=0) -> int", &gp_waves);
+  m.def("ssd_stamps(Tensor? buf) -> ()", &ssd_stamps);
   m.def("gp_splits(int M, int N, int K) -> int", &gp_splits);
   m.def("part_rows(str kind, int a, int b=0) -> int", &part_rows);
   m.def("gp_reduce(Tensor part, Tensor(a!) out, bool accumulate=False) -> ()");

@@ -372,9 +372,9 @@ struct GemmPkArgs {
 
 __device__ __attribute__((aligned(64))) uint4 g_pk_sink[64];  // epilogue stores of lanes outside C
 
-// WN: waves along N (2 x WN waves).  WN = 4: 8 waves of (16 MI) x (16 NJ), two per SIMD; WN = 2: 4 waves of
-// 128 x 128 (MI = NJ = 8), one per SIMD with 256 accumulator registers each -- half the LDS fragment reads per
-// MFMA of the 8-wave form (16 reads per 64 MFMAs instead of 12 per 32).
+// WN: waves along N (2 x WN waves).  WN = 4: 8 waves of (16 MI) x (16 NJ), two per SIMD (the shipped form);
+// WN = 2: 4 waves, one per SIMD -- half the LDS fragment reads per MFMA, but ~20% slower at every tile shape
+// (192/256 x 192/224/256; profiles/r4/pk4_four_wave_tiles_rejected.txt), so not instantiated.
 template <int MI, int NJ, bool RS, bool TAIL, int WN = 4>
 __global__ __launch_bounds__(128 * WN) void gemm_pk_k(GemmPkArgs a) {
   constexpr int NT = 128 * WN, MH = MI / 2, NW = 2 * WN;
@@ -595,18 +595,10 @@ __global__ void gp_reduce_k(const float* __restrict__ part, int S, int64_t strid
   *reinterpret_cast<float4*>(out + i) = s;
 }
 
-// waves per workgroup of the persistent engine: 8 (two per SIMD, 128 x 64 wave tiles) or 4 (one per SIMD, 128 x 128);
-// MAMBA_AMD_PK_WAVES sets the process default, set_gemm_pk_waves overrides it (A/B in one process)
-static int g_pk_waves = 0;
-int gemm_pk_waves() {
-  if (g_pk_waves == 0) {
-    const char* e = getenv("MAMBA_AMD_PK_WAVES");
-    g_pk_waves = (e && atoi(e) == 4) ? 4 : 8;
-  }
-  return g_pk_waves;
-}
-void set_gemm_pk_waves(int w) { g_pk_waves = (w == 4) ? 4 : 8; }
-// the same choice for the split-K / non-persistent engine (gemm_pipe_k: weight gradients), MAMBA_AMD_PIPE_WAVES
+// waves per workgroup of the split-K engine (gemm_pipe_k, weight gradients): 8 (two per SIMD, 128 x 64 wave
+// tiles) or 4 (one per SIMD, 128 x 128); MAMBA_AMD_PIPE_WAVES sets the process default, set_gemm_pipe_waves
+// overrides it.  (The persistent engine's 4-wave form measured ~20% slower at every tile shape:
+// profiles/r4/pk4_four_wave_tiles_rejected.txt.)
 static int g_pipe_waves = 0;
 int gemm_pipe_waves() {
   if (g_pipe_waves == 0) {
@@ -755,32 +747,11 @@ hipError_t launch_gemm_pk(int la, int lb, const void* A, int64_t lda, const void
   a.tm = (M + bm - 1) / bm; a.tn = (N + bn - 1) / bn;
   a.ntiles = a.tm * a.tn;
   const bool tail = K % 64 != 0 || a.kte * 64 != K;
-  int nwg = std::min(a.ntiles, ncu);
+  const int nwg = std::min(a.ntiles, ncu);
 #define PK_L(MI_, NJ_, RS_)                                                                              \
   if (tail) hipLaunchKernelGGL((gemm_pk_k<MI_, NJ_, RS_, true>), dim3(nwg), dim3(512), 0, st, a);          \
   else hipLaunchKernelGGL((gemm_pk_k<MI_, NJ_, RS_, false>), dim3(nwg), dim3(512), 0, st, a)
-#define PK_L4(MI_, NJ_, RS_)                                                                              \
-  if (tail) hipLaunchKernelGGL((gemm_pk_k<MI_, NJ_, RS_, true, 2>), dim3(nwg), dim3(256), 0, st, a);       \
-  else hipLaunchKernelGGL((gemm_pk_k<MI_, NJ_, RS_, false, 2>), dim3(nwg), dim3(256), 0, st, a)
-  if (gemm_pk_waves() == 4) {
-    // 4-wave tiles (MAMBA_AMD_PK4_TILE): 0 = 256 x 256 (256 accumulators: hipcc shuffles AGPRs), 1 = 192 x 256,
-    // 2 = 256 x 224, 3 = 256 x 192
-    static int shape = -1;
-    if (shape < 0) { const char* e = getenv("MAMBA_AMD_PK4_TILE"); shape = e ? atoi(e) : 1; }
-    const int bm4 = shape == 1 ? 192 : 256, bn4 = shape == 2 ? 224 : shape == 3 ? 192 : 256;
-    a.tm = (M + bm4 - 1) / bm4; a.tn = (N + bn4 - 1) / bn4;
-    a.ntiles = a.tm * a.tn;
-    nwg = std::min(a.ntiles, ncu);
-    if (shape == 1) {
-      if (rowscale) { PK_L4(6, 8, true); } else { PK_L4(6, 8, false); }
-    } else if (shape == 2) {
-      if (rowscale) { PK_L4(8, 7, true); } else { PK_L4(8, 7, false); }
-    } else if (shape == 3) {
-      if (rowscale) { PK_L4(8, 6, true); } else { PK_L4(8, 6, false); }
-    } else {
-      if (rowscale) { PK_L4(8, 8, true); } else { PK_L4(8, 8, false); }
-    }
-  } else if (bn == 192) {
+  if (bn == 192) {
     if (rowscale) { PK_L(8, 3, true); } else { PK_L(8, 3, false); }
   } else if (bm == 256) {
     if (rowscale) { PK_L(8, 4, true); } else { PK_L(8, 4, false); }
@@ -788,7 +759,6 @@ hipError_t launch_gemm_pk(int la, int lb, const void* A, int64_t lda, const void
     if (rowscale) { PK_L(4, 4, true); } else { PK_L(4, 4, false); }
   }
 #undef PK_L
-#undef PK_L4
   return hipGetLastError();
 }
 

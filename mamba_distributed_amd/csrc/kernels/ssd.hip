@@ -51,6 +51,30 @@ __device__ __forceinline__ void st_any(void* p, int dt, int64_t i, float v) {
   else reinterpret_cast<bf16_t*>(p)[i] = f2bf(v);
 }
 
+// ---- diagnostic phase timing (ssd_stamps): wave 0 of every workgroup accumulates s_memtime deltas per phase of its
+// loop and writes them (vector stores) to a host-provided buffer; the STAMPS = false kernels compile it away.
+static unsigned long long* g_ssd_stamps = nullptr;  // host: (blocks, 8) u64 per stamped kernel, or null
+void set_ssd_stamps(void* p) { g_ssd_stamps = reinterpret_cast<unsigned long long*>(p); }
+#define SSD_STAMP(k)                                                                   \
+  if constexpr (STAMPS) {                                                              \
+    __builtin_amdgcn_sched_barrier(0);                                                 \
+    if (threadIdx.x == 0) {                                                            \
+      const unsigned long long _n = __builtin_amdgcn_s_memtime();                      \
+      st_acc[k] += _n - st_prev;                                                       \
+      st_prev = _n;                                                                    \
+    }                                                                                  \
+    __builtin_amdgcn_sched_barrier(0);                                                 \
+  }
+#define SSD_STAMP_INIT                                                                 \
+  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_prev = 0;               \
+  if constexpr (STAMPS) { if (threadIdx.x == 0) st_prev = __builtin_amdgcn_s_memtime(); }
+#define SSD_STAMP_FLUSH(blk)                                                           \
+  if constexpr (STAMPS) {                                                              \
+    if (threadIdx.x == 0 && stamps) {                                                  \
+      for (int _k = 0; _k < 8; ++_k) stamps[(int64_t)(blk) * 8 + _k] = st_acc[_k];     \
+    }                                                                                  \
+  }
+
 // ============================== K0: dt transform + cumsum ====================================
 // One 256-thread workgroup per (b, chunk) stages the chunk's dt rows (64 steps x H heads, each step's heads
 // contiguous in the in_proj output) through LDS with the threads walking the rows in order, then every wave scans
@@ -160,8 +184,8 @@ struct TileState {
 // X, B, C, cum, dt of chunk c+1 are register-prefetched while chunk c computes.  Against the split
 // state/scan kernels this reads X once, never re-reads the 2x-larger state tensor, and needs no
 // per-head-group CB^T staging: HBM traffic ~ x + y + states instead of 2x + y + 2 states.
-template <int N>
-__global__ __launch_bounds__(256) void ssd_fused_fwd_k(SSDArgs a) {
+template <int N, bool STAMPS = false>
+__global__ __launch_bounds__(256) void ssd_fused_fwd_k(SSDArgs a, unsigned long long* stamps = nullptr) {
   constexpr int LDN = N + 16;  // conflict-free ds_read_b128 fragments (see LD64)
   constexpr int NTS = N / 16;  // state n-tiles per wave
   __shared__ __attribute__((aligned(16))) bf16_t Cs[Q * LDN];
@@ -215,8 +239,10 @@ __global__ __launch_bounds__(256) void ssd_fused_fwd_k(SSDArgs a) {
     }
   };
   prefetch(0);
+  SSD_STAMP_INIT
   for (int c = 0; c < a.nc; ++c) {
     __syncthreads();  // chunk c-1 is fully consumed
+    SSD_STAMP(0)
     px.store(Xs, LD64);
     pb.store(Bs, LDN);
     pc.store(Cs, LDN);
@@ -227,7 +253,9 @@ __global__ __launch_bounds__(256) void ssd_fused_fwd_k(SSDArgs a) {
     }
 #pragma unroll
     for (int nt = 0; nt < NTS; ++nt) acc_to_lds(Ss, LDN, 16 * w, 16 * nt, st[nt]);
+    SSD_STAMP(1)
     __syncthreads();
+    SSD_STAMP(2)
     // ---- global stores BEFORE the prefetch loads: vmcnt counts stores too and completes in order,
     // so the wait for chunk c+1's operands at the next loop top must not also wait for stores issued
     // at the end of this chunk.  Y rows of chunk c-1 (staged in Os by this same wave), then S_c.
@@ -243,6 +271,7 @@ __global__ __launch_bounds__(256) void ssd_fused_fwd_k(SSDArgs a) {
       }
     }
     if (c + 1 < a.nc) prefetch(c + 1);
+    SSD_STAMP(3)
     const float cl = cumr[Q - 1];
     // ---- Y_off = e^{cum_i} C_i . S_c^T   (rows i of tile w, 4 p-tiles)
     f32x4 acc[4];
@@ -261,6 +290,7 @@ __global__ __launch_bounds__(256) void ssd_fused_fwd_k(SSDArgs a) {
 #pragma unroll
         for (int pt = 0; pt < 4; ++pt) acc[pt][r] *= e[r];
     }
+    SSD_STAMP(4)
     // ---- Y_diag: CB^T tiles (rows j of tile jt <= w, cols i of tile w), masked, decayed, x dt_j
     const int i_col = 16 * w + li;
     const float cum_i = cumr[i_col];
@@ -291,6 +321,7 @@ __global__ __launch_bounds__(256) void ssd_fused_fwd_k(SSDArgs a) {
         for (int pt = 0; pt < 4; ++pt) acc[pt] = mfma16(A, frag_tr_perm(Xs, LD64, 32 * ks, 16 * pt), acc[pt]);
       }
     }
+    SSD_STAMP(5)
     // ---- + D x, stage this wave's 16 rows, store them (no block barrier: same-wave LDS order)
 #pragma unroll
     for (int pt = 0; pt < 4; ++pt) {
@@ -300,6 +331,7 @@ __global__ __launch_bounds__(256) void ssd_fused_fwd_k(SSDArgs a) {
       for (int r = 0; r < 4; ++r) yv[r] = acc[pt][r] + Dh * (float)xr[r];
       acc_to_lds_pk(Os, LDY, 16 * w, 16 * pt, yv);
     }
+    SSD_STAMP(6)
     // ---- S_{c+1} = e^{cl} S_c + (X o w)^T B
     const float decay = __expf(cl);
 #pragma unroll
@@ -315,7 +347,9 @@ __global__ __launch_bounds__(256) void ssd_fused_fwd_k(SSDArgs a) {
 #pragma unroll
       for (int nt = 0; nt < NTS; ++nt) st[nt] = mfma16(A, frag_tr(Bs, LDN, 32 * ks, 16 * nt), st[nt]);
     }
+    SSD_STAMP(7)
   }
+  SSD_STAMP_FLUSH(blockIdx.y * gridDim.x + blockIdx.x)
   store_y_rows(a.nc - 1);
   if (a.final_state) {
 #pragma unroll
@@ -406,8 +440,8 @@ __global__ __launch_bounds__(256) void ssd_dstate_bwd_k(SSDArgs a) {
 // halves (wid >> 2) split the p-tiles (dX, BdS, Yoff) and the n-tiles (dB/dC accumulators).  The
 // M / dM tiles of column w4 are computed by both halves (cheap: 2 MFMAs per tile) so neither has to
 // wait for the other; only half 0 accumulates dCB and the G row/col sums.
-template <int N>
-__global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
+template <int N, bool STAMPS = false>
+__global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a, unsigned long long* stamps = nullptr) {
   constexpr int LDN = N + 16;  // conflict-free ds_read_b128 fragments (see LD64)
   constexpr int NT = N / 16;
   constexpr int NTH = NT / 2;
@@ -538,9 +572,11 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
     }
   };
   const int jl = 16 * w + li;  // this lane's column index in the M / dM tiles
+  SSD_STAMP_INIT
   for (int hh = 0; hh < a.HG; ++hh) {
     const int h = h0 + hh;
     __syncthreads();  // previous head fully consumed (LDS tiles, dcum, Os)
+    SSD_STAMP(0)
     if (threadIdx.x < Q) {
       cumr[threadIdx.x] = pc;
       dtr[hh & 7][threadIdx.x] = pd;
@@ -550,8 +586,10 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
     py.store(dYs, LD64);
     ps.store(Ss, LDN);
     pds.store(dSs, LDN);
+    SSD_STAMP(1)
     __syncthreads();
     if (hh + 1 < a.HG) prefetch(h + 1);
+    SSD_STAMP(2)
     const float cl = cumr[Q - 1];
     const float Ah = a.a_log ? -__expf(a.A[h]) : a.A[h];
     const float Dh = a.D ? a.D[h] : 0.f;
@@ -586,6 +624,7 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
         *reinterpret_cast<uint2*>(MsT + jt * LD64 + 16 * I + 4 * lg) = make_uint2(pack2(mv[0], mv[1]), pack2(mv[2], mv[3]));
       }
     }
+    SSD_STAMP(3)
     // ---- (4) BdS = B dS^T, (6) Yoff = C S^T for this half's p-tiles (independent of M: they fill the
     // wait for the M^T barrier), then (3) dXdt = M^T dY
     f32x4 dxd[2], bds[2], yo[2];
@@ -605,6 +644,7 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
         yo[q] = mfma16(Ac, frag_kc(Ss, LDN, 16 * (2 * half + q), 32 * ks), yo[q]);
       }
     }
+    SSD_STAMP(4)
     __syncthreads();  // M^T complete
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -615,6 +655,7 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
           dxd[q] = mfma16(Af, frag_tr(dYs, LD64, 32 * ks, 16 * (2 * half + q)), dxd[q]);
       }
     }
+    SSD_STAMP(5)
     // ---- (5) dX, ddt_direct, U, dD ; (6) dcum Yoff term   (rows j = i = 16w + 4lg + r)
     bf16x4 xr[2], yr[2];
 #pragma unroll
@@ -673,6 +714,7 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
         }
       }
     }
+    SSD_STAMP(6)
     // ---- (9) e^{cl} sum(dS o S) -> dcum[last]   (16-B LDS reads)
     {
       float s = 0.f;
@@ -696,7 +738,9 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a) {
                                   (int64_t)h * a.sdxh + col) = *reinterpret_cast<const uint4*>(Os + row * LD64 + col);
     }
     if ((hh & 7) == 7 || hh == a.HG - 1) flush(hh & ~7, (hh & 7) + 1);
+    SSD_STAMP(7)
   }
+  SSD_STAMP_FLUSH((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x)
   if (a.fuse_dbc) {
     // ---- this workgroup holds every head of group g (HG == H / G): finish dC = dC_off + dCB B and
     // dB = dB_off + dCB^T C here (ssd_dbc_bwd's math in the same order, so bitwise the same result) instead of
@@ -891,7 +935,11 @@ hipError_t launch_ssd_fwd_f32(const SSDF32Args& a, hipStream_t st) {
 hipError_t launch_ssd_fwd(const SSDArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(ssd_cumsum_k, dim3((unsigned)((int64_t)a.B * a.nc)), dim3(256), 0, st, a);
   MAMBA_HIP_CHECK(hipGetLastError());
-  N_SWITCH(a.N, hipLaunchKernelGGL(ssd_fused_fwd_k<NN>, dim3(a.H, a.B), dim3(256), 0, st, a));
+  if (g_ssd_stamps && a.N == 128) {
+    hipLaunchKernelGGL((ssd_fused_fwd_k<128, true>), dim3(a.H, a.B), dim3(256), 0, st, a, g_ssd_stamps);
+    return hipGetLastError();
+  }
+  N_SWITCH(a.N, hipLaunchKernelGGL(ssd_fused_fwd_k<NN>, dim3(a.H, a.B), dim3(256), 0, st, a, nullptr));
   return hipGetLastError();
 }
 
@@ -899,7 +947,13 @@ hipError_t launch_ssd_bwd(const SSDArgs& a, hipStream_t st) {
   N_SWITCH(a.N, hipLaunchKernelGGL(ssd_dstate_bwd_k<NN>, dim3(a.H, a.B), dim3(256), 0, st, a));
   MAMBA_HIP_CHECK(hipGetLastError());
   if (a.fuse_dbc && a.HG != a.H / a.G) return hipErrorInvalidValue;  // the fused finish needs the whole group
-  N_SWITCH(a.N, hipLaunchKernelGGL(ssd_chunk_bwd_k<NN>, dim3(a.nc, a.nhg, a.B), dim3(512), 0, st, a));
+  if (g_ssd_stamps && a.N == 128) {
+    // the stamp buffer holds the forward's (H * B) rows first, then the chunk backward's
+    hipLaunchKernelGGL((ssd_chunk_bwd_k<128, true>), dim3(a.nc, a.nhg, a.B), dim3(512), 0, st, a,
+                       g_ssd_stamps + (int64_t)a.H * a.B * 8);
+  } else {
+    N_SWITCH(a.N, hipLaunchKernelGGL(ssd_chunk_bwd_k<NN>, dim3(a.nc, a.nhg, a.B), dim3(512), 0, st, a, nullptr));
+  }
   MAMBA_HIP_CHECK(hipGetLastError());
   if (a.fuse_dbc) return hipSuccess;
   N_SWITCH(a.N, hipLaunchKernelGGL(ssd_dbc_bwd_k<NN>, dim3(a.nc, a.G, a.B), dim3(256), 0, st, a));

@@ -93,7 +93,14 @@ class _InProjCMFn(torch.autograd.Function):
         h2, w = ctx.saved_tensors
         if dxz.stride(1) != 1:
             dxz = dxz.contiguous()
-        dh = torch.mm(dxz.t(), w) if ctx.needs_input_grad[0] else None
+        dh = None
+        if ctx.needs_input_grad[0]:
+            # dh (b*l, d) = dxz^T W with both operands stored contraction-major ([2di][tokens], [2di][d]): the
+            # native split-K engine's XC . XC product (csrc/kernels/gemm_pipe.hip), bf16 out, no K split
+            if _gp_xc_ok(dxz, w):
+                dh = _ext.ops().gp_mm(dxz, w, None, 1, 1, 0, 1, 256)
+            else:
+                dh = torch.mm(dxz.t(), w)
         dw = None
         if ctx.needs_input_grad[1]:
             p = ctx.param
@@ -101,6 +108,14 @@ class _InProjCMFn(torch.autograd.Function):
             if not handled:
                 dw = grad_accum.defer(p, torch.mm(dxz, h2).to(p.dtype))
         return dh, dw, None
+
+
+def _gp_xc_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """a (K, M) and b (K, N), both rows contiguous: the native XC . XC product C = a^T b (gemm_pipe_supported)."""
+    return (a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.dim() == 2 and b.dim() == 2
+            and a.stride(1) == 1 and b.stride(1) == 1 and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0
+            and a.shape[1] % 8 == 0 and b.shape[1] % 8 == 0 and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0
+            and a.shape[1] >= 4096 and _ext.use_native(a))
 
 
 def _wgrad_native(p, dY, X, dy_cm, x_cm):

@@ -62,10 +62,9 @@ class _FusedLinearCEFn(torch.autograd.Function):
       dh_c     = dlogits_c W                     hipBLASLt                         | native: gp_pk against W^T
       dW      += dlogits_c^T h_c                 hipBLASLt, fp32 output + accumulate | native: gp_mm, fp32 slab
     so the (B*T, V) logits never exist whole (6.6 GB at 64 x 1024 tokens) and nothing of the lm_head is kept
-    for the backward but dh and dW, which the backward scales by d(loss).  Engines (MAMBA_AMD_LMHEAD=lib|native):
-    the whole node at 64k tokens measured 17.0 ms on hipBLASLt, 17.5 with dh native, 19.0 all native (per chunk
-    the native fwd / dW products are 10-17% slower, the native dh 2% faster in isolation;
-    profiles/r3/lm_head_chunk_products.log), so the library is the default.
+    for the backward but dh and dW, which the backward scales by d(loss).  Engines (MAMBA_AMD_LMHEAD=native|lib):
+    native by default (round 3 measured the whole node at 64k tokens 19.0 ms all native vs 17.0 on hipBLASLt,
+    profiles/r3/lm_head_chunk_products.log; the library stays as an A/B switch).
     The reference materialises the full fp32 logits (model.py:44-46)."""
 
     @staticmethod
@@ -159,9 +158,9 @@ def _lm_native(h2: torch.Tensor, w: torch.Tensor) -> bool:
 
 
 def _lm_engines(h2: torch.Tensor, w: torch.Tensor):
-    """(logits, dh, dW) on the native engines?  MAMBA_AMD_LMHEAD=native: all three; lib (default): none."""
+    """(logits, dh, dW) on the native engines?  MAMBA_AMD_LMHEAD=native (default): all three; lib: none."""
     import os
-    nat = os.environ.get("MAMBA_AMD_LMHEAD", "lib") == "native" and _lm_native(h2, w)
+    nat = os.environ.get("MAMBA_AMD_LMHEAD", "native") == "native" and _lm_native(h2, w)
     return nat, nat, nat
 
 

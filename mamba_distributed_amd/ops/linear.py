@@ -3,8 +3,8 @@
 Forward and input-gradient GEMMs run on the persistent engine (``gp_pk``: one workgroup per CU walks the
 output tiles; the next tile's operands stream into LDS while the previous tile's bf16 epilogue drains as
 whole-row stores), the input gradient as dY . (W^T)^T against a transposed weight cached per optimizer step,
-for the shapes where it measured faster than hipBLASLt (``_pk_wins``: short K, moderate outputs); the long-K
-and lm_head products stay on the library with a tuned solution table.  The weight
+for every training-size shape (``_pk_wins``; hipBLASLt only for tiny token counts and as an A/B switch).  The
+weight
 gradient dW = dY^T X reduces over all B*T tokens into a small output (3352 x 768 for in_proj), where the
 library leaves most CUs idle: the native engine (csrc/kernels/gemm_pipe.hip, ``gp_mm`` with both operands
 token-major) splits the tokens into S K-slices written as fp32 slabs.  Inside an accumulation scope the
@@ -112,12 +112,12 @@ def _wgrad_inplace(dev) -> bool:
 
 
 def _proj_engine() -> str:
-    """Forward / input-gradient projection GEMM: "pk" (the persistent native engine, gemm_pk_k, for every shape
-    it takes), "auto" (pk only for the short-K shapes where it measured faster than the library), "lib"
-    (hipBLASLt), or a comma list of roles on pk: fwd / dgrad, each optionally suffixed _short (K <= 1024) or
-    _long (K > 1024), e.g. "fwd_short,dgrad".  MAMBA_AMD_PROJ_GEMM selects."""
+    """Forward / input-gradient projection GEMM: "pk" (default: the persistent native engine, gemm_pk_k, for
+    every shape it takes), "auto" (pk only for the short-K shapes where it measured faster than hipBLASLt), "lib"
+    (hipBLASLt, A/B only), or a comma list of roles on pk: fwd / dgrad, each optionally suffixed _short
+    (K <= 1024) or _long (K > 1024), e.g. "fwd_short,dgrad".  MAMBA_AMD_PROJ_GEMM selects."""
     import os
-    return os.environ.get("MAMBA_AMD_PROJ_GEMM", "auto")
+    return os.environ.get("MAMBA_AMD_PROJ_GEMM", "pk")
 
 
 def _pk_wins(m: int, n_out: int, k: int, role: str = "fwd") -> bool:

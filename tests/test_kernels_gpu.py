@@ -353,14 +353,24 @@ def test_model_native_vs_reference(cuda, layer):
 def test_model_native_vs_reference_headline_width(cuda, monkeypatch, layer, engine):
     """The 280M configs' layer width and sequence length (d_model 768, T=1024, 16 SSD chunks, 24 heads)
     through 2 layers: loss and every parameter gradient, native kernels vs the fp32 reference ops, with the
-    projection / lm_head forward and input-gradient GEMMs on hipBLASLt and on the persistent native engine."""
+    projection forward and input-gradient GEMMs on hipBLASLt and on the persistent native engine.  8 x 1024
+    tokens: enough rows for the persistent engine on every projection (Mamba-1's channel-major in_proj needs
+    M * N >= 2^24), and a spy checks that it ran (pk) or did not (lib)."""
     monkeypatch.setenv("MAMBA_AMD_PROJ_GEMM", engine)
     from mamba_distributed_amd import LMHeadModel, MambaConfig
+    from mamba_distributed_amd.ops import linear as lin
+    calls = []
+    orig = lin._pk_mm
+
+    def spy(a2, w):
+        calls.append(tuple(a2.shape) + (w.shape[0],))
+        return orig(a2, w)
+    monkeypatch.setattr(lin, "_pk_mm", spy)
     torch.manual_seed(0)
     cfg = MambaConfig(d_model=768, n_layer=2, vocab_size=4096, ssm_cfg={"layer": layer})
     m = LMHeadModel(cfg, device=cuda)
-    x = torch.randint(0, 4096, (2, 1024), device=cuda)
-    y = torch.randint(0, 4096, (2, 1024), device=cuda)
+    x = torch.randint(0, 4096, (8, 1024), device=cuda)
+    y = torch.randint(0, 4096, (8, 1024), device=cuda)
 
     def lossgrad(force_ref):
         if force_ref:
@@ -375,7 +385,70 @@ def test_model_native_vs_reference_headline_width(cuda, monkeypatch, layer, engi
             os.environ.pop("MAMBA_AMD_FORCE_REFERENCE", None)
 
     ln, gn = lossgrad(False)
+    # pk: every layer's in_proj / out_proj forward and input gradient (Mamba-1: in_proj fwd, out_proj dgrad... on
+    # the engine where the layout is KC . KC); lib: none
+    n_pk = len(calls)
+    assert (n_pk >= 2 * cfg.n_layer) if engine == "pk" else (n_pk == 0), calls
     lr, gr = lossgrad(True)
+    assert abs(ln - lr) < 1e-2 * abs(lr), (ln, lr)
+    bad = {n: rel(gn[n], gr[n]) for n in gr if rel(gn[n], gr[n]) > 5e-2}
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("layer", ["Mamba1", "Mamba2"])
+def test_bench_path_vs_reference(cuda, monkeypatch, layer):
+    """The exact bench.py / trainer step path against the fp32 reference ops: fused lm_head + cross-entropy
+    (return_logits=False) on the native engines, two micro-steps through parallel.microbatch.run_micro_batches
+    inside grad_accum.accumulation_scope with the model's auto deferral policy, 8192-token micro-batches (every
+    projection on the persistent GEMM), then loss and every parameter gradient.  Spies check that the native
+    lm_head engines and the persistent projection GEMM actually ran."""
+    from mamba_distributed_amd import LMHeadModel, MambaConfig
+    from mamba_distributed_amd.ops import cross_entropy as ce
+    from mamba_distributed_amd.ops import grad_accum
+    from mamba_distributed_amd.ops import linear as lin
+    from mamba_distributed_amd.parallel.microbatch import auto_defer_reduce, run_micro_batches
+    pk_calls, lm_native = [], []
+    orig_pk, orig_lm = lin._pk_mm, ce._lm_engines
+
+    def spy_pk(a2, w):
+        pk_calls.append(a2.shape[0])
+        return orig_pk(a2, w)
+
+    def spy_lm(h2, w):
+        r = orig_lm(h2, w)
+        lm_native.append(r)
+        return r
+    monkeypatch.setattr(lin, "_pk_mm", spy_pk)
+    monkeypatch.setattr(ce, "_lm_engines", spy_lm)
+    torch.manual_seed(0)
+    cfg = MambaConfig(d_model=768, n_layer=2, vocab_size=50304, ssm_cfg={"layer": layer})
+    m = LMHeadModel(cfg, device=cuda)
+    g = torch.Generator(device=cuda).manual_seed(3)
+    batches = [(torch.randint(0, 50304, (8, 1024), device=cuda, generator=g),
+                torch.randint(0, 50304, (8, 1024), device=cuda, generator=g)) for _ in range(2)]
+
+    def run(force_ref):
+        if force_ref:
+            os.environ["MAMBA_AMD_FORCE_REFERENCE"] = "1"
+        try:
+            m.zero_grad(set_to_none=True)
+            it = iter(batches)
+
+            def compute_loss(x, y):
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    _, loss = m(x, y, return_logits=False)
+                return loss / 2
+            with grad_accum.accumulation_scope(defer_reduce=auto_defer_reduce(cfg)):
+                loss = run_micro_batches(m, lambda: next(it), 2, compute_loss, overlap=True)
+            torch.cuda.synchronize()
+            return loss.item(), {n: p.grad.detach().float().clone() for n, p in m.named_parameters()}
+        finally:
+            os.environ.pop("MAMBA_AMD_FORCE_REFERENCE", None)
+
+    ln, gn = run(False)
+    assert lm_native and all(all(r) for r in lm_native), lm_native
+    assert len(pk_calls) >= 2 * 2 * cfg.n_layer and min(pk_calls) >= 8192, pk_calls
+    lr, gr = run(True)
     assert abs(ln - lr) < 1e-2 * abs(lr), (ln, lr)
     bad = {n: rel(gn[n], gr[n]) for n in gr if rel(gn[n], gr[n]) > 5e-2}
     assert not bad, bad
