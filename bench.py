@@ -165,6 +165,7 @@ def main():
                      "bucket_mb": [round(b / 2**20, 1) for b in bb],
                      "grad_bytes": int(sum(bb)), "grad_comm_dtype": a.grad_comm_dtype})
     peak_gb = torch.cuda.max_memory_allocated() / 2**30 if dev.startswith("cuda") else 0.0
+    reserved_gb = torch.cuda.max_memory_reserved() / 2**30 if dev.startswith("cuda") else 0.0
     # caching-allocator retries (a failed cudaMalloc -> free cached blocks -> device sync -> retry): nonzero means
     # the run is memory-bound on the allocator, not on the kernels
     alloc_retries = int(torch.cuda.memory_stats().get("num_alloc_retries", 0)) if dev.startswith("cuda") else 0
@@ -214,6 +215,7 @@ def main():
                 "activation_checkpointing": a.activation_checkpointing,
                 "final_loss": round(loss_v, 4),
                 "peak_mem_gb": round(peak_gb, 1),
+                "peak_reserved_gb": round(reserved_gb, 1),
                 "alloc_retries": alloc_retries,
                 "comm": comm,
                 "per_gpu_tok_s": round(value / world, 1),

@@ -152,12 +152,12 @@ def _pk_mm(a2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
 
 def mm_nt(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     """``a @ b.T`` for two K-contiguous bf16 operands (a: (M, K), b: (N, K)) on the native persistent GEMM when
-    the shape suits it (M * N >= 2^24, K > 192), else torch.mm.  E.g. the Mamba-1 channel-major in_proj
+    the shape suits it (M * N >= 2^23, K > 192), else torch.mm.  E.g. the Mamba-1 channel-major in_proj
     xz = W_in h^T."""
     ok = (a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.dim() == 2 and b.dim() == 2
           and a.stride(-1) == 1 and b.stride(-1) == 1 and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0
           and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0 and a.shape[1] > 192 and a.shape[1] % 8 == 0
-          and b.shape[0] % 8 == 0 and a.shape[0] * b.shape[0] >= (1 << 24)
+          and b.shape[0] % 8 == 0 and a.shape[0] * b.shape[0] >= (1 << 23)
           and _pk_wins(a.shape[0], b.shape[0], a.shape[1]))
     return _pk_mm(a, b) if ok else torch.mm(a, b.t())
 

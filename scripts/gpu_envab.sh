@@ -16,6 +16,6 @@ for r in $(seq 1 "$rounds"); do
     spec=$v; [ "$spec" = "-" ] && spec=""
     log=gpurun_out/envab/v${i}_r$r.log
     env $spec timeout -k 10 400 python -u bench.py "$@" > "$log" 2>&1 || { echo "FAILED: $v"; tail -20 "$log"; exit 1; }
-    echo "[$v] r$r $(grep -o '"value": [0-9.]*' "$log") $(grep -o '"peak_mem_gb": [0-9.]*' "$log") $(grep -o '"alloc_retries": [0-9]*' "$log")"
+    echo "[$v] r$r $(grep -o '"value": [0-9.]*' "$log") $(grep -o '"peak_mem_gb": [0-9.]*' "$log") $(grep -o '"peak_reserved_gb": [0-9.]*' "$log") $(grep -o '"alloc_retries": [0-9]*' "$log")"
   done
 done
