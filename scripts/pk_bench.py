@@ -56,10 +56,10 @@ def main():
     cases = []
     for name, K, N in (("in_fwd", 768, 3352), ("out_fwd", 1536, 768), ("in_dgrad", 3352, 768),
                        ("out_dgrad", 768, 1536), ("lm_fwd", 768, 50304), ("lm_dgrad", 50304, 768),
-                       ("in_fwd_pad", 768, 3392), ("in_dgrad_pad", 3392, 768), ("odd", 200, 200)):
+                       ("in_fwd_pad", 768, 3392), ("in_dgrad_pad", 3392, 768), ("odd", 200, 200), ("odd2", 328, 1000)):
         if a.only and name not in a.only.split(","):
             continue
-        m = 1000 if name == "odd" else M
+        m = 1000 if name.startswith("odd") else M
         cases.append((name, rnd(m, K), rnd(N, K, scale=0.05)))
     for name, A, B in cases:
         m, K = A.shape
@@ -72,13 +72,17 @@ def main():
         rs = torch.rand(m, device=dev, generator=g) + 0.5
         res = {"case": name, "M": m, "N": N, "K": K}
         err = rel(ops.gp_pk(A, B), ref)
+        if K >= 256:
+            res["pp_rel_err"] = float(f"{rel(ops.gp_pp(A, B), ref):.2e}")
+            assert res["pp_rel_err"] < 1e-2, res
         # row scale (the gated-norm rstd folded out of the out_proj operand)
         err_rs = rel(ops.gp_pk(A, B, None, 0, 0, 0, rs), ref.float() * rs[:, None])
         res["rel_err"], res["rel_err_rowscale"] = float(f"{err:.2e}"), float(f"{err_rs:.2e}")
-        if name != "odd" and not (name == "lm_dgrad" and m * K * 2 >= (1 << 32)):
-            t = {"pk": [], "lib": [], "gp_mm": []}
+        if not name.startswith("odd") and not (name == "lm_dgrad" and m * K * 2 >= (1 << 32)):
+            t = {"pk": [], "pp": [], "lib": [], "gp_mm": []}
             for _ in range(a.rounds):
                 t["pk"].append(timeit(lambda: ops.gp_pk(A, B), a.reps))
+                t["pp"].append(timeit(lambda: ops.gp_pp(A, B), a.reps))
                 t["lib"].append(timeit(lambda: torch.nn.functional.linear(A, B), a.reps))
                 if name in ("in_fwd", "out_fwd"):
                     t["gp_mm"].append(timeit(lambda: ops.gp_mm(A, B, None, 0, 0, 0, 1, 256), a.reps))
