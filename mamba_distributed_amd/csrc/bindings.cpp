@@ -946,31 +946,6 @@ Tensor gp_pk(Tensor A, Tensor B, optional<Tensor> out, int64_t la, int64_t lb, i
   return C;
 }
 
-// Ping-pong persistent MFMA GEMM (kernels/gemm_pp.hip, gemm_pp_k): C = A . B^T, both operands K-contiguous,
-// bf16 C.
-Tensor gp_pp(Tensor A, Tensor B, optional<Tensor> out) {
-  check_cuda(A, "A");
-  at::hip::HIPGuardMasqueradingAsCUDA guard(A.device());
-  TORCH_CHECK(A.dim() == 2 && B.dim() == 2, "gp_pp: 2-D operands");
-  TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "gp_pp: bf16 operands");
-  TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1, "gp_pp: unit inner strides");
-  const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
-  TORCH_CHECK(B.size(1) == K, "gp_pp: contraction sizes differ (", K, " vs ", B.size(1), ")");
-  TORCH_CHECK(M < (1ll << 31) && N < (1ll << 31) && K < (1ll << 31), "gp_pp: sizes");
-  TORCH_CHECK((uintptr_t)A.data_ptr() % 16 == 0 && (uintptr_t)B.data_ptr() % 16 == 0, "gp_pp: 16-B aligned operands");
-  Tensor C = (out.has_value() && out->defined()) ? *out : at::empty({M, N}, A.options());
-  TORCH_CHECK(C.dim() == 2 && C.scalar_type() == at::kBFloat16 && C.stride(1) == 1 && C.size(0) == M && C.size(1) == N,
-              "gp_pp: out shape/dtype");
-  TORCH_CHECK((uintptr_t)C.data_ptr() % 16 == 0, "gp_pp: 16-B aligned out");
-  const int64_t lda = M == 1 ? K : A.stride(0), ldb = N == 1 ? K : B.stride(0), ldc = M == 1 ? N : C.stride(0);
-  TORCH_CHECK(mamba_amd::gemm_pp_supported((int)M, (int)N, (int)K, lda, ldb, ldc),
-              "gp_pp: unsupported shape/strides (M=", M, " N=", N, " K=", K, " lda=", lda, " ldb=", ldb, " ldc=", ldc,
-              "; needs K >= 256, K % 8, N % 8, 8-aligned strides, operands < 4 GB)");
-  HIPCHK(mamba_amd::launch_gemm_pp(A.data_ptr(), lda, B.data_ptr(), ldb, C.data_ptr(), ldc, (int)M, (int)N, (int)K,
-                                   cur_stream()));
-  return C;
-}
-
 // diagnostic SSD phase timing: a contiguous uint64 (int64) buffer, or None to switch it off (kernels/ssd.hip)
 void ssd_stamps(optional<Tensor> buf) {
   if (buf.has_value() && buf->defined()) {
@@ -1124,7 +1099,6 @@ TORCH_LIBRARY(mamba_amd, m) {
         "bool x_cm=False, Tensor(z!)? part_buf=None, int part_mode=0) -> Tensor");
   m.def("wgrad_splits(int M, int P, int Q) -> int", &wgrad_splits);
   m.def("gp_mm(Tensor A, Tensor B, Tensor(a!)? out=None, int la=0, int lb=0, int mode=0, int splits=1, int bm=256) -> Tensor");
-  m.def("gp_pp(Tensor A, Tensor B, Tensor(a!)? out=None) -> Tensor");
   m.def("gp_pk(Tensor A, Tensor B, Tensor(a!)? out=None, int la=0, int lb=0, int mode=0, Tensor? rowscale=None) -> Tensor");
   m.def("gp_waves(int w=0) -> int", &gp_waves);
   m.def("ssd_stamps(Tensor? buf) -> ()", &ssd_stamps);
@@ -1149,7 +1123,6 @@ TORCH_LIBRARY_IMPL(mamba_amd, CUDA, m) {
   m.impl("gemm_wgrad_cm", &gemm_wgrad_cm);
   m.impl("gp_mm", &gp_mm);
   m.impl("gp_pk", &gp_pk);
-  m.impl("gp_pp", &gp_pp);
   m.impl("gp_reduce", &gp_reduce);
   m.impl("add_rmsnorm_bwd", &add_rmsnorm_bwd);
   m.impl("gated_rmsnorm_fwd", &gated_rmsnorm_fwd);

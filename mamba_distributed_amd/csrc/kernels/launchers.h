@@ -105,10 +105,6 @@ hipError_t launch_gemm_pipe(int la, int lb, const void* A, int64_t lda, const vo
 // persistent variant (one workgroup per CU walking the output tiles; KC . KC, bf16 output (epi 0) only,
 // staged through LDS into whole-row stores; rowscale (epi 0, nullable): C[m, :] *= rowscale[m])
 bool gemm_pk_supported(int la, int lb, int epi, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc);
-// ping-pong persistent GEMM (gemm_pp.hip): C (bf16) = A . B^T, both K-contiguous
-bool gemm_pp_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc);
-hipError_t launch_gemm_pp(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N,
-                          int K, hipStream_t st);
 hipError_t launch_gemm_pk(int la, int lb, const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
                           int64_t ldc, int M, int N, int K, int epi, const float* rowscale, hipStream_t st);
 // the split-K engine's workgroup shape: 8 waves (128 x 64 per wave) or 4 waves (128 x 128 per wave)

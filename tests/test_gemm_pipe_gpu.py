@@ -131,13 +131,10 @@ def test_gp_headline_shapes(cuda, which):
 
 # ---- persistent engine (gp_pk: KC . KC, bf16 out, optional row scale) --------------------------------------
 def _pmm(ops, eng, A, B, rs=None):
-    if eng == "pp":  # ping-pong engine (kernels/gemm_pp.hip): no row scale
-        assert rs is None
-        return ops.gp_pp(A, B)
     return ops.gp_pk(A, B, None, 0, 0, 0, rs)
 
 
-@pytest.mark.parametrize("eng", ["pk", "pp"])
+@pytest.mark.parametrize("eng", ["pk"])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 256), (512, 768, 768), (300, 264, 200), (1000, 3352, 776),
                                    (768, 520, 1544), (64, 8, 256), (4096, 392, 3352), (2048, 1000, 320),
                                    (70000, 136, 448)])
@@ -145,8 +142,6 @@ def test_gp_pk_bf16(cuda, eng, M, N, K):
     """Persistent tile walk: ragged M / N (rows past the descriptor read as zeros, stores into the sink),
     K tails (out-of-range offsets), more tiles than CUs (several tiles per workgroup), fewer tiles than CUs."""
     ops = _ops()
-    if eng == "pp" and K < 256:
-        pytest.skip("the ping-pong engine needs >= 4 K-tiles")
     g = torch.Generator(device=cuda).manual_seed(M * 5 + N * 3 + K)
     A, B = _mk(M, K, 0, cuda, g), _mk(N, K, 0, cuda, g)
     C = _pmm(ops, eng, A, B)
@@ -154,8 +149,6 @@ def test_gp_pk_bf16(cuda, eng, M, N, K):
     assert C.shape == (M, N) and C.dtype == torch.bfloat16
     assert _rel(C, ref) < 8e-3, _rel(C, ref)
     assert torch.equal(C, _pmm(ops, eng, A, B)) and torch.isfinite(C.float()).all()
-    if eng == "pp":
-        return
     rs = torch.rand(M, device=cuda, generator=g) + 0.5
     Cs = _pmm(ops, eng, A, B, rs)
     assert _rel(Cs, ref * rs[:, None]) < 8e-3
@@ -164,7 +157,7 @@ def test_gp_pk_bf16(cuda, eng, M, N, K):
     assert torch.isfinite(C.float()).all()
 
 
-@pytest.mark.parametrize("eng", ["pk", "pp"])
+@pytest.mark.parametrize("eng", ["pk"])
 def test_gp_pk_strided_out_and_unsupported(cuda, eng):
     """C written into a column slice of a wider buffer (neighbours untouched); K <= 192 is refused."""
     ops = _ops()
@@ -173,14 +166,14 @@ def test_gp_pk_strided_out_and_unsupported(cuda, eng):
     W = torch.randn(264, 768, device=cuda, generator=g).to(torch.bfloat16)
     outbig = torch.zeros(640, 400, device=cuda, dtype=torch.bfloat16)
     C = outbig[:, 64:64 + 264]
-    ops.gp_pk(A, W, C) if eng == "pk" else ops.gp_pp(A, W, C)
+    ops.gp_pk(A, W, C)
     assert _rel(C, A.float() @ W.float().t()) < 8e-3
     assert (outbig[:, :64] == 0).all() and (outbig[:, 64 + 264:] == 0).all()
     with pytest.raises(RuntimeError):
         _pmm(ops, eng, A[:, :128], W[:, :128])
 
 
-@pytest.mark.parametrize("eng", ["pk", "pp"])
+@pytest.mark.parametrize("eng", ["pk"])
 @pytest.mark.parametrize("which", ["in_fwd", "in_dgrad", "out_fwd", "out_dgrad", "lm_fwd", "lm_dgrad"])
 def test_gp_pk_headline_shapes(cuda, eng, which):
     """The persistent engine at the Mamba-2 280M bench micro-batch (32 x 1024 tokens), input gradients through
