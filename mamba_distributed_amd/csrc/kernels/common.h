@@ -64,15 +64,43 @@ __device__ __forceinline__ void st8bf(bf16_t* p, const float (&o)[8]) {
                                             pack2(o[6], o[7]));
 }
 
+// Whole-wave reductions on the VALU: DPP butterflies inside each 16-lane row (quad_perm [1,0,3,2], [2,3,0,1],
+// row_half_mirror, row_mirror), then the four rows meet through v_permlane32_swap / v_permlane16_swap (gfx950).
+// The __shfl_xor form is six ds_bpermute_b32 LDS round trips in a dependent chain (~100 cycles each); this one is
+// eight VALU instructions.  Every lane gets the total; the summation order is fixed (deterministic).
+// v_permlane{32,16}_swap x, y: x <- [x_lo, y_lo], y <- [x_hi, y_hi] (32-lane halves) and x <- [x_r0, y_r0, x_r2,
+// y_r2], y <- [x_r1, y_r1, x_r3, y_r3] (16-lane rows); with x = y = v, x + y is v[l] + v[l ^ 32] (resp. ^ 16).
+// Inline asm: this ROCm's builtins return the first result twice.  s_nop 1: VALU write -> swap read.
+__device__ __forceinline__ float wave_rows_combine_sum(float v) {
+  float x = v, y = v;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+  v = x + y;
+  x = v; y = v;
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+  return x + y;
+}
+__device__ __forceinline__ float wave_rows_combine_max(float v) {
+  float x = v, y = v;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+  v = fmaxf(x, y);
+  x = v; y = v;
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+  return fmaxf(x, y);
+}
+#define MAMBA_DPPF(v, ctrl) __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, (v)), (ctrl), 0xF, 0xF, false))
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
-  return v;
+  v += MAMBA_DPPF(v, 0xB1);
+  v += MAMBA_DPPF(v, 0x4E);
+  v += MAMBA_DPPF(v, 0x141);
+  v += MAMBA_DPPF(v, 0x140);
+  return wave_rows_combine_sum(v);
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m, 64));
-  return v;
+  v = fmaxf(v, MAMBA_DPPF(v, 0xB1));
+  v = fmaxf(v, MAMBA_DPPF(v, 0x4E));
+  v = fmaxf(v, MAMBA_DPPF(v, 0x141));
+  v = fmaxf(v, MAMBA_DPPF(v, 0x140));
+  return wave_rows_combine_max(v);
 }
 
 // v_rcp_f32 (~1 ulp) instead of the IEEE division sequence: 1 instruction instead of ~10 and far

@@ -149,11 +149,7 @@ __device__ __forceinline__ float row_sum16(float v) {
   return v;
 }
 // sum over the 4 rows (lanes l, l^16, l^32, l^48)
-__device__ __forceinline__ float rows_sum4(float v) {
-  v += __shfl_xor(v, 16, 64);
-  v += __shfl_xor(v, 32, 64);
-  return v;
-}
+__device__ __forceinline__ float rows_sum4(float v) { return wave_rows_combine_sum(v); }
 
 // read 4 consecutive rows r0+4g..+3 of column c0 + (l&15) from a [rows][ld] bf16 LDS tile (the rows /
 // column an MFMA accumulator lane owns) with one ds_read_b64_tr_b16

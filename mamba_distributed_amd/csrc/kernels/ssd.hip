@@ -458,8 +458,8 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a, unsigned long 
   // Every cross-lane partial goes to a slot owned by ONE wave (plain read-modify-write in program
   // order) and the slots are summed in a fixed order in (10): deterministic, no LDS float atomics.
   __shared__ float cumr[Q], dtr[8][Q], rawl[8][Q];
-  __shared__ float dcw[8][8][Q];   // [head][wave][step]  dcum contributions
-  __shared__ float ddw[8][2][Q];   // [head][half][step]  direct ddt contributions
+  __shared__ __attribute__((aligned(16))) float dcw[8][8][Q];   // [head][wave][step]  dcum contributions
+  __shared__ __attribute__((aligned(16))) float ddw[8][2][Q];   // [head][half][step]  direct ddt contributions
   __shared__ float redw[8][8];     // [head][wave]        dD
   const int c = blockIdx.x, hgi = blockIdx.y, b = blockIdx.z;
   const int h0 = hgi * a.HG, g = h0 / (a.H / a.G);
@@ -572,6 +572,16 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a, unsigned long 
     }
   };
   const int jl = 16 * w + li;  // this lane's column index in the M / dM tiles
+  // causal mask of the owned tiles as an additive exponent offset (0 or -inf: e^{d - inf} = 0 for any finite d):
+  // a select on (jt <= i) is loop-invariant, so hipcc hoists its 64-bit lane masks out of the head loop, runs out
+  // of SGPRs and spills them to VGPR lanes; the offsets come from one VGPR of mask bits instead
+  // bit 4k + r set: element (row 4 lg + r, column li) of owned tile k is above the diagonal (one VGPR for all 8)
+  unsigned mbits = 0u;
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      mbits |= (16 * tJ[k] + li <= 16 * tI[k] + 4 * lg + r) ? 0u : (1u << (4 * k + r));
   SSD_STAMP_INIT
   for (int hh = 0; hh < a.HG; ++hh) {
     const int h = h0 + hh;
@@ -607,17 +617,24 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a, unsigned long 
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int i = 16 * I + 4 * lg + r;
-          const float Lij = (jt <= i) ? __expf(cumr[i] - cumj) : 0.f;
+          const float moff = __uint_as_float((0u - ((mbits >> (4 * k + r)) & 1u)) & 0xFF800000u);  // 0 or -inf
+          const float Lij = __expf(cumr[i] - cumj + moff);
           const float dmv = dm[r] * dtj;
           mv[r] = cbo[k][r] * Lij;
           dcbo[k][r] += dmv * Lij;
           gr[r] = dmv * mv[r];
           colG += gr[r];
         }
+        // the 4 row sums of this lane group's rows as ONE 16-B read-modify-write (4 scalar ones serialise:
+        // hipcc cannot tell the slots apart and waits for each read before the next)
+        float rs[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float rs = row_sum16(gr[r]);
-          if (li == 0) dcw[hh & 7][wid][16 * I + 4 * lg + r] += rs;
+        for (int r = 0; r < 4; ++r) rs[r] = row_sum16(gr[r]);
+        if (li == 0) {
+          float4* pr = reinterpret_cast<float4*>(&dcw[hh & 7][wid][16 * I + 4 * lg]);
+          float4 o = *pr;
+          o.x += rs[0]; o.y += rs[1]; o.z += rs[2]; o.w += rs[3];
+          *pr = o;
         }
         colG = rows_sum4(colG);
         if (l < 16) dcw[hh & 7][wid][jt] -= colG;
@@ -664,6 +681,7 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a, unsigned long 
       yr[q] = acc_rows4(dYs, LD64, 16 * w, 16 * (2 * half + q));
     }
     float dDp = 0.f, usum = 0.f;
+    float ddv[4], dcv[4];  // this lane group's rows: direct ddt and dcum contributions (one 16-B RMW each below)
     f32x4 ov[2];  // dX tile values, staged to Os as 4-byte column pairs after the row loop
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -683,14 +701,20 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a, unsigned long 
         yp += yo[q][r] * dyv;
         dDp += xv * dyv;
       }
-      ddp = row_sum16(ddp);
+      ddv[r] = row_sum16(ddp);
       up = row_sum16(up) * wj;
       yp = row_sum16(yp) * ei;
-      if (li == 0) {
-        ddw[hh & 7][half][j] += ddp;
-        dcw[hh & 7][wid][j] += yp - up;
-      }
+      dcv[r] = yp - up;
       usum += up;
+    }
+    if (li == 0) {
+      float4* pd = reinterpret_cast<float4*>(&ddw[hh & 7][half][16 * w + 4 * lg]);
+      float4* pc = reinterpret_cast<float4*>(&dcw[hh & 7][wid][16 * w + 4 * lg]);
+      float4 od = *pd, oc = *pc;
+      od.x += ddv[0]; od.y += ddv[1]; od.z += ddv[2]; od.w += ddv[3];
+      oc.x += dcv[0]; oc.y += dcv[1]; oc.z += dcv[2]; oc.w += dcv[3];
+      *pd = od;
+      *pc = oc;
     }
 #pragma unroll
     for (int q = 0; q < 2; ++q) acc_to_lds_pk(Os, LD64, 16 * w, 16 * (2 * half + q), ov[q]);
