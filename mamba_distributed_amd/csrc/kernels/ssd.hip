@@ -457,7 +457,10 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a, unsigned long 
   // with one wave per head instead of serialising wave 0 inside the head loop
   // Every cross-lane partial goes to a slot owned by ONE wave (plain read-modify-write in program
   // order) and the slots are summed in a fixed order in (10): deterministic, no LDS float atomics.
-  __shared__ float cumr[Q], dtr[8][Q], rawl[8][Q];
+  __shared__ __attribute__((aligned(16))) float cumr[Q], dtr[8][Q], rawl[8][Q];
+  // per-step decay factors of the current head, computed once by the staging lanes instead of by all 16 lanes of
+  // every row group: eir = e^{cum_t}, ejr = e^{cl - cum_t}
+  __shared__ __attribute__((aligned(16))) float eir[Q], ejr[Q];
   __shared__ __attribute__((aligned(16))) float dcw[8][8][Q];   // [head][wave][step]  dcum contributions
   __shared__ __attribute__((aligned(16))) float ddw[8][2][Q];   // [head][half][step]  direct ddt contributions
   __shared__ float redw[8][8];     // [head][wave]        dD
@@ -591,6 +594,8 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a, unsigned long 
       cumr[threadIdx.x] = pc;
       dtr[hh & 7][threadIdx.x] = pd;
       rawl[hh & 7][threadIdx.x] = raw_f(praw, a.dt_dtype);
+      eir[threadIdx.x] = __expf(pc);
+      ejr[threadIdx.x] = __expf(__shfl(pc, Q - 1, 64) - pc);
     }
     px.store(Xs, LD64);
     py.store(dYs, LD64);
@@ -683,13 +688,18 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a, unsigned long 
     float dDp = 0.f, usum = 0.f;
     float ddv[4], dcv[4];  // this lane group's rows: direct ddt and dcum contributions (one 16-B RMW each below)
     f32x4 ov[2];  // dX tile values, staged to Os as 4-byte column pairs after the row loop
+    const float4 dt4 = *reinterpret_cast<const float4*>(&dtr[hh & 7][16 * w + 4 * lg]);
+    const float4 ej4 = *reinterpret_cast<const float4*>(&ejr[16 * w + 4 * lg]);
+    const float4 ei4 = *reinterpret_cast<const float4*>(&eir[16 * w + 4 * lg]);
+    const float dtv[4] = {dt4.x, dt4.y, dt4.z, dt4.w}, ejv[4] = {ej4.x, ej4.y, ej4.z, ej4.w};
+    const float eiv[4] = {ei4.x, ei4.y, ei4.z, ei4.w};
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int j = 16 * w + 4 * lg + r;
-      const float dt_ = dtr[hh & 7][j];
-      const float ej = __expf(cl - cumr[j]);
+      const float dt_ = dtv[r];
+      const float ej = ejv[r];
       const float wj = ej * dt_;
-      const float ei = __expf(cumr[j]);
+      const float ei = eiv[r];
       float ddp = 0.f, up = 0.f, yp = 0.f;
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
@@ -724,8 +734,8 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a, unsigned long 
     if (l == 0) redw[hh & 7][wid] = dDp;
     // ---- (7) dC_off += (e^{cum_i} dY) S , (8) dB_off += (w_j x) dS   for this half's n-tiles
     {
-      const float ei = __expf(cumr[jl]);
-      const float wl = __expf(cl - cumr[jl]) * dtr[hh & 7][jl];
+      const float ei = eir[jl];
+      const float wl = ejr[jl] * dtr[hh & 7][jl];
 #pragma unroll
       for (int ks = 0; ks < P / 32; ++ks) {
         const bf16x8 Ay = scale_frag(frag_kc(dYs, LD64, 16 * w, 32 * ks), ei);

@@ -53,6 +53,13 @@ def _mm_cm(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,
     if ok:
         A = A.contiguous()
         return _ext.ops().gemm_skinny(A, B, out, accumulate)
+    if not accumulate and _narrow_native_ok(A, B, out):
+        # the narrow long-K products (x_dbl = W_x conv_out: 80 rows; d x_dbl[:R] = W_dt^T ddelta: 48 rows) on the
+        # split-K engine: A as stored (KC rows, or XC for the transposed W_dt view), B channel-major (XC), one
+        # 256-row tile of which only the weight rows are live (hipBLASLt: MAMBA_AMD_PROJ_GEMM=lib)
+        la = 0 if A.stride(1) == 1 else 1
+        a_ = A if la == 0 else A.t()
+        return _ext.ops().gp_mm(a_, B, out, la, 1, 0, 1, 256)
     if accumulate:
         return out.addmm_(A, B)
     return torch.mm(A, B, out=out) if out is not None else torch.mm(A, B)
@@ -108,6 +115,21 @@ class _InProjCMFn(torch.autograd.Function):
             if not handled:
                 dw = grad_accum.defer(p, torch.mm(dxz, h2).to(p.dtype))
         return dh, dw, None
+
+
+def _narrow_native_ok(A: torch.Tensor, B: torch.Tensor, out) -> bool:
+    """A (N, K) narrow weight (KC, or the transpose of a row-contiguous (K, N) weight), B (K, M) channel-major, bf16
+    out (N, M): the gemm_pipe_k layouts (gemm_pipe_supported) and the projection engine switch."""
+    from ..ops.linear import _pk_wins
+    N, K = A.shape
+    M = B.shape[1]
+    kc = A.stride(1) == 1 and A.stride(0) % 8 == 0 and K % 8 == 0
+    xc = A.stride(0) == 1 and A.stride(1) % 8 == 0 and N % 8 == 0
+    return (A.is_cuda and A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16 and (kc or xc) and N <= 256
+            and K >= 256 and B.stride(1) == 1 and B.stride(0) % 8 == 0 and M % 8 == 0 and M >= 4096
+            and A.data_ptr() % 16 == 0 and B.data_ptr() % 16 == 0
+            and (out is None or (out.stride(1) == 1 and out.stride(0) % 4 == 0 and out.data_ptr() % 16 == 0))
+            and _pk_wins(N, M, K) and _ext.use_native(B))
 
 
 def _gp_xc_ok(a: torch.Tensor, b: torch.Tensor) -> bool:

@@ -60,7 +60,8 @@ class _FusedLinearCEFn(torch.autograd.Function):
       logits_c = h_c W^T                         hipBLASLt (tuned table)           | native: gp_pk
       loss_c, dlogits_c (in place, / n_valid)    ce_fwd (one read of the tile)
       dh_c     = dlogits_c W                     hipBLASLt                         | native: gp_pk against W^T
-      dW      += dlogits_c^T h_c                 hipBLASLt, fp32 output + accumulate | native: gp_mm, fp32 slab
+      dW      += dlogits_c^T h_c                 hipBLASLt, fp32 output + accumulate | native: gp_mm, fp32 K-split
+                                                                                      slabs summed once per node
     so the (B*T, V) logits never exist whole (6.6 GB at 64 x 1024 tokens) and nothing of the lm_head is kept
     for the backward but dh and dW, which the backward scales by d(loss).  Engines (MAMBA_AMD_LMHEAD=native|lib):
     native by default (round 3 measured the whole node at 64k tokens 19.0 ms all native vs 17.0 on hipBLASLt,
@@ -83,7 +84,9 @@ class _FusedLinearCEFn(torch.autograd.Function):
         buf = torch.empty(min(R, M), V, device=h2.device, dtype=compute_dtype)
         losses = torch.empty(M, device=h2.device, dtype=torch.float32)
         dh = torch.empty(M, K, device=h2.device, dtype=compute_dtype) if need_h else None
-        dw = torch.empty(1, V, K, device=h2.device, dtype=torch.float32) if need_w else None
+        # native dW: fp32 K-split slabs kept across the row chunks (each chunk adds into them), summed once at the end
+        S = _lm_dw_splits(V, K, h2.device) if (need_w and nat_w) else 1
+        dw = torch.empty(S, V, K, device=h2.device, dtype=torch.float32) if need_w else None
         wt = grad_accum.cached_transpose(weight, compute_dtype) if (need_h and nat_h) else None
         ops = _ext.ops()
         for r0 in range(0, M, R):
@@ -101,10 +104,14 @@ class _FusedLinearCEFn(torch.autograd.Function):
                     torch.mm(lg, w, out=dh[r0:r1])
             if need_w:
                 if nat_w:
-                    ops.gp_mm(lg, hc, dw, 1, 1, 1 if r0 == 0 else 2, 1, 256)
+                    ops.gp_mm(lg, hc, dw, 1, 1, 1 if r0 == 0 else 2, S, 256)
                 else:
                     _lib_wgrad_acc(dw[0], lg, hc, r0 == 0)
         del buf
+        if need_w and S > 1:
+            dw1 = torch.empty(1, V, K, device=h2.device, dtype=torch.float32)
+            ops.gp_reduce(dw, dw1[0], False)
+            dw = dw1
         loss = losses.sum() * inv
         ctx.save_for_backward(dh, dw)
         ctx.hshape, ctx.hdtype, ctx.wdtype = h.shape, h.dtype, weight.dtype
@@ -121,6 +128,22 @@ class _FusedLinearCEFn(torch.autograd.Function):
         if ctx.needs_input_grad[1] and dw_ is not None:
             dw = (dw_[0] * g).to(ctx.wdtype)
         return dh, dw, None, None, None, None, None
+
+
+def _lm_dw_splits(V: int, K: int, device) -> int:
+    """K splits of the native dW = dlogits^T h product (gemm_pipe_k, 256 x 256 tiles, one workgroup per CU): the
+    (V/256) x (K/256) tiles alone fill whole rounds of the CUs badly (V = 50304, K = 768: 591 tiles = 2.3 rounds of
+    256, i.e. 3 rounds of work for 2.3 of tiles); S splits give S times the tiles at 1/S the depth: pick S <= 4 (and <= 1 GB of
+    slabs) with the least ceil(tiles S / CUs) / S (S = 3: 6.9 rounds -> 7 rounds of 1/3-depth tiles = 2.33 full-depth rounds)."""
+    tiles = -(-V // 256) * -(-K // 256)
+    ncu = torch.cuda.get_device_properties(device).multi_processor_count if device.type == "cuda" else 256
+    smax = max(1, min(4, (1 << 30) // (V * K * 4)))  # at most ~1 GB of slabs (the lm_head runs at the activation peak)
+    best, bs = None, 1
+    for S in range(1, smax + 1):
+        cost = -(-tiles * S // ncu) / S
+        if best is None or cost < best - 1e-9:
+            best, bs = cost, S
+    return bs
 
 
 _F32_OUT = [None]  # hipBLASLt bf16 x bf16 -> fp32 products (aten::mm.dtype / addmm.dtype) usable here
