@@ -128,9 +128,11 @@ struct GemmPipeArgs {
 // the dynamic buffer parity and tile bookkeeping cost more in the K-loop than the hidden epilogue gained.)
 // WN = 4: 8 waves as 2 x 4, each 128 x 64 of the 256 x 256 tile (two per SIMD); WN = 2: 4 waves of 128 x 128
 // (one per SIMD, 256 accumulator registers): half the LDS fragment reads per MFMA
-template <int LA, int LB, int EPI, int WN = 4>
+// MI: 16-row tiles per wave along M (8: 256-row output tiles; 4: 128-row tiles for narrow outputs, e.g. the
+// Mamba-1 x_proj's 80 rows)
+template <int LA, int LB, int EPI, int WN = 4, int MI = 8>
 __global__ __launch_bounds__(128 * WN) void gemm_pipe_k(GemmPipeArgs a) {
-  constexpr int MI = 8, NT = 128 * WN;
+  constexpr int NT = 128 * WN;
   constexpr int NJ = 16 / WN;  // 16-col tiles per wave
   constexpr int BM = 32 * MI, BN = 16 * NJ * WN;
   constexpr int SA = BM * 128, SB = BN * 128;  // bytes per K-tile image
@@ -635,13 +637,19 @@ hipError_t launch_gemm_pipe(int la, int lb, const void* A, int64_t lda, const vo
                             int64_t ldc, int M, int N, int K, int splits, int64_t split_stride, int epi, int bm,
                             hipStream_t st) {
   if (!gemm_pipe_supported(la, lb, M, N, K, lda, ldb, ldc)) return hipErrorInvalidValue;
-  if (splits < 1 || (splits > 1 && epi == 0) || bm != 256) return hipErrorInvalidValue;
+  if (splits < 1 || (splits > 1 && epi == 0) || (bm != 256 && bm != 128)) return hipErrorInvalidValue;
+  if (bm == 128 && (epi != 0 || lb != 1)) return hipErrorInvalidValue;  // instantiated: narrow A . XC B, bf16 out
   GemmPipeArgs a;
   a.A = (const bf16_t*)A; a.lda = lda; a.B = (const bf16_t*)B; a.ldb = ldb;
   a.C = C; a.ldc = ldc; a.split_stride = split_stride;
   a.M = M; a.N = N; a.K = K; a.splits = splits;
   a.kslice = ((K + splits - 1) / splits + GP_BK - 1) / GP_BK * GP_BK;
-  const int nwg = ((M + 255) / 256) * ((N + 255) / 256) * splits;
+  const int nwg = ((M + bm - 1) / bm) * ((N + 255) / 256) * splits;
+  if (bm == 128) {
+    if (la == 0) hipLaunchKernelGGL((gemm_pipe_k<0, 1, 0, 4, 4>), dim3(nwg), dim3(GP_NT), 0, st, a);
+    else hipLaunchKernelGGL((gemm_pipe_k<1, 1, 0, 4, 4>), dim3(nwg), dim3(GP_NT), 0, st, a);
+    return hipGetLastError();
+  }
 #define GP_EPI(LA_, LB_)                                                                       \
   if (gemm_pipe_waves() == 4) {                                                                \
     switch (epi) {                                                                             \

@@ -56,10 +56,11 @@ def _mm_cm(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,
     if not accumulate and _narrow_native_ok(A, B, out):
         # the narrow long-K products (x_dbl = W_x conv_out: 80 rows; d x_dbl[:R] = W_dt^T ddelta: 48 rows) on the
         # split-K engine: A as stored (KC rows, or XC for the transposed W_dt view), B channel-major (XC), one
-        # 256-row tile of which only the weight rows are live (hipBLASLt: MAMBA_AMD_PROJ_GEMM=lib)
+        # 128-row tile (gemm_pipe_k with MI = 4) of which only the weight rows are live (hipBLASLt:
+        # MAMBA_AMD_PROJ_GEMM=lib)
         la = 0 if A.stride(1) == 1 else 1
         a_ = A if la == 0 else A.t()
-        return _ext.ops().gp_mm(a_, B, out, la, 1, 0, 1, 256)
+        return _ext.ops().gp_mm(a_, B, out, la, 1, 0, 1, 128 if A.shape[0] <= 128 else 256)
     if accumulate:
         return out.addmm_(A, B)
     return torch.mm(A, B, out=out) if out is not None else torch.mm(A, B)

@@ -209,3 +209,21 @@ def test_gp_pk_concurrent_streams(cuda):
     torch.cuda.synchronize()
     for o1, o2 in outs:
         assert torch.equal(o1, r1) and torch.equal(o2, r2)
+
+
+@pytest.mark.parametrize("la,M", [(0, 80), (1, 48), (0, 128), (1, 120)])
+def test_gp_narrow_128_row_tiles(cuda, la, M):
+    """The split-K engine's 128-row tile form (gemm_pipe_k, MI = 4; bm=128): the Mamba-1 narrow long-K products
+    x_dbl = W_x conv_out (KC weight, 80 rows) and d x_dbl[:R] = W_dt^T ddelta (the XC view of W_dt, 48 rows),
+    channel-major B, bf16 out, written into a row slice of a wider buffer as in the mixer."""
+    ops = _ops()
+    g = torch.Generator(device=cuda).manual_seed(M + 7 * la)
+    K, N = 1536, 8192 + 64
+    A = _mk(M, K, la, cuda, g)                     # la 1: stored (K, M), rows contiguous
+    B = _mk(N, K, 1, cuda, g)                      # stored (K, N): channel-major activation
+    out = torch.zeros(M + 32, N, device=cuda, dtype=torch.bfloat16)
+    C = ops.gp_mm(A, B, out[:M], la, 1, 0, 1, 128)
+    ref = _ref(A, B, la, 1)
+    assert _rel(C, ref) < 8e-3, _rel(C, ref)
+    assert (out[M:] == 0).all()
+    assert torch.equal(C, ops.gp_mm(A, B, None, la, 1, 0, 1, 256))  # same K order as the 256-row tiles
