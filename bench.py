@@ -45,6 +45,35 @@ def _relaunch_under_torchrun(argv, n):
     return subprocess.call(cmd, env=env)
 
 
+def _allreduce_probe(dev: str, world: int, bucket_mb: float, iters: int = 10) -> dict:
+    """Mean time and bus bandwidth of an fp32 all-reduce of one gradient bucket (and of 4x that), every rank."""
+    import torch.distributed as dist
+    out = {}
+    on_gpu = dev.startswith("cuda")
+    for mb in (bucket_mb, 4 * bucket_mb):
+        n = max(world, int(mb * 2**20) // 4 // world * world)
+        buf = torch.ones(n, dtype=torch.float32, device=dev)
+        for _ in range(3):
+            dist.all_reduce(buf)
+        if on_gpu:
+            torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            dist.all_reduce(buf)
+        if on_gpu:
+            torch.cuda.synchronize()
+        t = (time.perf_counter() - t0) / iters
+        tt = torch.tensor(t, device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt.item())
+        key = f"allreduce_{int(round(mb))}MB"
+        out[key + "_ms"] = round(1e3 * t, 3)
+        out[key + "_busbw_GBps"] = round(2 * (world - 1) / world * n * 4 / t / 1e9, 1)
+        del buf
+    return out
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -154,7 +183,14 @@ def main():
     elapsed = torch.tensor(time.perf_counter() - t0, device=dev, dtype=torch.float64)
     all_reduce_max(elapsed)
     elapsed = float(elapsed.item())
+    comm_probe = {}
+    if world > 1:
+        # after the timed region: the gradient all-reduce's bus bandwidth at the bucket size over this job's RCCL
+        # rings (xGMI on one node), rccl-tests convention busbw = 2 (n - 1) / n x bytes / t
+        comm_probe = _allreduce_probe(dev, world, a.bucket_cap_mb)
     comm = {"backend": info.backend, "world_size": world}
+    if world > 1:
+        comm.update(comm_probe)
     if red is not None:
         exp = red.exposed_ms()
         red.timing = False

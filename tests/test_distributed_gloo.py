@@ -156,6 +156,8 @@ def test_bench_multi_rank_flow_on_cpu(dp_impl):
     assert d["config"]["parallelism"] == "dp2" and d["config"]["dp_impl"] == dp_impl
     assert d["config"]["grad_accum"] == 2 and d["value"] > 0
     assert math.isfinite(d["config"]["final_loss"]), d
+    # the post-timing all-reduce probe (bus bandwidth of one 100 MB gradient bucket and of 400 MB)
+    assert d["config"]["comm"]["allreduce_100MB_busbw_GBps"] > 0 and d["config"]["comm"]["allreduce_400MB_ms"] > 0, d
 
 
 def test_bench_gpus2_relaunches_under_torchrun():
