@@ -36,8 +36,6 @@ struct SSDArgs {
   bf16_t* dB; int64_t sdBb, sdBl, sdBg;
   bf16_t* dC; int64_t sdCb, sdCl, sdCg;
   bool fuse_dbc;          // HG == H / G: ssd_chunk_bwd finishes dB / dC itself (no partials, no ssd_dbc_bwd)
-  int prio;               // chunk backward wave priority A/B (MAMBA_AMD_SSD_PRIO; set by the launcher): 0 none,
-                          // 1 waves 4-7 at priority 1, 2 waves 0-1 (the two-tile M / dM owners) at priority 1
   float* part_dcb;        // (b, nc, nhg, 64, 64)
   float* part_db;         // (b, nc, nhg, 64, N)
   float* part_dc;         // (b, nc, nhg, 64, N)

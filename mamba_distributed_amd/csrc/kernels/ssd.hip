@@ -575,8 +575,6 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a, unsigned long 
     }
   };
   const int jl = 16 * w + li;  // this lane's column index in the M / dM tiles
-  if (a.prio == 1 && wid >= 4) __builtin_amdgcn_s_setprio(1);  // wid is wave-uniform: a scalar branch
-  if (a.prio == 2 && wid < 2) __builtin_amdgcn_s_setprio(1);
   // causal mask of the owned tiles as an additive exponent offset (0 or -inf: e^{d - inf} = 0 for any finite d):
   // a select on (jt <= i) is loop-invariant, so hipcc hoists its 64-bit lane masks out of the head loop, runs out
   // of SGPRs and spills them to VGPR lanes; the offsets come from one VGPR of mask bits instead
@@ -979,18 +977,7 @@ hipError_t launch_ssd_fwd(const SSDArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-static int ssd_prio_env() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("MAMBA_AMD_SSD_PRIO");
-    v = e ? atoi(e) : 0;
-  }
-  return v;
-}
-
-hipError_t launch_ssd_bwd(const SSDArgs& a_in, hipStream_t st) {
-  SSDArgs a = a_in;
-  a.prio = ssd_prio_env();
+hipError_t launch_ssd_bwd(const SSDArgs& a, hipStream_t st) {
   N_SWITCH(a.N, hipLaunchKernelGGL(ssd_dstate_bwd_k<NN>, dim3(a.H, a.B), dim3(256), 0, st, a));
   MAMBA_HIP_CHECK(hipGetLastError());
   if (a.fuse_dbc && a.HG != a.H / a.G) return hipErrorInvalidValue;  // the fused finish needs the whole group
