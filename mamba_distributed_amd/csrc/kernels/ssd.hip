@@ -51,14 +51,20 @@ __device__ __forceinline__ void st_any(void* p, int dt, int64_t i, float v) {
   else reinterpret_cast<bf16_t*>(p)[i] = f2bf(v);
 }
 
-// ---- diagnostic phase timing (ssd_stamps): wave 0 of every workgroup accumulates s_memtime deltas per phase of its
+// ---- diagnostic phase timing (ssd_stamps): one wave of every workgroup (MAMBA_AMD_SSD_STAMP_WAVE, default 0)
+// accumulates s_memtime deltas per phase of its
 // loop and writes them (vector stores) to a host-provided buffer; the STAMPS = false kernels compile it away.
 static unsigned long long* g_ssd_stamps = nullptr;  // host: (blocks, 8) u64 per stamped kernel, or null
-void set_ssd_stamps(void* p) { g_ssd_stamps = reinterpret_cast<unsigned long long*>(p); }
+static int g_ssd_stamp_wave = 0;                     // the stamped wave (MAMBA_AMD_SSD_STAMP_WAVE, default 0)
+void set_ssd_stamps(void* p) {
+  g_ssd_stamps = reinterpret_cast<unsigned long long*>(p);
+  const char* e = getenv("MAMBA_AMD_SSD_STAMP_WAVE");
+  g_ssd_stamp_wave = e ? atoi(e) : 0;
+}
 #define SSD_STAMP(k)                                                                   \
   if constexpr (STAMPS) {                                                              \
     __builtin_amdgcn_sched_barrier(0);                                                 \
-    if (threadIdx.x == 0) {                                                            \
+    if (threadIdx.x == 64 * swave) {                                                   \
       const unsigned long long _n = __builtin_amdgcn_s_memtime();                      \
       st_acc[k] += _n - st_prev;                                                       \
       st_prev = _n;                                                                    \
@@ -67,10 +73,10 @@ void set_ssd_stamps(void* p) { g_ssd_stamps = reinterpret_cast<unsigned long lon
   }
 #define SSD_STAMP_INIT                                                                 \
   unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_prev = 0;               \
-  if constexpr (STAMPS) { if (threadIdx.x == 0) st_prev = __builtin_amdgcn_s_memtime(); }
+  if constexpr (STAMPS) { if (threadIdx.x == 64 * swave) st_prev = __builtin_amdgcn_s_memtime(); }
 #define SSD_STAMP_FLUSH(blk)                                                           \
   if constexpr (STAMPS) {                                                              \
-    if (threadIdx.x == 0 && stamps) {                                                  \
+    if (threadIdx.x == 64 * swave && stamps) {                                         \
       for (int _k = 0; _k < 8; ++_k) stamps[(int64_t)(blk) * 8 + _k] = st_acc[_k];     \
     }                                                                                  \
   }
@@ -185,7 +191,7 @@ struct TileState {
 // state/scan kernels this reads X once, never re-reads the 2x-larger state tensor, and needs no
 // per-head-group CB^T staging: HBM traffic ~ x + y + states instead of 2x + y + 2 states.
 template <int N, bool STAMPS = false>
-__global__ __launch_bounds__(256) void ssd_fused_fwd_k(SSDArgs a, unsigned long long* stamps = nullptr) {
+__global__ __launch_bounds__(256) void ssd_fused_fwd_k(SSDArgs a, unsigned long long* stamps = nullptr, int swave = 0) {
   constexpr int LDN = N + 16;  // conflict-free ds_read_b128 fragments (see LD64)
   constexpr int NTS = N / 16;  // state n-tiles per wave
   __shared__ __attribute__((aligned(16))) bf16_t Cs[Q * LDN];
@@ -441,7 +447,7 @@ __global__ __launch_bounds__(256) void ssd_dstate_bwd_k(SSDArgs a) {
 // M / dM tiles of column w4 are computed by both halves (cheap: 2 MFMAs per tile) so neither has to
 // wait for the other; only half 0 accumulates dCB and the G row/col sums.
 template <int N, bool STAMPS = false>
-__global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a, unsigned long long* stamps = nullptr) {
+__global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a, unsigned long long* stamps = nullptr, int swave = 0) {
   constexpr int LDN = N + 16;  // conflict-free ds_read_b128 fragments (see LD64)
   constexpr int NT = N / 16;
   constexpr int NTH = NT / 2;
@@ -475,20 +481,24 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a, unsigned long 
   float pc = 0.f, pd = 0.f;
   RawF praw;
   const int tl = min(c * Q + (int)(threadIdx.x & 63), a.L - 1);  // clamped: the loads below never branch
-  auto prefetch = [&](int h) {
+  // the next head's operands in three groups (x / dY / dt rows, S, dS): issued together, the 8 waves' 10 loads each
+  // queue behind one another in the vector-memory pipe and the younger half (waves 4-7) stalled ~1.2k cycles per
+  // head issuing them (per-wave s_memtime stamps); spread over the compute phases they issue under the MFMAs
+  auto prefetch_a = [&](int h) {
     px.load(a.x + (int64_t)b * a.sxb + (int64_t)c * Q * a.sxl + (int64_t)h * a.sxh, a.sxl, valid);
     praw = ld_raw(a.dt, a.dt_dtype, (int64_t)b * a.sdtb + (int64_t)tl * a.sdtl + (int64_t)h * a.sdth);
     py.load(a.dy + (int64_t)b * a.sdyb + (int64_t)c * Q * a.sdyl + (int64_t)h * a.sdyh, a.sdyl, valid);
-    const int64_t soff = ((((int64_t)b * a.nc + c) * a.H + h) * P) * N;
-    ps.load(a.states + soff);
-    pds.load(a.dstates + soff);
     {
       const int64_t bh = ((int64_t)b * a.H + h) * a.Lp + (int64_t)c * Q + (threadIdx.x & 63);
       pc = a.cum[bh];
       pd = a.dtp[bh];
     }
   };
-  prefetch(h0);
+  auto prefetch_s = [&](int h) { ps.load(a.states + ((((int64_t)b * a.nc + c) * a.H + h) * P) * N); };
+  auto prefetch_ds = [&](int h) { pds.load(a.dstates + ((((int64_t)b * a.nc + c) * a.H + h) * P) * N); };
+  prefetch_a(h0);
+  prefetch_s(h0);
+  prefetch_ds(h0);
   for (int v = threadIdx.x; v < 8 * 8 * Q; v += 512) (&dcw[0][0][0])[v] = 0.f;
   for (int v = threadIdx.x; v < 8 * 2 * Q; v += 512) (&ddw[0][0][0])[v] = 0.f;
   stage_tile<Q, N>(Cs, LDN, a.Cm + (int64_t)b * a.sCb + (int64_t)c * Q * a.sCl + (int64_t)g * a.sCg, a.sCl, valid);
@@ -603,7 +613,7 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a, unsigned long 
     pds.store(dSs, LDN);
     SSD_STAMP(1)
     __syncthreads();
-    if (hh + 1 < a.HG) prefetch(h + 1);
+    if (hh + 1 < a.HG) prefetch_a(h + 1);
     SSD_STAMP(2)
     const float cl = cumr[Q - 1];
     const float Ah = a.a_log ? -__expf(a.A[h]) : a.A[h];
@@ -646,6 +656,7 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a, unsigned long 
         *reinterpret_cast<uint2*>(MsT + jt * LD64 + 16 * I + 4 * lg) = make_uint2(pack2(mv[0], mv[1]), pack2(mv[2], mv[3]));
       }
     }
+    if (hh + 1 < a.HG) prefetch_s(h + 1);
     SSD_STAMP(3)
     // ---- (4) BdS = B dS^T, (6) Yoff = C S^T for this half's p-tiles (independent of M: they fill the
     // wait for the M^T barrier), then (3) dXdt = M^T dY
@@ -666,6 +677,7 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a, unsigned long 
         yo[q] = mfma16(Ac, frag_kc(Ss, LDN, 16 * (2 * half + q), 32 * ks), yo[q]);
       }
     }
+    if (hh + 1 < a.HG) prefetch_ds(h + 1);
     SSD_STAMP(4)
     __syncthreads();  // M^T complete
 #pragma unroll
@@ -970,7 +982,8 @@ hipError_t launch_ssd_fwd(const SSDArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(ssd_cumsum_k, dim3((unsigned)((int64_t)a.B * a.nc)), dim3(256), 0, st, a);
   MAMBA_HIP_CHECK(hipGetLastError());
   if (g_ssd_stamps && a.N == 128) {
-    hipLaunchKernelGGL((ssd_fused_fwd_k<128, true>), dim3(a.H, a.B), dim3(256), 0, st, a, g_ssd_stamps);
+    hipLaunchKernelGGL((ssd_fused_fwd_k<128, true>), dim3(a.H, a.B), dim3(256), 0, st, a, g_ssd_stamps,
+                       g_ssd_stamp_wave & 3);
     return hipGetLastError();
   }
   N_SWITCH(a.N, hipLaunchKernelGGL(ssd_fused_fwd_k<NN>, dim3(a.H, a.B), dim3(256), 0, st, a, nullptr));
@@ -984,9 +997,9 @@ hipError_t launch_ssd_bwd(const SSDArgs& a, hipStream_t st) {
   if (g_ssd_stamps && a.N == 128) {
     // the stamp buffer holds the forward's (H * B) rows first, then the chunk backward's
     hipLaunchKernelGGL((ssd_chunk_bwd_k<128, true>), dim3(a.nc, a.nhg, a.B), dim3(512), 0, st, a,
-                       g_ssd_stamps + (int64_t)a.H * a.B * 8);
+                       g_ssd_stamps + (int64_t)a.H * a.B * 8, g_ssd_stamp_wave & 7);
   } else {
-    N_SWITCH(a.N, hipLaunchKernelGGL(ssd_chunk_bwd_k<NN>, dim3(a.nc, a.nhg, a.B), dim3(512), 0, st, a, nullptr));
+    N_SWITCH(a.N, hipLaunchKernelGGL(ssd_chunk_bwd_k<NN>, dim3(a.nc, a.nhg, a.B), dim3(512), 0, st, a, nullptr, 0));
   }
   MAMBA_HIP_CHECK(hipGetLastError());
   if (a.fuse_dbc) return hipSuccess;
