@@ -147,6 +147,119 @@ __global__ __launch_bounds__(256) void add_rmsnorm_bwd_k(
   block_dw_partial<NCH>(acc, part, D, lds, pacc);
 }
 
+// ------------------------------------------------------------------------------------------
+// Typed fast paths for the training dtypes (x / y / dy / dx in TX, the residual stream res / ro / dro /
+// dres in TR -- bf16 + fp32 with residual_in_fp32).  The dynamic-dtype kernels above branch per load,
+// and the two load flavours meeting in a phi force a vmcnt(0) after EVERY load, so a row's 9-12 loads
+// run one latency at a time; here a row's loads are all issued before the first wait.  Columns past D
+// load a clamped (valid) address and contribute zero, so the row path has no per-lane branch either,
+// and w stays in registers across the grid-stride rows.
+template <int NCH, typename TX, typename TR, bool RES>
+__global__ __launch_bounds__(256) void add_rmsnorm_fwd_t_k(
+    const TX* __restrict__ x, int64_t sx, const TR* __restrict__ res, int64_t sr, const float* __restrict__ w,
+    TX* __restrict__ y, TR* __restrict__ ro, float* __restrict__ rstd, int64_t M, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  float v[NCH][4], r[NCH][4];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = (lane + 64 * c) * 4, cc = col < D ? col : 0;
+    ld4<TX>(x + row * sx + cc, v[c]);
+    if (RES) ld4<TR>(res + row * sr + cc, r[c]);
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = (lane + 64 * c) * 4;
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (RES) v[c][k] += r[c][k];
+      s = fmaf(v[c][k], v[c][k], s);
+    }
+    if (col < D) {
+      ss += s;
+      st4<TR>(ro + row * D + col, v[c]);
+    }
+  }
+  ss = wave_sum(ss);
+  const float rs = rsqrtf(ss / (float)D + eps);
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = (lane + 64 * c) * 4;
+    if (col < D) {
+      float wv[4], o[4];
+      ld4<float>(w + col, wv);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = v[c][k] * rs * wv[k];
+      st4<TX>(y + row * D + col, o);
+    }
+  }
+  if (lane == 0) rstd[row] = rs;
+}
+
+template <int NCH, typename TX, typename TR, bool DRO>
+__global__ __launch_bounds__(256) void add_rmsnorm_bwd_t_k(
+    const TX* __restrict__ dy, const TR* __restrict__ dro, const TR* __restrict__ ro, const float* __restrict__ w,
+    const float* __restrict__ rstd, TX* __restrict__ dx, TR* __restrict__ dres, float* __restrict__ part, bool pacc,
+    int64_t M, int D) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int lane = threadIdx.x & 63;
+  float acc[NCH][4], wv[NCH][4];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = (lane + 64 * c) * 4;
+    ld4<float>(w + (col < D ? col : 0), wv[c]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      acc[c][k] = 0.f;
+      if (col >= D) wv[c][k] = 0.f;  // out-of-row lanes: dyw = 0 -> no dot / acc contribution
+    }
+  }
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < M; row += (int64_t)gridDim.x * 4) {
+    float xh[NCH][4], g[NCH][4], d2[NCH][4];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = (lane + 64 * c) * 4, cc = col < D ? col : 0;
+      ld4<TR>(ro + row * D + cc, xh[c]);
+      ld4<TX>(dy + row * D + cc, g[c]);
+      if (DRO) ld4<TR>(dro + row * D + cc, d2[c]);
+    }
+    const float rs = rstd[row];
+    float dot = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        xh[c][k] *= rs;
+        dot = fmaf(g[c][k] * wv[c][k], xh[c][k], dot);
+        if ((lane + 64 * c) * 4 < D) acc[c][k] = fmaf(g[c][k], xh[c][k], acc[c][k]);
+      }
+    dot = wave_sum(dot) / (float)D;
+    // d2 is only read under the (col < D) store guard: pin it here, or the compiler sinks its load into
+    // that branch, behind the reduction, with a vmcnt(0) of its own
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+      if (DRO) asm volatile("" : "+v"(d2[c][0]), "+v"(d2[c][1]), "+v"(d2[c][2]), "+v"(d2[c][3]));
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = (lane + 64 * c) * 4;
+      if (col < D) {
+        float o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          o[k] = (g[c][k] * wv[c][k] - xh[c][k] * dot) * rs;
+          if (DRO) o[k] += d2[c][k];
+        }
+        st4<TX>(dx + row * D + col, o);
+        if (dres) st4<TR>(dres + row * D + col, o);
+      }
+    }
+  }
+  block_dw_partial<NCH>(acc, part, D, lds, pacc);
+}
+
 // out[c] = sum_r part[r * rstride + c] in a fixed order.  Block = 64 columns x 16 row-groups (1024
 // threads); each thread sums a strided row subset (independent loads -> deep memory-level
 // parallelism), the 16 group sums are combined through LDS in index order -> bitwise deterministic.
@@ -660,6 +773,17 @@ hipError_t launch_add_rmsnorm_fwd(const void* x, int xdt, int64_t sx, const void
                                   int D, float eps, hipStream_t st) {
   if (M == 0) return hipSuccess;
   dim3 grid((unsigned)((M + 3) / 4)), block(256);
+  if (xdt == kBF16 && ydt == kBF16 && rodt == kF32 && (!res || rdt == kF32)) {
+    const bf16_t* xb = (const bf16_t*)x;
+    if (res) {
+      NCH_SWITCH(D, hipLaunchKernelGGL((add_rmsnorm_fwd_t_k<NCH, bf16_t, float, true>), grid, block, 0, st, xb, sx,
+                                       (const float*)res, sr, w, (bf16_t*)y, (float*)ro, rstd, M, D, eps));
+    } else {
+      NCH_SWITCH(D, hipLaunchKernelGGL((add_rmsnorm_fwd_t_k<NCH, bf16_t, float, false>), grid, block, 0, st, xb, sx,
+                                       (const float*)nullptr, sr, w, (bf16_t*)y, (float*)ro, rstd, M, D, eps));
+    }
+    return hipGetLastError();
+  }
   NCH_SWITCH(D, hipLaunchKernelGGL((add_rmsnorm_fwd_k<NCH>), grid, block, 0, st, x, xdt, sx, res, rdt, sr, w, y,
                                    ydt, ro, rodt, rstd, M, D, eps));
   return hipGetLastError();
@@ -672,8 +796,21 @@ hipError_t launch_add_rmsnorm_bwd(const void* dy, int ydt, const void* dro, int 
                                   float* part, float* dw, bool pacc, int64_t M, int D, hipStream_t st) {
   const int g = bwd_grid(M);
   const size_t lds = 4 * (size_t)D * sizeof(float);
-  NCH_SWITCH(D, hipLaunchKernelGGL((add_rmsnorm_bwd_k<NCH>), dim3(g), dim3(256), lds, st, dy, ydt, dro, drodt, ro,
-                                   rodt, w, rstd, dx, xdt, dres, rdt, part, pacc, M, D));
+  if (ydt == kBF16 && xdt == kBF16 && rodt == kF32 && (!dro || drodt == kF32) && (!dres || rdt == kF32)) {
+    const bf16_t* dyb = (const bf16_t*)dy;
+    if (dro) {
+      NCH_SWITCH(D, hipLaunchKernelGGL((add_rmsnorm_bwd_t_k<NCH, bf16_t, float, true>), dim3(g), dim3(256), lds, st,
+                                       dyb, (const float*)dro, (const float*)ro, w, rstd, (bf16_t*)dx, (float*)dres,
+                                       part, pacc, M, D));
+    } else {
+      NCH_SWITCH(D, hipLaunchKernelGGL((add_rmsnorm_bwd_t_k<NCH, bf16_t, float, false>), dim3(g), dim3(256), lds, st,
+                                       dyb, (const float*)nullptr, (const float*)ro, w, rstd, (bf16_t*)dx,
+                                       (float*)dres, part, pacc, M, D));
+    }
+  } else {
+    NCH_SWITCH(D, hipLaunchKernelGGL((add_rmsnorm_bwd_k<NCH>), dim3(g), dim3(256), lds, st, dy, ydt, dro, drodt, ro,
+                                     rodt, w, rstd, dx, xdt, dres, rdt, part, pacc, M, D));
+  }
   MAMBA_HIP_CHECK(hipGetLastError());
   return dw ? launch_colsum(part, g, D, dw, st) : hipSuccess;
 }
