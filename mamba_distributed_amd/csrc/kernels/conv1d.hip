@@ -415,13 +415,14 @@ __device__ __forceinline__ void store_row(bf16_t* p, const f2v (&o)[2]) {
 
 // CV = channels per lane (8: 16-B rows, 4: 8-B rows -- half the registers, twice the waves in flight and
 // no idle lanes when C % 512 != 0, e.g. the 280M conv width 1792)
-template <int W, int TT, int CV>
+template <int W, int TT, int CV, bool SILU>
 __global__ __launch_bounds__(256) void conv_cl_fwd_bf16_k(const bf16_t* __restrict__ x, int64_t sxb, int64_t sxl,
                                                           const float* __restrict__ w, const float* __restrict__ bias,
                                                           bf16_t* __restrict__ out, int64_t sob, int64_t sol, int L,
-                                                          int C, bool silu) {
+                                                          int C) {
   constexpr int NQ = CV / 2;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: row guards are scalar branches
   const int c = (blockIdx.x * 64 + lane) * CV;
   const int t0 = (blockIdx.y * 4 + wave) * TT;
   const int b = blockIdx.z;
@@ -446,46 +447,54 @@ __global__ __launch_bounds__(256) void conv_cl_fwd_bf16_k(const bf16_t* __restri
 #pragma unroll
   for (int k = 0; k < W - 1; ++k) ldrow(t0 - (W - 1) + k).unpack(xr[k]);
   const int nsteps = tend - t0;
-  // each group of W rows is requested one group ahead (two groups of loads in flight per wave)
-  RowV<CV> rx[W];
+  // Groups of W rows, ping-pong between two register sets (loop unrolled by two groups): group g+1 is
+  // requested before group g is computed.  The loads are unconditional (row clamped to L-1; rows past
+  // tend are never consumed): conditional loads and a rotating copy (rx = next) made the compiler wait
+  // for the just-issued group at every back-edge.
+  auto ldgrp = [&](RowV<CV>(&r)[W], int i0) {
 #pragma unroll
-  for (int u = 0; u < W; ++u) rx[u] = ldrow(t0 + u);
-  for (int i0 = 0; i0 < nsteps; i0 += W) {
-    RowV<CV> nx[W];
-#pragma unroll
-    for (int u = 0; u < W; ++u) nx[u] = ldrow(t0 + i0 + W + u);
+    for (int u = 0; u < W; ++u) r[u].load(xb + (int64_t)min(t0 + i0 + u, L - 1) * sxl);
+  };
+  auto step = [&](RowV<CV>(&r)[W], int i0) {
 #pragma unroll
     for (int u = 0; u < W; ++u) {
       const int i = i0 + u;
       if (i < nsteps) {
         const int sl = (u + W - 1) % W;
-        rx[u].unpack(xr[sl]);
+        r[u].unpack(xr[sl]);
         f2v o[NQ];
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
           f2v a = bs[q];
 #pragma unroll
           for (int k = 0; k < W; ++k) a += wk[k][q] * xr[(u + k) % W][q];
-          if (silu) a = a * f2v{sigmoidf_(a.x), sigmoidf_(a.y)};
+          if (SILU) a = a * f2v{sigmoidf_(a.x), sigmoidf_(a.y)};
           o[q] = a;
         }
         store_row(ob + (t0 + i) * sol, o);
       }
     }
-#pragma unroll
-    for (int u = 0; u < W; ++u) rx[u] = nx[u];
+  };
+  RowV<CV> ra[W], rb[W];
+  ldgrp(ra, 0);
+  for (int i0 = 0; i0 < nsteps; i0 += 2 * W) {
+    ldgrp(rb, i0 + W);
+    step(ra, i0);
+    ldgrp(ra, i0 + 2 * W);
+    step(rb, i0 + W);
   }
 }
 
-template <int W, int TT, int CV>
+template <int W, int TT, int CV, bool SILU>
 __global__ __launch_bounds__(256) void conv_cl_bwd_bf16_k(const bf16_t* __restrict__ x, int64_t sxb, int64_t sxl,
                                                           const float* __restrict__ w, const float* __restrict__ bias,
                                                           const bf16_t* __restrict__ dout, int64_t sgb, int64_t sgl,
                                                           bf16_t* __restrict__ dx, int64_t sdb, int64_t sdl,
-                                                          float* __restrict__ part, bool pacc, int L, int C, bool silu) {
+                                                          float* __restrict__ part, bool pacc, int L, int C) {
   constexpr int NQ = CV / 2;
   __shared__ float red[4][64 * CV * (W + 1)];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: row guards are scalar branches
   const int c = (blockIdx.x * 64 + lane) * CV;
   const int t0 = (blockIdx.y * 4 + wave) * TT;
   const int b = blockIdx.z;
@@ -521,35 +530,34 @@ __global__ __launch_bounds__(256) void conv_cl_bwd_bf16_k(const bf16_t* __restri
       for (int q = 0; q < NQ; ++q) dp[k][q] = f2v{0.f, 0.f};
       if (k < W - 1) ldrow(xb, sxl, t0 - (W - 1) + k).unpack(xr[k]);
     }
-    // each group of W rows of x and dout is requested one group ahead (two groups in flight per wave)
-    RowV<CV> rx[W], rg[W];
-#pragma unroll
-    for (int u = 0; u < W; ++u) {
-      rx[u] = ldrow(xb, sxl, t0 + u);
-      rg[u] = ldrow(gb, sgl, t0 + u);
-    }
-    for (int i0 = 0; i0 < nsteps; i0 += W) {
-      RowV<CV> nx[W], ng[W];
+    // Groups of W rows of x and dout, ping-pong between two register sets (loop unrolled by two groups):
+    // group g+1 is requested before group g is computed.  Loads are unconditional (row clamped to L-1:
+    // rows t >= L only feed terms zeroed by the t < L / t < tend guards); conditional loads and a
+    // rotating copy made the compiler wait for the just-issued group at every back-edge.
+    auto ldgrp = [&](RowV<CV>(&rx_)[W], RowV<CV>(&rg_)[W], int i0) {
 #pragma unroll
       for (int u = 0; u < W; ++u) {
-        nx[u] = ldrow(xb, sxl, t0 + i0 + W + u);
-        ng[u] = ldrow(gb, sgl, t0 + i0 + W + u);
+        const int64_t t = min(t0 + i0 + u, L - 1);
+        rx_[u].load(xb + t * sxl);
+        rg_[u].load(gb + t * sgl);
       }
+    };
+    auto step = [&](RowV<CV>(&x_)[W], RowV<CV>(&g_)[W], int i0) {
 #pragma unroll
       for (int u = 0; u < W; ++u) {
         const int i = i0 + u, t = t0 + i;
         if (i < nsteps) {
           const int sl = (u + W - 1) % W;  // slot of step t (compile-time after unrolling)
-          rx[u].unpack(xr[sl]);
+          x_[u].unpack(xr[sl]);
           f2v g[NQ];
-          rg[u].unpack(g);
+          g_[u].unpack(g);
 #pragma unroll
           for (int q = 0; q < NQ; ++q) {
             f2v a = bs[q];
 #pragma unroll
             for (int k = 0; k < W; ++k) a += wk[k][q] * xr[(u + k) % W][q];
             f2v d = g[q];
-            if (silu) {
+            if (SILU) {
               const float s0 = sigmoidf_(a.x), s1 = sigmoidf_(a.y);
               const f2v sv = f2v{s0, s1};
               d = g[q] * sv * (1.f + a * (1.f - sv));
@@ -577,11 +585,14 @@ __global__ __launch_bounds__(256) void conv_cl_bwd_bf16_k(const bf16_t* __restri
           }
         }
       }
-#pragma unroll
-      for (int u = 0; u < W; ++u) {
-        rx[u] = nx[u];
-        rg[u] = ng[u];
-      }
+    };
+    RowV<CV> xa[W], ga[W], xb2[W], gb2[W];
+    ldgrp(xa, ga, 0);
+    for (int i0 = 0; i0 < nsteps; i0 += 2 * W) {
+      ldgrp(xb2, gb2, i0 + W);
+      step(xa, ga, i0);
+      ldgrp(xa, ga, i0 + 2 * W);
+      step(xb2, gb2, i0 + W);
     }
   }
 #pragma unroll
@@ -844,12 +855,16 @@ static hipError_t cl_fwd(const T* x, int64_t sxb, int64_t sxl, const float* w, c
       constexpr int TF = 32;
       if (conv_cl_cv(C) == 4) {
         dim3 g2((C + 255) / 256, (L + 4 * TF - 1) / (4 * TF), Bn);
-        W_SWITCH(Wd, hipLaunchKernelGGL((conv_cl_fwd_bf16_k<WW, TF, 4>), g2, dim3(256), 0, st, x, sxb, sxl, w, bias,
-                                        out, sob, sol, L, C, silu));
+        if (silu) W_SWITCH(Wd, hipLaunchKernelGGL((conv_cl_fwd_bf16_k<WW, TF, 4, true>), g2, dim3(256), 0, st, x, sxb,
+                                                  sxl, w, bias, out, sob, sol, L, C));
+        else W_SWITCH(Wd, hipLaunchKernelGGL((conv_cl_fwd_bf16_k<WW, TF, 4, false>), g2, dim3(256), 0, st, x, sxb, sxl,
+                                             w, bias, out, sob, sol, L, C));
       } else {
         dim3 g2((C + 511) / 512, (L + 4 * TF - 1) / (4 * TF), Bn);
-        W_SWITCH(Wd, hipLaunchKernelGGL((conv_cl_fwd_bf16_k<WW, TF, 8>), g2, dim3(256), 0, st, x, sxb, sxl, w, bias,
-                                        out, sob, sol, L, C, silu));
+        if (silu) W_SWITCH(Wd, hipLaunchKernelGGL((conv_cl_fwd_bf16_k<WW, TF, 8, true>), g2, dim3(256), 0, st, x, sxb,
+                                                  sxl, w, bias, out, sob, sol, L, C));
+        else W_SWITCH(Wd, hipLaunchKernelGGL((conv_cl_fwd_bf16_k<WW, TF, 8, false>), g2, dim3(256), 0, st, x, sxb, sxl,
+                                             w, bias, out, sob, sol, L, C));
       }
       return hipGetLastError();
     }
@@ -888,11 +903,15 @@ static hipError_t cl_bwd(const T* x, int64_t sxb, int64_t sxl, const float* w, c
     if (vec) {
       if (conv_cl_cv(C) == 4) {
         dim3 g4((C + 255) / 256, grid.y, grid.z);
-        W_SWITCH(Wd, hipLaunchKernelGGL((conv_cl_bwd_bf16_k<WW, CLB_T, 4>), g4, block, 0, st, x, sxb, sxl, w, bias,
-                                        g, sgb, sgl, dx, sdb, sdl, part, pacc, L, C, silu));
+        if (silu) W_SWITCH(Wd, hipLaunchKernelGGL((conv_cl_bwd_bf16_k<WW, CLB_T, 4, true>), g4, block, 0, st, x, sxb,
+                                                  sxl, w, bias, g, sgb, sgl, dx, sdb, sdl, part, pacc, L, C));
+        else W_SWITCH(Wd, hipLaunchKernelGGL((conv_cl_bwd_bf16_k<WW, CLB_T, 4, false>), g4, block, 0, st, x, sxb, sxl,
+                                             w, bias, g, sgb, sgl, dx, sdb, sdl, part, pacc, L, C));
       } else {
-        W_SWITCH(Wd, hipLaunchKernelGGL((conv_cl_bwd_bf16_k<WW, CLB_T, 8>), grid, block, 0, st, x, sxb, sxl, w, bias,
-                                        g, sgb, sgl, dx, sdb, sdl, part, pacc, L, C, silu));
+        if (silu) W_SWITCH(Wd, hipLaunchKernelGGL((conv_cl_bwd_bf16_k<WW, CLB_T, 8, true>), grid, block, 0, st, x, sxb,
+                                                  sxl, w, bias, g, sgb, sgl, dx, sdb, sdl, part, pacc, L, C));
+        else W_SWITCH(Wd, hipLaunchKernelGGL((conv_cl_bwd_bf16_k<WW, CLB_T, 8, false>), grid, block, 0, st, x, sxb,
+                                             sxl, w, bias, g, sgb, sgl, dx, sdb, sdl, part, pacc, L, C));
       }
       MAMBA_HIP_CHECK(hipGetLastError());
       return dw ? launch_colsum(part, conv_cl_bwd_partial_rows(Bn, L), C * (Wd + 1), dw, st) : hipSuccess;

@@ -161,12 +161,13 @@ __global__ __launch_bounds__(256) void add_rmsnorm_fwd_t_k(
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
-  float v[NCH][4], r[NCH][4];
+  float v[NCH][4], r[NCH][4], wv[NCH][4];
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     const int col = (lane + 64 * c) * 4, cc = col < D ? col : 0;
     ld4<TX>(x + row * sx + cc, v[c]);
     if (RES) ld4<TR>(res + row * sr + cc, r[c]);
+    ld4<float>(w + cc, wv[c]);
   }
   float ss = 0.f;
 #pragma unroll
@@ -189,10 +190,9 @@ __global__ __launch_bounds__(256) void add_rmsnorm_fwd_t_k(
   for (int c = 0; c < NCH; ++c) {
     const int col = (lane + 64 * c) * 4;
     if (col < D) {
-      float wv[4], o[4];
-      ld4<float>(w + col, wv);
+      float o[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) o[k] = v[c][k] * rs * wv[k];
+      for (int k = 0; k < 4; ++k) o[k] = v[c][k] * rs * wv[c][k];
       st4<TX>(y + row * D + col, o);
     }
   }
@@ -605,11 +605,14 @@ __global__ __launch_bounds__(256) void gated_rmsnorm_fwd_v8_k(const bf16_t* __re
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
   uint4 px[NCH], pz[NCH];
+  float4 w0[NCH], w1[NCH];  // w issued with the row, not after the reduction (an L2 round trip per chunk)
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     const int col = (lane + 64 * c) * 8;
     px[c] = *reinterpret_cast<const uint4*>(x + row * sx + col);
     pz[c] = *reinterpret_cast<const uint4*>(z + row * sz + col);
+    w0[c] = *reinterpret_cast<const float4*>(w + col);
+    w1[c] = *reinterpret_cast<const float4*>(w + col + 4);
   }
   float g[NCH][8];
   float ss = 0.f;
@@ -629,8 +632,7 @@ __global__ __launch_bounds__(256) void gated_rmsnorm_fwd_v8_k(const bf16_t* __re
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     const int col = (lane + 64 * c) * 8;
-    const float4 w0 = *reinterpret_cast<const float4*>(w + col), w1 = *reinterpret_cast<const float4*>(w + col + 4);
-    const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+    const float wv[8] = {w0[c].x, w0[c].y, w0[c].z, w0[c].w, w1[c].x, w1[c].y, w1[c].z, w1[c].w};
     float o[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = g[c][j] * rs * wv[j];
@@ -646,6 +648,12 @@ __global__ __launch_bounds__(256) void gated_rmsnorm_bwd_v8_k(
     bf16_t* __restrict__ dz, int64_t sdz, float* __restrict__ part, bool pacc, int64_t M, int D) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // w staged once per block in LDS behind the dw-partial area: both passes read it per row, and from
+  // global memory the compiler rematerialised those reads (to save VGPRs) as L2 round trips with a
+  // vmcnt(0) each in the output pass
+  float* wl = lds + 4 * D;
+  for (int i = threadIdx.x * 4; i < D; i += 1024) *reinterpret_cast<float4*>(wl + i) = *reinterpret_cast<const float4*>(w + i);
+  __syncthreads();
   float acc[NCH][8];
 #pragma unroll
   for (int c = 0; c < NCH; ++c)
@@ -665,7 +673,7 @@ __global__ __launch_bounds__(256) void gated_rmsnorm_bwd_v8_k(
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int col = (lane + 64 * c) * 8;
-      const float4 w0 = *reinterpret_cast<const float4*>(w + col), w1 = *reinterpret_cast<const float4*>(w + col + 4);
+      const float4 w0 = *reinterpret_cast<const float4*>(wl + col), w1 = *reinterpret_cast<const float4*>(wl + col + 4);
       const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
       float gv[8], xv[8], zv[8];
       unpack8f(pg[c], gv);
@@ -688,7 +696,7 @@ __global__ __launch_bounds__(256) void gated_rmsnorm_bwd_v8_k(
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int col = (lane + 64 * c) * 8;
-      const float4 w0 = *reinterpret_cast<const float4*>(w + col), w1 = *reinterpret_cast<const float4*>(w + col + 4);
+      const float4 w0 = *reinterpret_cast<const float4*>(wl + col), w1 = *reinterpret_cast<const float4*>(wl + col + 4);
       const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
       float gv[8], xv[8], zv[8], ox[8], oz[8];
       unpack8f(pg[c], gv);
@@ -844,7 +852,7 @@ hipError_t launch_gated_rmsnorm_bwd(const void* dy, int ydt, const void* x, int 
   const bool fast = ydt == kBF16 && xdt == kBF16 && zdt == kBF16;
   if (fast && gated_v8_ok(D, G, nbg, xdt, zdt, sx, sz, x, z) && sdx % 8 == 0 && sdz % 8 == 0 &&
       (uintptr_t)dx % 16 == 0 && (uintptr_t)dz % 16 == 0 && (uintptr_t)dy % 16 == 0) {
-    NCH8_SWITCH(D, hipLaunchKernelGGL((gated_rmsnorm_bwd_v8_k<NCH>), dim3(g), dim3(256), lds, st, (const bf16_t*)dy,
+    NCH8_SWITCH(D, hipLaunchKernelGGL((gated_rmsnorm_bwd_v8_k<NCH>), dim3(g), dim3(256), lds + D * sizeof(float), st, (const bf16_t*)dy,
                                       (const bf16_t*)x, sx, (const bf16_t*)z, sz, w, rstd, (bf16_t*)dx, sdx,
                                       (bf16_t*)dz, sdz, part, pacc, M, D));
   } else if (fast && nbg) {
