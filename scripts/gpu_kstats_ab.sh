@@ -1,0 +1,21 @@
+#!/bin/bash
+# GPU box: per-kernel average times of one microbenchmark command in the working tree and in a built
+# worktree ab/<name>, interleaved (rocprofv3 --kernel-trace --stats only).
+#   bash scripts/gpu_kstats_ab.sh <name> <rounds> <script.py args...>
+cd /tmp && export TMPDIR=/tmp; cd $GRAFT_REPO_ROOT
+name=$1; rounds=$2; shift 2
+mkdir -p gpurun_out/kab
+for r in $(seq 1 $rounds); do
+  for side in cur $name; do
+    d=$GRAFT_REPO_ROOT; [ $side = cur ] || d=$GRAFT_REPO_ROOT/ab/$name
+    out=$GRAFT_REPO_ROOT/gpurun_out/kab/${side}_$r
+    (cd $d && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out -o k -- python3 "$@") > $out.log 2>&1 || { tail -20 $out.log; exit 1; }
+    python3 - "$out" "$side" <<'PY'
+import glob, sqlite3, sys
+db = glob.glob(sys.argv[1] + "/**/*.db", recursive=True)[0]
+c = sqlite3.connect(db)
+for n, k, t in c.execute("select name, count(*), avg(duration)/1000.0 from kernels group by name order by 3 desc limit 8"):
+    print(f"{sys.argv[2]:4s} {t:9.1f} us  x{k:<4d} {n[:90]}")
+PY
+  done
+done
