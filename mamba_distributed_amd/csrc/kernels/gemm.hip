@@ -381,6 +381,9 @@ bool wgrad_big(int M, const void* dY, const void* X) {
 // >= 8 k-steps per slice; small tiles run 2 per CU -> aim at >= 512
 int wgrad_splits(int M, int P, int Q, bool big) {
   if (big) {
+    // one round (not launchers.h split_k_count): this kernel is the side-stream in-place wgrad of the wide
+    // models, where the main stream fills a short last round and extra slabs only add traffic (Mamba-2 1.4B
+    // with the rounds-aware rule: 93.8k vs 95.0k tok/s, profiles/r4/wgrad_splits.txt)
     const int tiles = ((P + BT - 1) / BT) * ((Q + BT - 1) / BT);
     int S = std::max(1, 256 / tiles);
     while (S > 1 && M / S < 8 * WK) --S;

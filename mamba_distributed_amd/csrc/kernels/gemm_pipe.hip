@@ -626,11 +626,8 @@ bool gemm_pipe_supported(int la, int lb, int M, int N, int K, int64_t lda, int64
 }
 
 int gemm_pipe_splits(int M, int N, int K) {
-  // one workgroup per CU (128 KB of LDS): aim at ~one full round of 256 workgroups, >= 16 stages per split
-  const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
-  int S = std::max(1, 256 / tiles);
-  while (S > 1 && K / S < 8 * GP_BK) --S;
-  return S;
+  // one workgroup per CU (128 KB of LDS), >= 8 K-tiles per split (launchers.h)
+  return split_k_count(((int64_t)(M + 255) / 256) * ((N + 255) / 256), M, N, K, 8 * GP_BK);
 }
 
 hipError_t launch_gemm_pipe(int la, int lb, const void* A, int64_t lda, const void* B, int64_t ldb, void* C,

@@ -7,6 +7,22 @@
 
 namespace mamba_amd {
 
+// Split-K count of a weight-gradient GEMM with `tiles` 256x256 output tiles of a (P, Q) fp32 result over K
+// tokens, one workgroup per CU (256 CUs): minimise ceil(tiles S / 256) / S -- the time in full-K tile units,
+// so a grid just past a round (272 tiles: 2 rounds at S = 1) is split until the last round is nearly full --
+// plus the fp32 slab round trip of each extra split (P Q x 8 B at ~5 TB/s against 256 x 256 x 2K flop per CU
+// at ~3.5 TF/s: P Q / (23405 K) tile units), keeping >= min_k tokens per split.
+inline int split_k_count(int64_t tiles, int64_t P, int64_t Q, int64_t K, int64_t min_k) {
+  int best = 1;
+  double bc = 1e30;
+  for (int S = 1; S <= 16; ++S) {
+    if (S > 1 && K / S < min_k) break;
+    const double c = (double)((tiles * S + 255) / 256) / S + (double)S * P * Q / (23405.0 * K);
+    if (c < bc - 1e-9) { bc = c; best = S; }
+  }
+  return best;
+}
+
 // Backward kernels with a `part` buffer write one fp32 partial row per workgroup for a parameter
 // gradient; pacc = true ADDS into the rows instead (accumulation across the no-sync micro-steps of one
 // optimizer step), and dw == nullptr skips the final column sum (deferred to the sync micro-step).

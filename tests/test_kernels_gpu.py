@@ -688,11 +688,16 @@ def test_gemm_tn(cuda, M, N, K):
     assert wide[:, :8].abs().sum() == 0 and wide[:, 8 + N:].abs().sum() == 0
 
 
-@pytest.mark.parametrize("M,P,Q", [(32768, 768, 1536), (32768, 3352, 768), (1000, 200, 136), (64, 8, 8)])
+@pytest.mark.parametrize("M,P,Q", [(32768, 768, 1536), (32768, 3352, 768), (1000, 200, 136), (64, 8, 8),
+                                   (8192, 4352, 4096)])
 def test_gemm_wgrad(cuda, M, P, Q):
-    """dW = dY^T X in fp32 (split over M, fixed-order reduction) vs fp32 matmul; accumulate mode."""
+    """dW = dY^T X in fp32 (split over M, fixed-order reduction) vs fp32 matmul; accumulate mode.  The last shape
+    has 272 output tiles, just past one round of 256 CUs: the persistent engine's rounds-aware split rule splits
+    it (S = 1 before; this side-stream kernel keeps one round)."""
     ops = torch.ops.mamba_amd
     torch.manual_seed(1)
+    if P * Q == 4352 * 4096:
+        assert ops.gp_splits(P, Q, M) > 1
     dY = torch.randn(M, P, device=cuda).to(torch.bfloat16)
     X = torch.randn(M, Q, device=cuda).to(torch.bfloat16)
     ref = dY.float().t() @ X.float()
