@@ -447,21 +447,20 @@ __global__ __launch_bounds__(256) void conv_cl_fwd_bf16_k(const bf16_t* __restri
 #pragma unroll
   for (int k = 0; k < W - 1; ++k) ldrow(t0 - (W - 1) + k).unpack(xr[k]);
   const int nsteps = tend - t0;
-  // Groups of W rows, ping-pong between two register sets (loop unrolled by two groups): group g+1 is
-  // requested before group g is computed.  The loads are unconditional (row clamped to L-1; rows past
-  // tend are never consumed): conditional loads and a rotating copy (rx = next) made the compiler wait
-  // for the just-issued group at every back-edge.
-  auto ldgrp = [&](RowV<CV>(&r)[W], int i0) {
+  // each group of W rows is requested one group ahead (two groups of loads in flight per wave)
+  RowV<CV> rx[W];
 #pragma unroll
-    for (int u = 0; u < W; ++u) r[u].load(xb + (int64_t)min(t0 + i0 + u, L - 1) * sxl);
-  };
-  auto step = [&](RowV<CV>(&r)[W], int i0) {
+  for (int u = 0; u < W; ++u) rx[u] = ldrow(t0 + u);
+  for (int i0 = 0; i0 < nsteps; i0 += W) {
+    RowV<CV> nx[W];
+#pragma unroll
+    for (int u = 0; u < W; ++u) nx[u] = ldrow(t0 + i0 + W + u);
 #pragma unroll
     for (int u = 0; u < W; ++u) {
       const int i = i0 + u;
       if (i < nsteps) {
         const int sl = (u + W - 1) % W;
-        r[u].unpack(xr[sl]);
+        rx[u].unpack(xr[sl]);
         f2v o[NQ];
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
@@ -474,14 +473,8 @@ __global__ __launch_bounds__(256) void conv_cl_fwd_bf16_k(const bf16_t* __restri
         store_row(ob + (t0 + i) * sol, o);
       }
     }
-  };
-  RowV<CV> ra[W], rb[W];
-  ldgrp(ra, 0);
-  for (int i0 = 0; i0 < nsteps; i0 += 2 * W) {
-    ldgrp(rb, i0 + W);
-    step(ra, i0);
-    ldgrp(ra, i0 + 2 * W);
-    step(rb, i0 + W);
+#pragma unroll
+    for (int u = 0; u < W; ++u) rx[u] = nx[u];
   }
 }
 
@@ -530,27 +523,28 @@ __global__ __launch_bounds__(256) void conv_cl_bwd_bf16_k(const bf16_t* __restri
       for (int q = 0; q < NQ; ++q) dp[k][q] = f2v{0.f, 0.f};
       if (k < W - 1) ldrow(xb, sxl, t0 - (W - 1) + k).unpack(xr[k]);
     }
-    // Groups of W rows of x and dout, ping-pong between two register sets (loop unrolled by two groups):
-    // group g+1 is requested before group g is computed.  Loads are unconditional (row clamped to L-1:
-    // rows t >= L only feed terms zeroed by the t < L / t < tend guards); conditional loads and a
-    // rotating copy made the compiler wait for the just-issued group at every back-edge.
-    auto ldgrp = [&](RowV<CV>(&rx_)[W], RowV<CV>(&rg_)[W], int i0) {
+    // each group of W rows of x and dout is requested one group ahead (two groups in flight per wave)
+    RowV<CV> rx[W], rg[W];
+#pragma unroll
+    for (int u = 0; u < W; ++u) {
+      rx[u] = ldrow(xb, sxl, t0 + u);
+      rg[u] = ldrow(gb, sgl, t0 + u);
+    }
+    for (int i0 = 0; i0 < nsteps; i0 += W) {
+      RowV<CV> nx[W], ng[W];
 #pragma unroll
       for (int u = 0; u < W; ++u) {
-        const int64_t t = min(t0 + i0 + u, L - 1);
-        rx_[u].load(xb + t * sxl);
-        rg_[u].load(gb + t * sgl);
+        nx[u] = ldrow(xb, sxl, t0 + i0 + W + u);
+        ng[u] = ldrow(gb, sgl, t0 + i0 + W + u);
       }
-    };
-    auto step = [&](RowV<CV>(&x_)[W], RowV<CV>(&g_)[W], int i0) {
 #pragma unroll
       for (int u = 0; u < W; ++u) {
         const int i = i0 + u, t = t0 + i;
         if (i < nsteps) {
           const int sl = (u + W - 1) % W;  // slot of step t (compile-time after unrolling)
-          x_[u].unpack(xr[sl]);
+          rx[u].unpack(xr[sl]);
           f2v g[NQ];
-          g_[u].unpack(g);
+          rg[u].unpack(g);
 #pragma unroll
           for (int q = 0; q < NQ; ++q) {
             f2v a = bs[q];
@@ -585,14 +579,11 @@ __global__ __launch_bounds__(256) void conv_cl_bwd_bf16_k(const bf16_t* __restri
           }
         }
       }
-    };
-    RowV<CV> xa[W], ga[W], xb2[W], gb2[W];
-    ldgrp(xa, ga, 0);
-    for (int i0 = 0; i0 < nsteps; i0 += 2 * W) {
-      ldgrp(xb2, gb2, i0 + W);
-      step(xa, ga, i0);
-      ldgrp(xa, ga, i0 + 2 * W);
-      step(xb2, gb2, i0 + W);
+#pragma unroll
+      for (int u = 0; u < W; ++u) {
+        rx[u] = nx[u];
+        rg[u] = ng[u];
+      }
     }
   }
 #pragma unroll

@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU box: per-kernel average times of one microbenchmark command in the working tree and in a built
 # worktree ab/<name>, interleaved (rocprofv3 --kernel-trace --stats only).
-#   bash scripts/gpu_kstats_ab.sh <name> <rounds> <script.py args...>
+#   [KFILTER=substr] bash scripts/gpu_kstats_ab.sh <name> <rounds> <script.py args...>
 cd /tmp && export TMPDIR=/tmp; cd $GRAFT_REPO_ROOT
 name=$1; rounds=$2; shift 2
 mkdir -p gpurun_out/kab
@@ -14,8 +14,12 @@ for r in $(seq 1 $rounds); do
 import glob, sqlite3, sys
 db = glob.glob(sys.argv[1] + "/**/*.db", recursive=True)[0]
 c = sqlite3.connect(db)
-for n, k, t in c.execute("select name, count(*), avg(duration)/1000.0 from kernels group by name order by 3 desc limit 8"):
+import os
+f = os.environ.get("KFILTER", "")
+q = "select name, count(*), avg(duration)/1000.0 from kernels group by name order by 3 desc"
+for n, k, t in [r for r in c.execute(q) if f in r[0]][:8]:
     print(f"{sys.argv[2]:4s} {t:9.1f} us  x{k:<4d} {n[:90]}")
 PY
+    rm -rf "$out"  # the trace database: only the summary above is kept (gpurun_out/ returns <= 64 MiB)
   done
 done
