@@ -49,17 +49,22 @@ def run_both(fn_native, fn_ref, inputs, grad_seed=0):
 # ------------------------------------------------------------------------------------------
 @pytest.mark.parametrize("D", [256, 768, 1040])
 @pytest.mark.parametrize("with_res", [False, True])
-def test_add_rmsnorm(cuda, D, with_res):
+@pytest.mark.parametrize("dts", ["bf16_f32res", "f32", "bf16_bf16res"])
+def test_add_rmsnorm(cuda, D, with_res, dts):
+    """bf16 activations + fp32 residual stream run the typed kernels (norm.hip add_rmsnorm_*_t_k); the other dtype
+    combinations the dynamic-dtype ones.  D = 1040 leaves the last lane chunk partly past the row."""
     from mamba_distributed_amd.ops.norm import rms_norm_fn
     torch.manual_seed(0)
     M = 333
-    x = torch.randn(M, D, device=cuda, dtype=torch.bfloat16)
-    r = torch.randn(M, D, device=cuda, dtype=torch.float32) if with_res else None
+    xdt = torch.float32 if dts == "f32" else torch.bfloat16
+    rdt = torch.bfloat16 if dts == "bf16_bf16res" else torch.float32
+    x = torch.randn(M, D, device=cuda, dtype=xdt)
+    r = torch.randn(M, D, device=cuda, dtype=rdt) if with_res else None
     w = torch.rand(D, device=cuda) + 0.5
 
     def f(x, w, r):
-        y, res = rms_norm_fn(x, w, None, residual=r, prenorm=True, residual_in_fp32=True, eps=1e-5)
-        return y.float() * 1.0 + res * 0.37
+        y, res = rms_norm_fn(x, w, None, residual=r, prenorm=True, residual_in_fp32=rdt == torch.float32, eps=1e-5)
+        return y.float() * 1.0 + res.float() * 0.37
 
     on, orf, gn, gr = run_both(f, f, [x, w, r])
     assert rel(on, orf) < 1e-2
