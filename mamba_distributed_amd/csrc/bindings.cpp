@@ -785,6 +785,19 @@ Tensor gemm_tn(Tensor A, Tensor B, optional<Tensor> out) {
   return C;
 }
 
+// Y (C, R) = X (R, C)^T for a bf16 matrix with unit column stride (kernels/gemm.hip transpose_bf16_k)
+Tensor transpose_bf16(Tensor X) {
+  check_cuda(X, "X");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
+  TORCH_CHECK(X.dim() == 2 && X.scalar_type() == at::kBFloat16 && X.stride(1) == 1 && (uintptr_t)X.data_ptr() % 16 == 0,
+              "transpose_bf16: 2-D bf16, unit column stride, 16-B aligned");
+  const int64_t R = X.size(0), C = X.size(1);
+  TORCH_CHECK(R % 8 == 0 && C % 8 == 0 && X.stride(0) % 8 == 0, "transpose_bf16: sizes and row stride % 8 == 0");
+  Tensor Y = at::empty({C, R}, X.options());
+  HIPCHK(mamba_amd::launch_transpose_bf16(X.data_ptr(), X.stride(0), Y.data_ptr(), R, (int)R, (int)C, cur_stream()));
+  return Y;
+}
+
 // C (N, M) (+)= A (N, K) . B (K, M) for the channel-major Mamba-1 projections (x_proj / dt_proj and their
 // input gradients); B / out rows are contiguous along M and may be row-strided views (x_dbl[:R])
 Tensor gemm_skinny(Tensor A, Tensor B, optional<Tensor> out, bool accumulate) {
@@ -1105,6 +1118,7 @@ TORCH_LIBRARY(mamba_amd, m) {
   m.def("gp_splits(int M, int N, int K) -> int", &gp_splits);
   m.def("part_rows(str kind, int a, int b=0) -> int", &part_rows);
   m.def("gp_reduce(Tensor part, Tensor(a!) out, bool accumulate=False) -> ()");
+  m.def("transpose_bf16(Tensor X) -> Tensor");
   m.def("gemm_skinny(Tensor A, Tensor B, Tensor(a!)? out=None, bool accumulate=False) -> Tensor");
   m.def("ssm_state_update(Tensor(a!) state, Tensor x, Tensor dt, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? z, "
         "Tensor? dt_bias, bool softplus) -> Tensor");
@@ -1124,6 +1138,7 @@ TORCH_LIBRARY_IMPL(mamba_amd, CUDA, m) {
   m.impl("gp_mm", &gp_mm);
   m.impl("gp_pk", &gp_pk);
   m.impl("gp_reduce", &gp_reduce);
+  m.impl("transpose_bf16", &transpose_bf16);
   m.impl("add_rmsnorm_bwd", &add_rmsnorm_bwd);
   m.impl("gated_rmsnorm_fwd", &gated_rmsnorm_fwd);
   m.impl("gated_rmsnorm_bwd", &gated_rmsnorm_bwd);

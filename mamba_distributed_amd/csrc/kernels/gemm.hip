@@ -584,4 +584,40 @@ hipError_t launch_gemm_tn_bf16(const void* A, int64_t lda, const void* B, int64_
   return hipGetLastError();
 }
 
+// ================================ bf16 transpose (the input-gradient GEMMs' W^T operand) ===========================
+// Y (C, R) = X (R, C)^T, once per optimizer step per projection weight.  64 x 64 tiles through LDS: 16-B row loads
+// and 16-B row stores (R % 8 == 0, C % 8 == 0); torch's copy of a transposed view runs element-wise (strided
+// reads, ~16 us for a 3392 x 768 weight).
+__global__ __launch_bounds__(256) void transpose_bf16_k(const bf16_t* __restrict__ x, int64_t ldx,
+                                                        bf16_t* __restrict__ y, int64_t ldy, int R, int C) {
+  __shared__ __attribute__((aligned(16))) unsigned short t[64][72];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int idx = threadIdx.x + k * 256, r = idx >> 3, c = (idx & 7) * 8;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (r0 + r < R && c0 + c < C) v = *reinterpret_cast<const uint4*>(x + (int64_t)(r0 + r) * ldx + c0 + c);
+    *reinterpret_cast<uint4*>(&t[r][c]) = v;
+  }
+  __syncthreads();
+  const int i = threadIdx.x >> 2, j0 = (threadIdx.x & 3) * 16;
+  if (c0 + i >= C) return;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int j = j0 + 8 * h;
+    if (r0 + j >= R) break;
+    unsigned q[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) q[e] = (unsigned)t[j + 2 * e][i] | ((unsigned)t[j + 2 * e + 1][i] << 16);
+    *reinterpret_cast<uint4*>(y + (int64_t)(c0 + i) * ldy + r0 + j) = make_uint4(q[0], q[1], q[2], q[3]);
+  }
+}
+
+hipError_t launch_transpose_bf16(const void* x, int64_t ldx, void* y, int64_t ldy, int R, int C, hipStream_t st) {
+  if (R <= 0 || C <= 0 || R % 8 || C % 8 || ldx % 8 || ldy % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(transpose_bf16_k, dim3((C + 63) / 64, (R + 63) / 64), dim3(256), 0, st, (const bf16_t*)x, ldx,
+                     (bf16_t*)y, ldy, R, C);
+  return hipGetLastError();
+}
+
 }  // namespace mamba_amd

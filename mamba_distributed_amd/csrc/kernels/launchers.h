@@ -127,6 +127,7 @@ hipError_t launch_gemm_pk(int la, int lb, const void* A, int64_t lda, const void
 int gemm_pipe_waves();
 void set_gemm_pipe_waves(int w);
 // out[i] (+)= sum_s part[s * stride + i], fixed order
+hipError_t launch_transpose_bf16(const void* x, int64_t ldx, void* y, int64_t ldy, int R, int C, hipStream_t st);
 hipError_t launch_gp_reduce(const float* part, int S, int64_t stride, int64_t n, float* out, bool accumulate,
                             hipStream_t st);
 

@@ -185,16 +185,27 @@ def cached_value(w: torch.Tensor, tag: str, fn):
     return t
 
 
+def _transpose(w: torch.Tensor) -> torch.Tensor:
+    """``w.t().contiguous()``; bf16 GPU matrices on the native 64 x 64-tile transpose (csrc/kernels/gemm.hip
+    transpose_bf16_k: 16-B row loads and stores; torch copies a transposed view element by element)."""
+    if (w.is_cuda and w.dtype == torch.bfloat16 and w.dim() == 2 and w.stride(1) == 1 and w.shape[0] % 8 == 0
+            and w.shape[1] % 8 == 0 and w.stride(0) % 8 == 0 and w.data_ptr() % 16 == 0):
+        from . import _ext
+        if _ext.use_native(w):
+            return _ext.ops().transpose_bf16(w)
+    return w.t().contiguous()
+
+
 def cached_transpose(w: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     """``w.to(dtype).t().contiguous()`` (the input-gradient GEMM's k-contiguous B operand), reused across
     the micro-steps of the current scope like ``cached_cast``."""
     if _scope_depth == 0:
-        return w.to(dtype).t().contiguous()
+        return _transpose(w.to(dtype))
     key = (id(w), dtype, "t")
     ent = _wcache.get(key)
     if ent is not None and ent[0] is w:
         return ent[1]
-    t = cached_cast(w, dtype).t().contiguous()
+    t = _transpose(cached_cast(w, dtype))
     _wcache[key] = (w, t)
     return t
 

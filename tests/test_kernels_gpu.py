@@ -715,6 +715,16 @@ def test_gemm_wgrad(cuda, M, P, Q):
     assert torch.equal(C, C2)  # deterministic
 
 
+@pytest.mark.parametrize("R,C", [(3392, 768), (768, 3352), (40, 72), (8, 8)])
+def test_transpose_bf16(cuda, R, C):
+    """The native bf16 transpose behind grad_accum.cached_transpose (partial 64 x 64 tiles included) is exact."""
+    from mamba_distributed_amd.ops import grad_accum
+    x = torch.randn(R, C, device=cuda).to(torch.bfloat16)
+    y = torch.ops.mamba_amd.transpose_bf16(x)
+    assert y.shape == (C, R) and torch.equal(y, x.t())
+    assert torch.equal(grad_accum.cached_transpose(x, torch.bfloat16), x.t())
+
+
 @pytest.mark.parametrize("layer", ["Mamba1", "Mamba2"])
 def test_in_place_grad_accumulation_matches_autograd(cuda, layer):
     """accumulation_scope (in-place split-K wgrad accumulation + one batched add for the small
