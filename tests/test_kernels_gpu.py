@@ -116,6 +116,26 @@ def test_conv1d(cuda, layout, L, d):
         assert rel(a, b_) < 2e-2
 
 
+@pytest.mark.parametrize("L,act", [(512, "silu"), (1536, None), (2048, "silu")])
+def test_conv1d_channel_first_whole_chunks(cuda, L, act):
+    """Channel-first rows of 1 / 3 / 4 whole 512-step chunks (the chunk carry and halo across chunk boundaries),
+    with and without the SiLU."""
+    from mamba_distributed_amd.ops.conv1d import causal_conv1d_fn
+    torch.manual_seed(5)
+    b, d, W = 2, 136, 4
+    base = torch.randn(b, 2 * d, L, device=cuda, dtype=torch.bfloat16)
+    w = torch.randn(d, 1, W, device=cuda) * 0.5
+    bias = torch.randn(d, device=cuda) * 0.1
+
+    def f(base, w, bias):
+        return causal_conv1d_fn(base[:, :d], w, bias, act)
+
+    on, orf, gn, gr = run_both(f, f, [base, w, bias])
+    assert rel(on, orf) < 1e-2
+    for a, b_ in zip(gn, gr):
+        assert rel(a, b_) < 2e-2
+
+
 def test_cross_entropy(cuda):
     from mamba_distributed_amd.ops.cross_entropy import cross_entropy, fused_linear_cross_entropy
     torch.manual_seed(3)
