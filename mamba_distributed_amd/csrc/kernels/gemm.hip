@@ -444,6 +444,8 @@ __global__ __launch_bounds__(256) void gemm_skinny_k(const bf16_t* __restrict__ 
   constexpr int WM = TM / 4, NJ = WM / 16, MI = SK_TN / 16;
   constexpr int AB = SK_TN * LDA_ * 2, BB = BK * LDB_ * 2, CB = SK_TN * LDC_ * 2;
   constexpr int SMEM = (AB + BB) > CB ? (AB + BB) : CB;
+  constexpr int QA = (SK_TN * BK / 8 + 255) / 256, QB = BK * TM / 8 / 256, QC = SK_TN * TM / 8 / 256;
+  static_assert(BK * TM / 8 % 256 == 0 && SK_TN * TM / 8 % 256 == 0, "whole 16-B pieces per thread");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   bf16_t* As = reinterpret_cast<bf16_t*>(smem);
   bf16_t* Bs = reinterpret_cast<bf16_t*>(smem + AB);
@@ -454,22 +456,39 @@ __global__ __launch_bounds__(256) void gemm_skinny_k(const bf16_t* __restrict__ 
   for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = zero4();
+  // Every global load is unconditional, from a clamped (legal) address, and zeroed by a select where it is
+  // consumed: a guarded load meets its zero in a phi and is waited for on the spot.  The stage after the
+  // current one is requested before the current one's MFMAs, and (ACC) every piece of the C tile the epilogue
+  // adds into is requested at once -- in the guarded form the epilogue's 8 read-add-write rounds ran one HBM
+  // latency each.
+  uint4 ra[QA], rb[QB], rc[QC];
+  auto ld_stage = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < QA; ++u) {
+      const int q = threadIdx.x + 256 * u, r = q / (BK / 8), c = (q % (BK / 8)) * 8;
+      ra[u] = *reinterpret_cast<const uint4*>(A + (int64_t)min(n0 + r, N - 1) * lda + min(k0 + c, K - 8));
+    }
+#pragma unroll
+    for (int u = 0; u < QB; ++u) {
+      const int q = threadIdx.x + 256 * u, kk = q / (TM / 8), c = (q % (TM / 8)) * 8;
+      rb[u] = *reinterpret_cast<const uint4*>(B + (int64_t)min(k0 + kk, K - 1) * ldb + min(m0 + c, M - 8));
+    }
+  };
+  ld_stage(0);
   for (int k0 = 0; k0 < K; k0 += BK) {
 #pragma unroll
-    for (int q = threadIdx.x; q < SK_TN * BK / 8; q += 256) {  // A tile: 64 rows x BK
-      const int r = q / (BK / 8), c = (q % (BK / 8)) * 8;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (n0 + r < N && k0 + c < K) v = *reinterpret_cast<const uint4*>(A + (int64_t)(n0 + r) * lda + k0 + c);
-      *reinterpret_cast<uint4*>(As + r * LDA_ + c) = v;
+    for (int u = 0; u < QA; ++u) {  // A tile: 64 rows x BK
+      const int q = threadIdx.x + 256 * u, r = q / (BK / 8), c = (q % (BK / 8)) * 8;
+      if (q < SK_TN * BK / 8)
+        *reinterpret_cast<uint4*>(As + r * LDA_ + c) = (n0 + r < N && k0 + c < K) ? ra[u] : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
-    for (int q = threadIdx.x; q < BK * TM / 8; q += 256) {  // B tile: BK k-rows x TM tokens
-      const int kk = q / (TM / 8), c = (q % (TM / 8)) * 8;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (k0 + kk < K && m0 + c < M) v = *reinterpret_cast<const uint4*>(B + (int64_t)(k0 + kk) * ldb + m0 + c);
-      *reinterpret_cast<uint4*>(Bs + kk * LDB_ + c) = v;
+    for (int u = 0; u < QB; ++u) {  // B tile: BK k-rows x TM tokens
+      const int q = threadIdx.x + 256 * u, kk = q / (TM / 8), c = (q % (TM / 8)) * 8;
+      *reinterpret_cast<uint4*>(Bs + kk * LDB_ + c) = (k0 + kk < K && m0 + c < M) ? rb[u] : make_uint4(0, 0, 0, 0);
     }
     __syncthreads();
+    ld_stage(min(k0 + BK, (K - 1) / BK * BK));  // the next stage (the last one again at the end)
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
       bf16x8 bfr[NJ];
@@ -494,27 +513,33 @@ __global__ __launch_bounds__(256) void gemm_skinny_k(const bf16_t* __restrict__ 
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         Cs[(16 * i + 4 * (l >> 4) + r) * LDC_ + w * WM + 16 * j + (l & 15)] = f2bf(acc[i][j][r]);
-  __syncthreads();
-  for (int q = threadIdx.x; q < SK_TN * TM / 8; q += 256) {
-    const int r = q / (TM / 8), c = (q % (TM / 8)) * 8;
-    if (n0 + r < N && m0 + c < M) {
-      bf16_t* dst = C + (int64_t)(n0 + r) * ldc + m0 + c;
-      uint4 v = *reinterpret_cast<const uint4*>(Cs + r * LDC_ + c);
-      if (ACC) {
-        float f[8], o[8];
-        ld8bf(reinterpret_cast<const bf16_t*>(&v), f);
-        ld8bf(dst, o);
+  if (ACC) {  // all of the tile's C pieces in flight at once (the accumulators are dead: no register cost)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) f[e] += o[e];
-        st8bf(reinterpret_cast<bf16_t*>(&v), f);
-      }
-      *reinterpret_cast<uint4*>(dst) = v;
+    for (int u = 0; u < QC; ++u) {
+      const int q = threadIdx.x + 256 * u, r = q / (TM / 8), c = (q % (TM / 8)) * 8;
+      rc[u] = *reinterpret_cast<const uint4*>(C + (int64_t)min(n0 + r, N - 1) * ldc + min(m0 + c, M - 8));
     }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < QC; ++u) {
+    const int q = threadIdx.x + 256 * u, r = q / (TM / 8), c = (q % (TM / 8)) * 8;
+    uint4 v = *reinterpret_cast<const uint4*>(Cs + r * LDC_ + c);
+    if (ACC) {
+      float f[8], o[8];
+      ld8bf(reinterpret_cast<const bf16_t*>(&v), f);
+      ld8bf(reinterpret_cast<const bf16_t*>(&rc[u]), o);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] += o[e];
+      st8bf(reinterpret_cast<bf16_t*>(&v), f);
+    }
+    if (n0 + r < N && m0 + c < M) *reinterpret_cast<uint4*>(C + (int64_t)(n0 + r) * ldc + m0 + c) = v;
   }
 }
 
 bool gemm_skinny_supported(int N, int K, int M, int64_t lda, int64_t ldb, int64_t ldc) {
-  return N > 0 && K > 0 && M > 0 && K % 8 == 0 && M % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0;
+  // K, M >= 8: the clamped 16-B loads (min(k, K - 8), min(m, M - 8)) stay inside the operands
+  return N > 0 && K >= 8 && M >= 8 && K % 8 == 0 && M % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0;
 }
 
 hipError_t launch_gemm_skinny(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int N,
