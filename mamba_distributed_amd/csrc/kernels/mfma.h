@@ -79,29 +79,41 @@ __device__ __forceinline__ bf16x8 scale_frag(bf16x8 v, float s) {
   return r;
 }
 
-// ---- global <-> LDS tile staging (256 threads, 16-B chunks) ---------------------------------
-// copy rows [0, R) x cols [0, Cn) of a bf16 global tile (row stride gs elements) into LDS
-// [R][ld]; rows >= valid are zero-filled; optional per-row fp32 scale.  Cn % 8 == 0.
-template <int R, int Cn>
-__device__ __forceinline__ void stage_tile(bf16_t* lds, int ld, const bf16_t* g, int64_t gs, int valid,
-                                           const float* rowscale = nullptr) {
-  constexpr int CPR = Cn / 8;  // 16-B chunks per row
-  for (int v = threadIdx.x; v < R * CPR; v += blockDim.x) {
-    const int r = v / CPR, c = (v % CPR) * 8;
-    uint4 d = make_uint4(0, 0, 0, 0);
-    if (r < valid) {
-      d = *reinterpret_cast<const uint4*>(g + (int64_t)r * gs + c);
-      if (rowscale) {
-        float f[8];
-        ld8bf(reinterpret_cast<const bf16_t*>(&d), f);
-        const float s = rowscale[r];
+// ---- global <-> LDS tile staging (16-B chunks) ---------------------------------------------
+// Register staging in two halves, so several tiles' loads can be in flight before the first LDS store: rows
+// >= valid re-read the last valid row (a legal address) and are zeroed at the store -- a guarded load meets its
+// zero in a phi and is waited for on the spot.
+template <int R, int Cn, int NT>
+struct StageRegs {
+  static constexpr int CPR = Cn / 8;  // 16-B chunks per row
+  static constexpr int K = (R * CPR + NT - 1) / NT;
+  uint4 d[K];
+  int nv;
+  __device__ __forceinline__ void load(const bf16_t* g, int64_t gs, int valid) {
+    nv = valid;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] *= s;
-        st8bf(reinterpret_cast<bf16_t*>(&d), f);
-      }
+    for (int k = 0; k < K; ++k) {
+      const int v = threadIdx.x + k * NT, r = min(v / CPR, R - 1), c = (v % CPR) * 8;
+      if (R * CPR % NT == 0 || v < R * CPR) d[k] = *reinterpret_cast<const uint4*>(g + (int64_t)min(r, valid - 1) * gs + c);
     }
-    *reinterpret_cast<uint4*>(lds + r * ld + c) = d;
   }
+  __device__ __forceinline__ void store(bf16_t* lds, int ld) const {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int v = threadIdx.x + k * NT, r = v / CPR, c = (v % CPR) * 8;
+      if (R * CPR % NT != 0 && v >= R * CPR) break;
+      *reinterpret_cast<uint4*>(lds + r * ld + c) = r < nv ? d[k] : make_uint4(0, 0, 0, 0);
+    }
+  }
+};
+
+// copy rows [0, R) x cols [0, Cn) of a bf16 global tile (row stride gs elements) into LDS [R][ld]; rows >= valid
+// are zero-filled.  Cn % 8 == 0; NT threads.
+template <int R, int Cn, int NT>
+__device__ __forceinline__ void stage_tile(bf16_t* lds, int ld, const bf16_t* g, int64_t gs, int valid) {
+  StageRegs<R, Cn, NT> t;
+  t.load(g, gs, valid);
+  t.store(lds, ld);
 }
 
 // accumulator tile (16x16 at rows r0.., cols c0..) -> LDS bf16 [..][ld]

@@ -501,8 +501,13 @@ __global__ __launch_bounds__(512) void ssd_chunk_bwd_k(SSDArgs a, unsigned long 
   prefetch_ds(h0);
   for (int v = threadIdx.x; v < 8 * 8 * Q; v += 512) (&dcw[0][0][0])[v] = 0.f;
   for (int v = threadIdx.x; v < 8 * 2 * Q; v += 512) (&ddw[0][0][0])[v] = 0.f;
-  stage_tile<Q, N>(Cs, LDN, a.Cm + (int64_t)b * a.sCb + (int64_t)c * Q * a.sCl + (int64_t)g * a.sCg, a.sCl, valid);
-  stage_tile<Q, N>(Bs, LDN, a.Bm + (int64_t)b * a.sBb + (int64_t)c * Q * a.sBl + (int64_t)g * a.sBg, a.sBl, valid);
+  {  // both tiles' loads in flight before the first LDS store
+    StageRegs<Q, N, 512> sc, sb;
+    sc.load(a.Cm + (int64_t)b * a.sCb + (int64_t)c * Q * a.sCl + (int64_t)g * a.sCg, a.sCl, valid);
+    sb.load(a.Bm + (int64_t)b * a.sBb + (int64_t)c * Q * a.sBl + (int64_t)g * a.sBg, a.sBl, valid);
+    sc.store(Cs, LDN);
+    sb.store(Bs, LDN);
+  }
   // (1)(2) tile ownership: the 10 lower-triangular 16x16 tiles (I >= J) of M / dM go to the 8 waves
   // (waves 0 and 1 take two diagonal tiles each) -- no tile is computed twice and the busiest wave has
   // 2 tiles (a column-tile split gives 4:3:2:1).  M^T goes through LDS to the waves that need it in (3).
@@ -864,8 +869,13 @@ __global__ __launch_bounds__(256) void ssd_dbc_bwd_k(SSDArgs a) {
   const int valid = min(Q, a.L - c * Q);
   const int hpg = a.H / a.G;
   const int hg0 = g * hpg / a.HG, hg1 = (g + 1) * hpg / a.HG;
-  stage_tile<Q, N>(Cs, LDN, a.Cm + (int64_t)b * a.sCb + (int64_t)c * Q * a.sCl + (int64_t)g * a.sCg, a.sCl, valid);
-  stage_tile<Q, N>(Bs, LDN, a.Bm + (int64_t)b * a.sBb + (int64_t)c * Q * a.sBl + (int64_t)g * a.sBg, a.sBl, valid);
+  {  // both tiles' loads in flight before the first LDS store
+    StageRegs<Q, N, 256> sc, sb;
+    sc.load(a.Cm + (int64_t)b * a.sCb + (int64_t)c * Q * a.sCl + (int64_t)g * a.sCg, a.sCl, valid);
+    sb.load(a.Bm + (int64_t)b * a.sBb + (int64_t)c * Q * a.sBl + (int64_t)g * a.sBg, a.sBl, valid);
+    sc.store(Cs, LDN);
+    sb.store(Bs, LDN);
+  }
   for (int v = threadIdx.x; v < Q * Q; v += 256) {
     float s = 0.f;
     for (int hg = hg0; hg < hg1; ++hg) s += a.part_dcb[((((int64_t)b * a.nc + c) * a.nhg + hg) * Q) * Q + v];
