@@ -240,6 +240,8 @@ class _Mamba1InnerFn(torch.autograd.Function):
         ctx.save_for_backward(xz, w2, conv_b, Wx, Wdt, dt_bias, A, D, conv_out, x_dbl, delta, carries)
         ctx.meta = (b, l, conv_w.shape, W_x.dtype, W_dt.dtype)
         ctx.wparams = (W_x, W_dt)  # the parameters themselves (native weight gradients accumulate into .grad)
+        # key of the deferred A / D / dt-bias partials: the dt bias parameter itself (fp32: .float() is the leaf)
+        ctx.pkey = dt_bias if (dt_bias is not None and dt_bias.is_leaf and dt_bias.requires_grad) else None
         return _flat(y)
 
     @staticmethod
@@ -257,10 +259,18 @@ class _Mamba1InnerFn(torch.autograd.Function):
         Bm = _cm(x_dbl[R:R + N], b, l).unsqueeze(1)
         Cm = _cm(x_dbl[R + N:], b, l).unsqueeze(1)
         dx_dbl = torch.empty_like(x_dbl)
+        # the A / D / dt-bias gradient partials (B x D x (N + 2) fp32) are summed over the batch once per optimizer
+        # step, even though Mamba-1 reduces its other partials every micro-step (microbatch.auto_defer_reduce):
+        # per micro-step that reduction is a zero fill, two batch sums, casts and three small gradient adds
+        d_s = (grad_accum.deferred(ctx.pkey, "selscan_small", (b * di * (N + 2),), xz.device, force=True)
+               if ctx.pkey is not None else None)
         du, ddelta, dA, dB, dC, dD, dz, ddt_bias = ops.selscan_bwd_into(
             _cm(dy2.contiguous() if dy2.stride(-1) != 1 else dy2, b, l), conv_out, _cm(delta, b, l), A,
             Bm, Cm, D, z, dt_bias, carries, True,
-            dxz3[:, di:], _cm(dx_dbl[R:R + N], b, l).unsqueeze(1), _cm(dx_dbl[R + N:], b, l).unsqueeze(1))
+            dxz3[:, di:], _cm(dx_dbl[R:R + N], b, l).unsqueeze(1), _cm(dx_dbl[R + N:], b, l).unsqueeze(1),
+            *(d_s or (None, 0)))
+        nz = lambda t: t if t.numel() else None  # noqa: E731  (empty: deferred to the sync micro-step)
+        dA, dD, ddt_bias = nz(dA), nz(dD), nz(ddt_bias)
         dd2 = _flat(ddelta)
         pWx, pWdt = ctx.wparams
         # both operands channel-major: (di, M) . (R, M)^T on the native wgrad GEMM

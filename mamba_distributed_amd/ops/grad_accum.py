@@ -107,7 +107,7 @@ def join_side() -> None:
     _side_dirty.clear()
 
 
-def deferred(param, tag: str, shape, device):
+def deferred(param, tag: str, shape, device, force: bool = False):
     """Deferred reduction of ``param``'s gradient inside an accumulation scope.
 
     Returns None outside a scope (the op reduces as usual), else ``(buffer, part_mode)``: a persistent fp32
@@ -115,12 +115,13 @@ def deferred(param, tag: str, shape, device):
     micro-step's partials, no reduction, the op returns an empty gradient (no-sync micro-step); 3 / 4:
     store / add, then reduce: the op returns the gradient of every micro-step of this optimizer step
     (sync micro-step).  A second call in the same sync micro-step starts over (3) and its gradient is
-    added by autograd as usual."""
+    added by autograd as usual.  ``force``: defer even when the scope did not ask for deferred reductions
+    (small partials whose per-micro-step reduction is pure launch overhead; MAMBA_AMD_DEFER_REDUCE=0 still wins)."""
     import os
     if _scope_depth == 0 or not isinstance(param, torch.Tensor) or not param.requires_grad:
         return None
     env = os.environ.get("MAMBA_AMD_DEFER_REDUCE", "")
-    if env == "0" or (env != "1" and not _defer_scope):
+    if env == "0" or (env != "1" and not _defer_scope and not force):
         return None
     key = (id(param), tag)
     shape = tuple(int(v) for v in shape)
