@@ -25,7 +25,7 @@ import torch.nn.functional as F
 
 from ..ops import _ext, grad_accum
 from ..ops.conv1d import causal_conv1d_fn, causal_conv1d_update
-from ..ops.linear import mm_nt
+from ..ops.linear import _wgrad_inplace, mm_nt
 from ..ops.reference import causal_conv1d_ref, selective_scan_ref, softplus_inverse
 from ..ops.selective_scan import selective_scan_fn, selective_state_update
 
@@ -157,7 +157,8 @@ def _wgrad_native(p, dY, X, dy_cm, x_cm):
           and dY.data_ptr() % 16 == 0 and X.data_ptr() % 16 == 0)
     if not ok:
         return False, None
-    if grad_accum.accumulable(p) and p.grad.dtype == torch.float32 and p.grad.is_contiguous():
+    if (grad_accum.accumulable(p) and p.grad.dtype == torch.float32 and p.grad.is_contiguous()
+            and _wgrad_inplace(dY.device)):
         side = grad_accum.side_stream(dY.device)
         if side is None:
             _ext.ops().gemm_wgrad_cm(dY, X, p.grad, True, dy_cm, x_cm)

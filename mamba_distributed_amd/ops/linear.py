@@ -90,8 +90,8 @@ _INPLACE_STATE: dict = {}   # device index -> [calls until the next re-check, de
 def _wgrad_inplace(dev) -> bool:
     """Non-deferred no-sync micro-steps: the split-K wgrad adds into p.grad in place on the side stream, or (False)
     transient fp32 slabs on the persistent engine, reduced on the main stream. MAMBA_AMD_WGRAD_INPLACE=1/0 forces
-    either; auto takes the side stream while the allocated peak stays under 70% of the device and the caching
-    allocator has never had to retry (re-checked every 64 calls: memory_stats() is not free). The side-stream form
+    either; auto takes the side stream while the allocated peak stays under 70% of the device, the reserved peak
+    under 96%, and the caching allocator has never had to retry (re-checked every 64 calls: memory_stats() is not free). The side-stream form
     keeps dy/x alive (record_stream) past the main stream's frees; near capacity that turns into allocator
     retries, which synchronise the device: Mamba-2 2.8B @ 8192 (222 GiB peak) ran 29.6k tok/s with it (17
     retries) vs 46.8k without, while 1.4B @ 1024 (130 GiB) gains ~8% from it (profiles/r3/ab15_*)."""
@@ -105,7 +105,10 @@ def _wgrad_inplace(dev) -> bool:
         st = _INPLACE_STATE[key] = [0, True, torch.cuda.get_device_properties(key).total_memory]
     if st[0] <= 0:
         s = torch.cuda.memory_stats(key)
-        st[1] = (s.get("allocated_bytes.all.peak", 0) < 0.7 * st[2]) and s.get("num_alloc_retries", 0) == 0
+        # reserved: the side stream's record_stream lifetimes grow the reserved peak well past the allocated one
+        # (Mamba-1 370M: 112 GB allocated, 269 GB reserved); at the cap every allocation retries first
+        st[1] = (s.get("allocated_bytes.all.peak", 0) < 0.7 * st[2] and s.get("num_alloc_retries", 0) == 0
+                 and s.get("reserved_bytes.all.peak", 0) < 0.96 * st[2])
         st[0] = 64
     st[0] -= 1
     return st[1]
