@@ -40,11 +40,16 @@ __global__ __launch_bounds__(CE_THREADS) void ce_fwd_bf16_k(const bf16_t* __rest
   const int nvec = V / 8;
   uint4 cache[CE_MAXV];
   float m = -INFINITY;
+  // the row's loads all in flight before the first use: a per-lane guard around each load made the compiler
+  // wait for every one of them on the spot (16 serialized HBM round trips per row); the guard is uniform per
+  // slot here and lanes past the row re-read its last vector
+#pragma unroll
+  for (int i = 0; i < CE_MAXV; ++i)
+    if (i * CE_THREADS < nvec) cache[i] = reinterpret_cast<const uint4*>(p)[min((int)threadIdx.x + i * CE_THREADS, nvec - 1)];
 #pragma unroll
   for (int i = 0; i < CE_MAXV; ++i) {
     const int vi = threadIdx.x + i * CE_THREADS;
     if (vi < nvec) {
-      cache[i] = reinterpret_cast<const uint4*>(p)[vi];
       unsigned wv[4] = {cache[i].x, cache[i].y, cache[i].z, cache[i].w};
 #pragma unroll
       for (int k = 0; k < 4; ++k)
