@@ -101,10 +101,22 @@ __global__ __launch_bounds__(256) void ssd_cumsum_k(SSDArgs a) {
   for (int h0 = 0; h0 < a.H; h0 += CS_HMAX) {
     const int nh = min(CS_HMAX, a.H - h0);
     if (h0 > 0) __syncthreads();  // the previous pass's readers are done
-    for (int e = threadIdx.x; e < Q * nh; e += 256) {
-      const int r = e / nh, hh = e - r * nh, tr = c * Q + r;
-      raw_s[r][hh] = tr < a.L ? ld_any(a.dt, a.dt_dtype, (int64_t)b * a.sdtb + (int64_t)tr * a.sdtl + (int64_t)(h0 + hh) * a.sdth)
-                              : 0.f;
+    {  // every element's load in flight before the first LDS store (ld_raw: branch-free, clamped row)
+      constexpr int NE = (Q * CS_HMAX + 255) / 256;
+      RawF rv[NE];
+#pragma unroll
+      for (int k = 0; k < NE; ++k) {
+        const int e = min((int)threadIdx.x + 256 * k, Q * nh - 1), r = e / nh, hh = e - r * nh;
+        const int tr = min(c * Q + r, a.L - 1);
+        rv[k] = ld_raw(a.dt, a.dt_dtype, (int64_t)b * a.sdtb + (int64_t)tr * a.sdtl + (int64_t)(h0 + hh) * a.sdth);
+      }
+#pragma unroll
+      for (int k = 0; k < NE; ++k) {
+        const int e = threadIdx.x + 256 * k;
+        if (e >= Q * nh) break;
+        const int r = e / nh, hh = e - r * nh;
+        raw_s[r][hh] = c * Q + r < a.L ? raw_f(rv[k], a.dt_dtype) : 0.f;
+      }
     }
     __syncthreads();
     for (int hh = w; hh < nh; hh += 4) {
