@@ -131,7 +131,10 @@ def main():
     assert a.global_batch_tokens % (a.B * a.T * world) == 0
     accum = a.global_batch_tokens // (a.B * a.T * world)
     from mamba_distributed_amd.utils.gemm_tuning import enable_tuned_gemms
-    tuned = False if a.no_tuned_gemms else enable_tuned_gemms()
+    # the TunableOp table only matters when a library GEMM can run: the hipBLASLt A/B switches, or the reference ops
+    lib_gemms = (os.environ.get("MAMBA_AMD_PROJ_GEMM", "pk") != "pk" or os.environ.get("MAMBA_AMD_LMHEAD") == "lib"
+                 or a.reference_ops)
+    tuned = False if (a.no_tuned_gemms or not lib_gemms) else enable_tuned_gemms()
     torch.manual_seed(1337)
     model = LMHeadModel(cfg, device=dev)
     if a.activation_checkpointing:
@@ -245,7 +248,8 @@ def main():
                 "seq_len": a.T,
                 "parallelism": f"dp{world}",
                 "ops": "pytorch-reference" if (a.reference_ops or not on_gpu) else "native-hip",
-                "gemm_table": "tunableop-gfx950" if tuned else "library-default",
+                "gemm_table": ("tunableop-gfx950" if tuned else "library-default") if lib_gemms
+                              else "unused (every GEMM on the native engines)",
                 "microbatch_overlap": overlap,
                 "dp_impl": a.dp_impl if world > 1 else "none",
                 "activation_checkpointing": a.activation_checkpointing,

@@ -954,8 +954,14 @@ Tensor gp_pk(Tensor A, Tensor B, optional<Tensor> out, int64_t la, int64_t lb, i
   TORCH_CHECK(mamba_amd::gemm_pk_supported((int)la, (int)lb, (int)mode, (int)M, (int)N, (int)K, lda, ldb, ldc),
               "gp_pk: unsupported shape/strides (M=", M, " N=", N, " K=", K, " lda=", lda, " ldb=", ldb, " ldc=", ldc,
               "; needs strides and N % 8, KC K % 8, XC A M % 8, operands < 4 GB)");
-  HIPCHK(mamba_amd::launch_gemm_pk((int)la, (int)lb, A.data_ptr(), lda, B.data_ptr(), ldb, C.data_ptr(), ldc, (int)M,
-                                   (int)N, (int)K, (int)mode, rs, cur_stream()));
+  const hipError_t e = mamba_amd::launch_gemm_pk((int)la, (int)lb, A.data_ptr(), lda, B.data_ptr(), ldb, C.data_ptr(),
+                                                 ldc, (int)M, (int)N, (int)K, (int)mode, rs, cur_stream());
+  TORCH_CHECK(e != hipErrorNotReady,
+              "gp_pk: no tile-claim counter pair: either the first gp_pk launch of this device is inside a HIP graph "
+              "capture (run one eager launch first), or this process has captured more than ",
+              mamba_amd::gemm_pk_graph_counter_capacity(), " gp_pk launches into graphs (captured pairs are never "
+              "recycled: re-capture less often, e.g. reuse a GraphedDecoder instead of rebuilding it)");
+  HIPCHK(e);
   return C;
 }
 
@@ -963,9 +969,9 @@ Tensor gp_pk(Tensor A, Tensor B, optional<Tensor> out, int64_t la, int64_t lb, i
 void ssd_stamps(optional<Tensor> buf) {
   if (buf.has_value() && buf->defined()) {
     TORCH_CHECK(buf->is_cuda() && buf->scalar_type() == at::kLong && buf->is_contiguous(), "ssd_stamps: int64 buffer");
-    mamba_amd::set_ssd_stamps(buf->data_ptr());
+    mamba_amd::set_ssd_stamps(buf->data_ptr(), buf->numel());
   } else {
-    mamba_amd::set_ssd_stamps(nullptr);
+    mamba_amd::set_ssd_stamps(nullptr, 0);
   }
 }
 

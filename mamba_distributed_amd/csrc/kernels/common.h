@@ -95,11 +95,17 @@ __device__ __forceinline__ float wave_sum(float v) {
   v += MAMBA_DPPF(v, 0x140);
   return wave_rows_combine_sum(v);
 }
+// Contract for wave_sum / wave_max: the whole wave is active (EXEC all ones; every call site is).  A DPP read from
+// an inactive source lane returns `old`: 0 for the sum (its identity); for the max `old` is the lane's own value, so
+// an inactive source can never win (a 0 would for all-negative rows).  v_permlane{32,16}_swap: gfx950 only.
+#define MAMBA_DPPF_SELF(v, ctrl)                                                                              \
+  __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, (v)), __builtin_bit_cast(int, (v)), \
+                                                        (ctrl), 0xF, 0xF, false))
 __device__ __forceinline__ float wave_max(float v) {
-  v = fmaxf(v, MAMBA_DPPF(v, 0xB1));
-  v = fmaxf(v, MAMBA_DPPF(v, 0x4E));
-  v = fmaxf(v, MAMBA_DPPF(v, 0x141));
-  v = fmaxf(v, MAMBA_DPPF(v, 0x140));
+  v = fmaxf(v, MAMBA_DPPF_SELF(v, 0xB1));
+  v = fmaxf(v, MAMBA_DPPF_SELF(v, 0x4E));
+  v = fmaxf(v, MAMBA_DPPF_SELF(v, 0x141));
+  v = fmaxf(v, MAMBA_DPPF_SELF(v, 0x140));
   return wave_rows_combine_max(v);
 }
 

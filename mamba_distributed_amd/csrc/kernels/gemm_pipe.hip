@@ -698,8 +698,10 @@ bool gemm_pk_supported(int la, int lb, int epi, int M, int N, int K, int64_t lda
 // HIP graph take pairs from a separate, never-recycled range (a replayed graph keeps its baked pair, which an
 // eager launch must never reuse).  The buffer is allocated on the device's first eager launch; a first launch
 // inside stream capture fails loudly (run one eager launch, e.g. the warm-up step, before capturing).
+constexpr int PK_RING = 16384, PK_CAPTURED = 8192;  // eager ring, graph-captured range (pairs)
+int gemm_pk_graph_counter_capacity() { return PK_CAPTURED; }
 static int* pk_counters(int dev, hipStream_t st) {
-  constexpr int R = 16384, RC = 8192;  // eager ring, graph-captured range
+  constexpr int R = PK_RING, RC = PK_CAPTURED;
   static int* bufs[16] = {};
   static unsigned seq[16] = {};
   static unsigned cap[16] = {};

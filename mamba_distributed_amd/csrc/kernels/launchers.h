@@ -123,6 +123,9 @@ hipError_t launch_gemm_pipe(int la, int lb, const void* A, int64_t lda, const vo
 bool gemm_pk_supported(int la, int lb, int epi, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc);
 hipError_t launch_gemm_pk(int la, int lb, const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
                           int64_t ldc, int M, int N, int K, int epi, const float* rowscale, hipStream_t st);
+// launches that may ever be captured into HIP graphs per process (their counter pairs are never recycled; a
+// launch past it returns hipErrorNotReady)
+int gemm_pk_graph_counter_capacity();
 // the split-K engine's workgroup shape: 8 waves (128 x 64 per wave) or 4 waves (128 x 128 per wave)
 int gemm_pipe_waves();
 void set_gemm_pipe_waves(int w);

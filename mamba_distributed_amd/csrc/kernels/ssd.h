@@ -61,7 +61,7 @@ hipError_t launch_ssd_fwd_f32(const SSDF32Args& a, hipStream_t st);
 hipError_t launch_ssd_fwd(const SSDArgs& a, hipStream_t st);
 // diagnostic: non-null = the next forward / chunk-backward launches record per-phase s_memtime sums (8 x u64 per
 // workgroup: the forward's H*B rows, then the chunk backward's nc*nhg*B rows); N = 128 only
-void set_ssd_stamps(void* p);
+void set_ssd_stamps(void* p, int64_t n);  // n: capacity in u64 (stamped launches that need more run unstamped)
 hipError_t launch_ssd_bwd(const SSDArgs& a, hipStream_t st);
 
 }  // namespace mamba_amd

@@ -55,9 +55,11 @@ __device__ __forceinline__ void st_any(void* p, int dt, int64_t i, float v) {
 // accumulates s_memtime deltas per phase of its
 // loop and writes them (vector stores) to a host-provided buffer; the STAMPS = false kernels compile it away.
 static unsigned long long* g_ssd_stamps = nullptr;  // host: (blocks, 8) u64 per stamped kernel, or null
+static int64_t g_ssd_stamps_n = 0;                   // its capacity in u64; a launch that needs more runs unstamped
 static int g_ssd_stamp_wave = 0;                     // the stamped wave (MAMBA_AMD_SSD_STAMP_WAVE, default 0)
-void set_ssd_stamps(void* p) {
+void set_ssd_stamps(void* p, int64_t n) {
   g_ssd_stamps = reinterpret_cast<unsigned long long*>(p);
+  g_ssd_stamps_n = p ? n : 0;
   const char* e = getenv("MAMBA_AMD_SSD_STAMP_WAVE");
   g_ssd_stamp_wave = e ? atoi(e) : 0;
 }
@@ -1003,7 +1005,7 @@ hipError_t launch_ssd_fwd_f32(const SSDF32Args& a, hipStream_t st) {
 hipError_t launch_ssd_fwd(const SSDArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(ssd_cumsum_k, dim3((unsigned)((int64_t)a.B * a.nc)), dim3(256), 0, st, a);
   MAMBA_HIP_CHECK(hipGetLastError());
-  if (g_ssd_stamps && a.N == 128) {
+  if (g_ssd_stamps && a.N == 128 && (int64_t)a.H * a.B * 8 <= g_ssd_stamps_n) {
     hipLaunchKernelGGL((ssd_fused_fwd_k<128, true>), dim3(a.H, a.B), dim3(256), 0, st, a, g_ssd_stamps,
                        g_ssd_stamp_wave & 3);
     return hipGetLastError();
@@ -1016,8 +1018,8 @@ hipError_t launch_ssd_bwd(const SSDArgs& a, hipStream_t st) {
   N_SWITCH(a.N, hipLaunchKernelGGL(ssd_dstate_bwd_k<NN>, dim3(a.H, a.B), dim3(256), 0, st, a));
   MAMBA_HIP_CHECK(hipGetLastError());
   if (a.fuse_dbc && a.HG != a.H / a.G) return hipErrorInvalidValue;  // the fused finish needs the whole group
-  if (g_ssd_stamps && a.N == 128) {
-    // the stamp buffer holds the forward's (H * B) rows first, then the chunk backward's
+  if (g_ssd_stamps && a.N == 128 && ((int64_t)a.H * a.B + (int64_t)a.nc * a.nhg * a.B) * 8 <= g_ssd_stamps_n) {
+    // the stamp buffer holds the forward's (H * B) rows first, then the chunk backward's (nc * nhg * B)
     hipLaunchKernelGGL((ssd_chunk_bwd_k<128, true>), dim3(a.nc, a.nhg, a.B), dim3(512), 0, st, a,
                        g_ssd_stamps + (int64_t)a.H * a.B * 8, g_ssd_stamp_wave & 7);
   } else {

@@ -5,7 +5,8 @@ so checkpoints are interchangeable with the reference.
 
 Layout choice (MI355X-first, not upstream's): the whole inner path runs channel-major with the
 batch folded inside, i.e. tensors of logical shape (b, d, l) live in memory as (d, b, l).  Every
-projection is then ONE plain 2-D GEMM on hipBLASLt —
+projection is then ONE plain 2-D GEMM on the native engines (csrc/kernels/gemm_pipe.hip persistent /
+split-K, gemm.hip skinny; hipBLASLt only under the MAMBA_AMD_PROJ_GEMM=lib A/B switch) —
   xz    = W_in  @ h^T           (2di, b*l)
   x_dbl = W_x   @ conv_out      (R+2N, b*l)
   delta = W_dt  @ x_dbl[:R]     (di, b*l)
@@ -45,8 +46,8 @@ def _mm_cm(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,
     the native streaming kernel (csrc/kernels/gemm.hip::gemm_skinny_k) for wide short-K products when
     the layout allows it, torch.mm otherwise.  Used for x_proj / dt_proj and their input gradients."""
     M = B.shape[1]
-    # native only for the wide, short-K products (delta = W_dt x_dbl[:R], dconv += W_x^T dx_dbl):
-    # for the long-K ones (x_dbl, dx_dbl[:R]) hipBLASLt measured faster (scripts/m1_gemms.py)
+    # the streaming kernel only for the wide, short-K products (delta = W_dt x_dbl[:R], dconv += W_x^T dx_dbl);
+    # the narrow long-K ones (x_dbl, dx_dbl[:R]) take the split-K engine's 128-row tile form below
     ok = (A.shape[0] >= 256 and A.shape[1] <= 128 and A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16 and A.is_cuda and B.stride(1) == 1
           and A.shape[1] % 8 == 0 and M % 8 == 0 and B.stride(0) % 8 == 0 and B.data_ptr() % 16 == 0
           and (out is None or (out.stride(1) == 1 and out.stride(0) % 8 == 0 and out.data_ptr() % 16 == 0)))
@@ -138,7 +139,13 @@ def _gp_xc_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
     return (a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.dim() == 2 and b.dim() == 2
             and a.stride(1) == 1 and b.stride(1) == 1 and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0
             and a.shape[1] % 8 == 0 and b.shape[1] % 8 == 0 and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0
-            and a.shape[1] >= 4096 and _ext.use_native(a))
+            and a.shape[1] >= 4096 and _pk_wins_xc(a.shape[1], b.shape[1], a.shape[0]) and _ext.use_native(a))
+
+
+def _pk_wins_xc(m: int, n: int, k: int) -> bool:
+    """The projection-engine switch (MAMBA_AMD_PROJ_GEMM, ops/linear.py::_pk_wins) for the XC . XC input gradient."""
+    from ..ops.linear import _pk_wins
+    return _pk_wins(m, n, k, "dgrad")
 
 
 def _wgrad_native(p, dY, X, dy_cm, x_cm):

@@ -4,10 +4,10 @@ Parameter names, shapes and init follow upstream ``mamba_ssm/modules/mamba2.py::
  so checkpoints interchange.  Training forward:
 
     zxbcdt = in_proj(u)                      native persistent GEMM fwd into 64-aligned padded rows,
-                                             hipBLASLt dgrad (K = padded width), native split-K wgrad
+                                             native persistent dgrad (K = padded width), native split-K wgrad
     y      = mamba2_inner_fn(zxbcdt, ...)    HIP: conv1d(xBC)+SiLU -> SSD -> gated RMSNorm
-    out    = out_proj(y)                     hipBLASLt fwd, native persistent dgrad, native wgrad
-(projection routing: ops/linear.py, MAMBA_AMD_PROJ_GEMM)
+    out    = out_proj(y)                     native persistent fwd and dgrad, native split-K wgrad
+(projection routing: ops/linear.py; hipBLASLt only under the MAMBA_AMD_PROJ_GEMM=lib A/B switch)
 
 The conv, SSD and norm kernels read their operands straight out of the strided zxbcdt buffer
 and the backward writes d(zxbcdt) as one buffer in the same padded layout (ops/ssd.py).

@@ -57,11 +57,11 @@ class _FusedLinearCEFn(torch.autograd.Function):
 
     The tokens are processed in row chunks (``_row_chunk``: <= 16384 rows, i.e. a 1.65 GB bf16 logits tile at
     V = 50304).  Per chunk:
-      logits_c = h_c W^T                         hipBLASLt (tuned table)           | native: gp_pk
+      logits_c = h_c W^T                         native persistent GEMM (gp_pk)
       loss_c, dlogits_c (in place, / n_valid)    ce_fwd (one read of the tile)
-      dh_c     = dlogits_c W                     hipBLASLt                         | native: gp_pk against W^T
-      dW      += dlogits_c^T h_c                 hipBLASLt, fp32 output + accumulate | native: gp_mm, fp32 K-split
-                                                                                      slabs summed once per node
+      dh_c     = dlogits_c W                     gp_pk against W^T (cached once per optimizer step)
+      dW      += dlogits_c^T h_c                 split-K engine (gp_mm), fp32 K-split slabs summed once per node
+    (MAMBA_AMD_LMHEAD=lib puts all three products on hipBLASLt, fp32 output + accumulate for dW: A/B only)
     so the (B*T, V) logits never exist whole (6.6 GB at 64 x 1024 tokens) and nothing of the lm_head is kept
     for the backward but dh and dW, which the backward scales by d(loss).  Engines (MAMBA_AMD_LMHEAD=native|lib):
     native by default (round 3 measured the whole node at 64k tokens 19.0 ms all native vs 17.0 on hipBLASLt,

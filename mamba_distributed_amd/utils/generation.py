@@ -110,6 +110,9 @@ def decode(input_ids: torch.Tensor, model, max_length: int, top_k: int = 1, top_
     ent = cache.get(key)
     if ent is None or ent[0] != sig:
         cache.pop(key, None)  # parameters moved or changed dtype: the captured graph reads stale addresses
+        # NB every rebuild re-captures the decode graph, and each persistent-GEMM launch captured into a graph
+        # holds one of a fixed number of tile-claim counter pairs for the life of the process
+        # (gemm_pipe.hip PK_CAPTURED = 8192; the capture fails with a clear error once they are spent)
         dec = GraphedDecoder(model, batch_size=b, max_seqlen=max_length, use_graph=None if cg else False)
         cache[key] = (sig, dec)
     else:

@@ -59,25 +59,29 @@ def main():
     print(f"unstamped: ssd_fwd {ms(fwd):.3f} ms, ssd_bwd {ms(bwd):.3f} ms", flush=True)
     nc = (L + 63) // 64
     n_f = H * B
-    n_b = nc * 1 * B  # one head group (HG = H) per workgroup at this shape
-    buf = torch.zeros((n_f + n_b) * 8, dtype=torch.int64, device=dev)
+    # the chunk backward writes nc * nhg * B rows; nhg (head groups, pick_hg / MAMBA_AMD_SSD_HG) is at most H, so
+    # size for that and read back the rows actually written (the kernels skip stamping when the buffer is short)
+    n_b = nc * H * B
+    buf = torch.full(((n_f + n_b) * 8,), -1, dtype=torch.int64, device=dev)
     ops.ssd_stamps(buf)
     t_f = ms(fwd, 1)
     t_b = ms(bwd, 1)
     ops.ssd_stamps(None)
     st = buf.view(-1, 8).double().cpu()
     f, b = st[:n_f], st[n_f:n_f + n_b]
+    b = b[b[:, 0] >= 0]  # the rows of the nc * nhg * B workgroups that ran
     print(f"stamped: ssd_fwd {t_f:.3f} ms, ssd_bwd {t_b:.3f} ms (s_memtime ticks)")
     ftot = f.sum(1).mean().item()
     print(f"forward walk: {ftot / nc:.0f} ticks per chunk per workgroup ({nc} chunks)")
     for k, name in enumerate(FWD):
         v = f[:, k].mean().item() / nc
         print(f"  F{k} {name:28s} {v:8.0f}  {100 * v * nc / ftot:5.1f}%")
+    hpw = H // max(1, b.shape[0] // (nc * B))  # heads per workgroup
     btot = b.sum(1).mean().item()
-    print(f"chunk backward: {btot / H:.0f} ticks per head per workgroup ({H} heads)")
+    print(f"chunk backward: {btot / hpw:.0f} ticks per head per workgroup ({hpw} heads)")
     for k, name in enumerate(BWD):
-        v = b[:, k].mean().item() / H
-        print(f"  B{k} {name:28s} {v:8.0f}  {100 * v * H / btot:5.1f}%")
+        v = b[:, k].mean().item() / hpw
+        print(f"  B{k} {name:28s} {v:8.0f}  {100 * v * hpw / btot:5.1f}%")
 
 
 if __name__ == "__main__":
