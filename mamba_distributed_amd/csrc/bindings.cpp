@@ -822,6 +822,25 @@ Tensor gemm_skinny(Tensor A, Tensor B, optional<Tensor> out, bool accumulate) {
 
 // dW (fp32, (P, Q)) = dY^T X for token-major bf16 dY (M, P), X (M, Q); out optional (accumulate=True
 // adds into it, e.g. an existing fp32 .grad)
+// C (+)= dY^T X on the staged-ring split-K engine (kernels/gemm_pipe.hip gemm_wg_k via launch_gemm_pipe): transient
+// fp32 slabs, then the fixed-order slab sum into C.  la / lb: 1 = the operand is token-major ((M, P) / (M, Q)),
+// 0 = channel-major ((P, M) / (Q, M)).  False when the engine does not take the layout (the caller falls back).
+static bool staged_wgrad(const Tensor& dY, int la, const Tensor& X, int lb, int64_t M, int64_t P, int64_t Q,
+                         Tensor& C, bool accumulate) {
+  if (mamba_amd::gemm_wg_nb() == 0) return false;
+  const int64_t lda = dY.size(0) == 1 ? dY.size(1) : dY.stride(0), ldb = X.size(0) == 1 ? X.size(1) : X.stride(0);
+  if (!mamba_amd::gemm_pipe_supported(la, lb, (int)P, (int)Q, (int)M, lda, ldb, Q)) return false;
+  const int S = mamba_amd::gemm_pipe_splits((int)P, (int)Q, (int)M);
+  auto part = at::empty({S, P, Q}, dY.options().dtype(at::kFloat));
+  const hipError_t e = mamba_amd::launch_gemm_pipe(la, lb, dY.data_ptr(), lda, X.data_ptr(), ldb, part.data_ptr(), Q,
+                                                   (int)P, (int)Q, (int)M, S, P * Q, 1, 256, cur_stream());
+  if (e == hipErrorInvalidValue) return false;
+  HIPCHK(e);
+  HIPCHK(mamba_amd::launch_gp_reduce(part.data_ptr<float>(), S, P * Q, P * Q, C.data_ptr<float>(), accumulate,
+                                     cur_stream()));
+  return true;
+}
+
 Tensor gemm_wgrad(Tensor dY, Tensor X, optional<Tensor> out, bool accumulate) {
   check_cuda(dY, "dY");
   at::hip::HIPGuardMasqueradingAsCUDA guard(dY.device());
@@ -834,6 +853,7 @@ Tensor gemm_wgrad(Tensor dY, Tensor X, optional<Tensor> out, bool accumulate) {
   TORCH_CHECK(C.scalar_type() == at::kFloat && C.is_contiguous() && C.size(0) == P && C.size(1) == Q,
               "gemm_wgrad: out must be contiguous fp32 (P,Q)");
   TORCH_CHECK(!accumulate || (out.has_value() && out->defined()), "gemm_wgrad: accumulate needs out");
+  if (staged_wgrad(dY, 1, X, 1, M, P, Q, C, accumulate)) return C;
   const int S = mamba_amd::gemm_wgrad_splits((int)M, (int)P, (int)Q);
   auto part = at::empty({S, P, Q}, dY.options().dtype(at::kFloat));
   HIPCHK(mamba_amd::launch_gemm_wgrad(dY.data_ptr(), dY.stride(0), X.data_ptr(), X.stride(0), part.data_ptr<float>(),
@@ -861,6 +881,7 @@ Tensor gemm_wgrad_cm(Tensor dY, Tensor X, optional<Tensor> out, bool accumulate,
   TORCH_CHECK(C.scalar_type() == at::kFloat && C.is_contiguous() && C.size(0) == P && C.size(1) == Q,
               "gemm_wgrad_cm: out must be contiguous fp32 (P,Q)");
   TORCH_CHECK(!accumulate || (out.has_value() && out->defined()), "gemm_wgrad_cm: accumulate needs out");
+  if (part_mode_ == 0 && staged_wgrad(dY, dy_cm ? 0 : 1, X, x_cm ? 0 : 1, M, P, Q, C, accumulate)) return C;
   const int S = mamba_amd::gemm_wgrad_splits((int)M, (int)P, (int)Q);
   // part_mode (ops/grad_accum.py::deferred): 0 transient slabs reduced now; 1 / 2 store / add into the
   // persistent slabs, no reduction (returns an empty tensor); 3 / 4 store / add, then reduce into C
@@ -979,6 +1000,12 @@ void ssd_stamps(optional<Tensor> buf) {
 int64_t gp_waves(int64_t w) {
   if (w > 0) mamba_amd::set_gemm_pipe_waves((int)w);
   return mamba_amd::gemm_pipe_waves();
+}
+
+// split-K XC . XC weight-gradient engine: LDS slots of gemm_wg_k (4 / 5) or 0 (gemm_pipe_k); nb < 0 only reads it
+int64_t gp_wg_nb(int64_t nb) {
+  if (nb >= 0) mamba_amd::set_gemm_wg_nb((int)nb);
+  return mamba_amd::gemm_wg_nb();
 }
 
 int64_t wgrad_splits(int64_t M, int64_t P, int64_t Q) { return mamba_amd::gemm_wgrad_splits((int)M, (int)P, (int)Q); }
@@ -1120,6 +1147,7 @@ TORCH_LIBRARY(mamba_amd, m) {
   m.def("gp_mm(Tensor A, Tensor B, Tensor(a!)? out=None, int la=0, int lb=0, int mode=0, int splits=1, int bm=256) -> Tensor");
   m.def("gp_pk(Tensor A, Tensor B, Tensor(a!)? out=None, int la=0, int lb=0, int mode=0, Tensor? rowscale=None) -> Tensor");
   m.def("gp_waves(int w=0) -> int", &gp_waves);
+  m.def("gp_wg_nb(int nb=-1) -> int", &gp_wg_nb);
   m.def("ssd_stamps(Tensor? buf) -> ()", &ssd_stamps);
   m.def("gp_splits(int M, int N, int K) -> int", &gp_splits);
   m.def("part_rows(str kind, int a, int b=0) -> int", &part_rows);

@@ -33,7 +33,9 @@
 //    share the A panel / the K slab in one XCD's L2.
 //  * K tails: chunks with k >= K are DMA'd from a 16-B zero page (per-lane source), rows / columns past
 //    M / N are clamped on load and never stored.
+#include <cstdint>
 #include <cstdlib>
+#include <type_traits>
 
 #include "mfma.h"
 #include "launchers.h"
@@ -42,6 +44,8 @@ namespace mamba_amd {
 namespace {
 
 typedef __attribute__((address_space(3))) void lds_void;
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int GP_NT = 512;   // threads per workgroup
 constexpr int GP_BK = 64;    // k per K-tile (one LDS buffer)
@@ -113,6 +117,7 @@ struct GemmPipeArgs {
   const bf16_t* B; int64_t ldb;
   void* C; int64_t ldc; int64_t split_stride;  // elements between the fp32 slabs of consecutive K splits
   int M, N, K, kslice, splits;
+  unsigned nbA, nbB;  // operand bytes covered by the buffer descriptors (gemm_wg_k)
 };
 
 // LA / LB: operand layouts (0 = KC, 1 = XC); MI: 16-row tiles per wave along M (BM = 32 MI); EPI: 0 = bf16
@@ -305,6 +310,248 @@ __global__ __launch_bounds__(128 * WN) void gemm_pipe_k(GemmPipeArgs a) {
     ktile(kt, smem, smem + SS, false, kt > 0 && kt + 1 < KT);
     if (kt + 1 < KT) ktile(kt + 1, smem + SS, smem, false, kt + 2 < KT);
   }
+
+  // epilogue: lane holds C[m][n .. n+3], m = m0 + am0 + 16 i + (l & 15), n = n0 + bn0 + 16 j + 4 (l >> 4)
+  const int mr = l & 15, nc = 4 * (l >> 4);
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int mm = am0 + 16 * i + mr;
+    if (mm >= mvalid) continue;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int nn = bn0 + 16 * j + nc;
+      if (nn >= nvalid) continue;
+      const int64_t off = (int64_t)(m0 + mm) * a.ldc + n0 + nn;
+      if constexpr (EPI == 0) {
+        bf16_t* c = reinterpret_cast<bf16_t*>(a.C) + off;
+        *reinterpret_cast<uint2*>(c) = make_uint2(pack2(acc[i][j][0], acc[i][j][1]), pack2(acc[i][j][2], acc[i][j][3]));
+      } else {
+        float* c = reinterpret_cast<float*>(a.C) + (int64_t)split * a.split_stride + off;
+        float4 v = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+        if constexpr (EPI == 2) {
+          const float4 o = *reinterpret_cast<const float4*>(c);
+          v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+        }
+        *reinterpret_cast<float4*>(c) = v;
+      }
+    }
+  }
+}
+
+// ---- staged-ring engine (gemm_wg_k): the split-K weight gradients and every other gp_mm product ----------------
+// dW = dY^T X reduces over tokens into a small output, so each workgroup runs ONE long K-loop (171 K-tiles of 64 at
+// the 280M in_proj shape) and the loop alone sets the speed.  gemm_pipe_k's 2-buffer ring gives every LDS-DMA one
+// 64-deep K-tile to land and drains it with vmcnt(0) at the barrier; worse, hipcc cannot tell its
+// global_load_lds writes from the LDS reads that follow (ds_read_b64_tr_b16 builtins) and waits vmcnt(0) right
+// after each DMA issue.  Here:
+//  * the K-loop advances in 32-deep STAGES through an NB-slot ring (NB x 32 KB at 256 x 256):
+//      stage s: read ahi(s) | MFMA alo(s) x b(s) | lgkmcnt(0); vmcnt(G (NB-2)) [stage s+1 landed]; s_barrier
+//               [slot s read by every wave] | DMA stage s+NB -> slot s, read alo(s+1), b(s+1) | MFMA ahi(s) x b(s)
+//    so a stage's DMA has NB-1 stages to land and no wait drains the ring (b alternates between two register sets
+//    by stage parity; the steady loop is unrolled to lcm(NB, 2) stages so every slot address is a constant);
+//  * operands are DMA'd with buffer_load ... lds through descriptors that cover exactly the operands' bytes (rows
+//    past M / N and k-rows past K read as zeros; KC k-chunks past K get an out-of-range offset), and every LDS
+//    fragment read is inline asm with explicit lgkmcnt waits, so hipcc inserts no DMA drain;
+//  * images: XC [32 k][128] halves (256-B rows, gemm_pipe_k's xc_swz swizzle, ds_read_b64_tr_b16 x 2 per
+//    fragment); KC [rows][32 k] (64-B rows, 16-B chunk c of row r at c ^ kc32_swz(r): every 16-lane group of a
+//    ds_read_b128 hits 16 distinct slots of a bank row).
+// Split-K slices sit on gemm_pipe_k's 64-token grid, and the k order (one MFMA per 32 tokens, in sequence) is the
+// same, so both engines write the same slabs bit for bit (MAMBA_AMD_WG_NB=0 routes gp_mm back to gemm_pipe_k).
+// 4 slots measured faster than 5 at every weight-gradient shape (profiles/r5/wg_engine_ab.txt).
+__device__ __forceinline__ int kc32_swz(int r) { return (0x1320 >> (4 * ((r >> 2) & 3))) & 3; }  // [0, 2, 3, 1]
+
+template <int LA, int LB, int EPI, int NB, int MI>
+__global__ __launch_bounds__(512) void gemm_wg_k(GemmPipeArgs a) {
+  constexpr int NT = 512, WN = 4, NJ = 4, MH = MI / 2;
+  constexpr int BM = 32 * MI, BN = 256, BK = 32;
+  constexpr int SA = BM * BK * 2, SB = BN * BK * 2, SS = SA + SB;  // bytes per operand image / slot
+  constexpr int GA = BM / 128, GB = BN / 128, G = GA + GB;          // DMA instructions per thread per stage
+  constexpr int RA = LA ? 2 : 1, RB = LB ? 2 : 1;                   // LDS read instructions per fragment
+  static_assert(NB >= 3 && NB * SS <= 163840, "LDS");
+  __shared__ __attribute__((aligned(1024))) char smem[NB * SS];
+
+  const int tn = (a.N + BN - 1) / BN, tm = (a.M + BM - 1) / BM;
+  const int nwg = tm * tn * a.splits;
+  const int t = xcd_remap(blockIdx.x, nwg);
+  const int split = t / (tm * tn), tile = t % (tm * tn);
+  const int m0 = (tile / tn) * BM, n0 = (tile % tn) * BN;
+  const int kbeg = split * a.kslice, kend = min(a.K, kbeg + a.kslice);
+  const int KT = (kend - kbeg + BK - 1) / BK;  // stages
+  const int KTF = (kend - kbeg) / BK;          // full stages
+  const int mvalid = min(BM, a.M - m0), nvalid = min(BN, a.N - n0);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, tid = threadIdx.x;
+  const int wr = w / WN, wc = w % WN;
+  const int am0 = wr * (BM / 2), bn0 = wc * (BN / WN);
+
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, (short)0, (int)a.nbA, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)a.B, (short)0, (int)a.nbB, 0x00020000);
+  // per-thread DMA byte offsets of stage 0 (32-bit, host-checked) and the per-stage step
+  // XC: instruction ii = half ii of [32 k][R]: k-row tid >> 4, chunk (tid & 15) swizzled on the source (rule 21)
+  // KC: instruction ii = rows 128 ii .. +127 of [R][32 k]: row (ii 512 + tid) >> 2, 16-B chunk (tid & 3) ^ kc32_swz
+  auto off0 = [&](int L, int ii, int base, int valid, int64_t ld) -> unsigned {
+    if (L == 1) {
+      const int kr = tid >> 4, sx = tid & 15;
+      return (unsigned)((((int64_t)kbeg + kr) * ld + base + min(ii * 128 + 8 * (sx ^ (2 * xc_swz(kr))), valid - 8)) * 2);
+    }
+    const int r = (ii * NT + tid) >> 2, c = (tid & 3) ^ kc32_swz(r);
+    return (unsigned)((((int64_t)base + r) * ld + kbeg + 8 * c) * 2);
+  };
+  unsigned offA[GA], offB[GB];
+#pragma unroll
+  for (int ii = 0; ii < GA; ++ii) offA[ii] = off0(LA, ii, m0, mvalid, a.lda);
+#pragma unroll
+  for (int ii = 0; ii < GB; ++ii) offB[ii] = off0(LB, ii, n0, nvalid, a.ldb);
+  const unsigned stepA = LA ? (unsigned)(BK * a.lda * 2) : BK * 2u, stepB = LB ? (unsigned)(BK * a.ldb * 2) : BK * 2u;
+  const int kchunk = 8 * ((tid & 3) ^ kc32_swz(tid >> 2));  // KC: this thread's k offset in a stage (all ii)
+  const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // DMA of stage s into slot buf; `chk`: KC k-chunks past kend get an out-of-range offset (zeros)
+  auto dma = [&](int s_, char* buf, bool chk) {
+    const unsigned s = (unsigned)__builtin_amdgcn_readfirstlane(s_);
+    const unsigned ua = __builtin_amdgcn_readfirstlane(s * stepA), ub = __builtin_amdgcn_readfirstlane(s * stepB);
+    const bool dead = chk && kbeg + (int)s * BK + kchunk >= kend;
+#pragma unroll
+    for (int ii = 0; ii < GA; ++ii) {
+      const unsigned v = (LA == 0 && dead) ? 0xFFFFFFF0u : offA[ii] + ua;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(buf + ii * 8192 + wu * 1024), 16, v, 0, 0, 0);
+    }
+#pragma unroll
+    for (int ii = 0; ii < GB; ++ii) {
+      const unsigned v = (LB == 0 && dead) ? 0xFFFFFFF0u : offB[ii] + ub;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(buf + SA + ii * 8192 + wu * 1024), 16, v, 0, 0, 0);
+    }
+  };
+
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = zero4();
+  bf16x8 alo[MH], ahi[MH], b0[NJ], b1[NJ];
+  // Fragment reads as INLINE ASM with explicit lgkmcnt waits (see above).  LDS byte addresses: XC one per
+  // 16-column block (its XOR swizzle is lane- and block-dependent), KC one per operand (row blocks are immediates);
+  // the slot base is added per stage.
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  const int lkc = (l & 15) * 64 + (((l >> 4) ^ kc32_swz(l & 15)) << 4);
+  constexpr int NOA = LA ? MI : 1, NOB = LB ? NJ : 1;
+  unsigned oa[NOA], ob[NOB];
+#pragma unroll
+  for (int i = 0; i < NOA; ++i)
+    oa[i] = LA ? lds0 + ((am0 + 16 * i) >> 7) * (32 * 256) + lane_xc(am0 + 16 * i) : lds0 + am0 * 64 + lkc;
+#pragma unroll
+  for (int j = 0; j < NOB; ++j)
+    ob[j] = LB ? lds0 + SA + ((bn0 + 16 * j) >> 7) * (32 * 256) + lane_xc(bn0 + 16 * j) : lds0 + SA + bn0 * 64 + lkc;
+  auto rd_xc = [&](bf16x8& d, unsigned addr) {
+    u32x2 x, y;
+    asm volatile("ds_read_b64_tr_b16 %0, %2\n\tds_read_b64_tr_b16 %1, %2 offset:1024" : "=&v"(x), "=&v"(y) : "v"(addr));
+    d = __builtin_bit_cast(bf16x8, __builtin_shufflevector(x, y, 0, 1, 2, 3));
+  };
+  auto rd_kc = [&](bf16x8& d, unsigned addr, auto off) {
+    u32x4 x;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(x) : "v"(addr), "n"(decltype(off)::value));
+    d = __builtin_bit_cast(bf16x8, x);
+  };
+  // fragment i of A (16 rows) / j of B (16 columns) from the slot at byte offset `so`
+  auto fa = [&](bf16x8& d, auto I, unsigned so) {
+    constexpr int i = decltype(I)::value;
+    if constexpr (LA) rd_xc(d, oa[i] + so);
+    else rd_kc(d, oa[0] + so, std::integral_constant<int, 1024 * i>{});
+  };
+  auto fb = [&](bf16x8& d, auto J, unsigned so) {
+    constexpr int j = decltype(J)::value;
+    if constexpr (LB) rd_xc(d, ob[j] + so);
+    else rd_kc(d, ob[0] + so, std::integral_constant<int, 1024 * j>{});
+  };
+  auto lgkm = [](auto n) {  // fenced on both sides: no MFMA may cross it either way
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(decltype(n)::value) : "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto mm_lo = [&](bf16x8 (&bf)[NJ]) {
+#pragma unroll
+    for (int i = 0; i < MH; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = mfma16(bf[j], alo[i], acc[i][j]);
+  };
+  // compile-time loops over fragment indices (the asm immediates and register arrays need constants)
+  auto rd_ahi = [&](unsigned so) {
+    [&]<int... I>(std::integer_sequence<int, I...>) {
+      (fa(ahi[I], std::integral_constant<int, MH + I>{}, so), ...);
+    }(std::make_integer_sequence<int, MH>{});
+  };
+  auto rd_lo = [&](unsigned so, bf16x8 (&bn)[NJ]) {
+    [&]<int... I>(std::integer_sequence<int, I...>) {
+      (fa(alo[I], std::integral_constant<int, I>{}, so), ...);
+    }(std::make_integer_sequence<int, MH>{});
+    [&]<int... J>(std::integer_sequence<int, J...>) {
+      (fb(bn[J], std::integral_constant<int, J>{}, so), ...);
+    }(std::make_integer_sequence<int, NJ>{});
+  };
+  // mm_hi (ahi x bc) with the next stage's alo / bn reads spread between its MFMAs: one fragment per MFMA
+  auto mm_hi_rd = [&](bf16x8 (&bc)[NJ], bf16x8 (&bn)[NJ], unsigned so, bool rd) {
+    [&]<int... Q>(std::integer_sequence<int, Q...>) {
+      ([&] {
+        constexpr int q = Q, i = q / NJ, j = q % NJ;
+        if (rd) {
+          if constexpr (q < MH) fa(alo[q], std::integral_constant<int, q>{}, so);
+          else if constexpr (q < MH + NJ) fb(bn[q - MH], std::integral_constant<int, q - MH>{}, so);
+        }
+        acc[MH + i][j] = mfma16(bc[j], ahi[i], acc[MH + i][j]);
+        __builtin_amdgcn_sched_barrier(0);
+      }(), ...);
+    }(std::make_integer_sequence<int, MH * NJ>{});
+  };
+  // stage s from slot offset `cur` (which then receives stage s+NB); slot `nxt` holds stage s+1.  `steady`:
+  // stages s+1 .. s+NB exist and are full (counted vmcnt wait, unchecked DMA).  Reads in flight on entry: alo / bc
+  // of stage s.
+  auto stage = [&](int s, unsigned cur, unsigned nxt, bf16x8 (&bc)[NJ], bf16x8 (&bn)[NJ], bool steady) {
+    rd_ahi(cur);
+    lgkm(std::integral_constant<int, MH * RA>{});  // alo / bc have landed (LDS returns in order)
+    mm_lo(bc);
+    lgkm(std::integral_constant<int, 0>{});  // ahi has landed: this wave is done reading slot s
+    const bool more = steady || s + 1 < KT;
+    if (more) {
+      if (steady) vm_wait<G * (NB - 2)>();  // stage s+1 has landed (NB-2 younger stages stay in flight)
+      else vm_wait<0>();
+      __builtin_amdgcn_s_barrier();  // ... for every wave; every wave is done reading slot s
+      __builtin_amdgcn_sched_barrier(0);
+      if (steady) dma(s + NB, smem + cur, false);
+      else if (s + NB < KT) dma(s + NB, smem + cur, s + NB >= KTF);
+    }
+    mm_hi_rd(bc, bn, nxt, more);
+  };
+
+  if (KT > 0) {
+#pragma unroll
+    for (int s = 0; s < NB; ++s)
+      if (s < KT) dma(s, smem + s * SS, s >= KTF);
+    if (KT >= NB) vm_wait<G * (NB - 1)>();  // stage 0 landed
+    else vm_wait<0>();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    rd_lo(0u, b0);
+  }
+  // steady loop: U = lcm(NB, 2) stages per iteration
+  constexpr int U = NB % 2 ? 2 * NB : NB;
+  int s = 0;
+#pragma unroll 1
+  for (; s + U + NB <= KTF; s += U) {  // stages s+1 .. s+U-1+NB exist and are full
+#pragma unroll
+    for (int u = 0; u < U; u += 2) {
+      stage(s + u, (u % NB) * SS, ((u + 1) % NB) * SS, b0, b1, true);
+      stage(s + u + 1, ((u + 1) % NB) * SS, ((u + 2) % NB) * SS, b1, b0, true);
+    }
+  }
+  // tail (a multiple of U stages done: stage s is in slot 0): every wait vmcnt(0)
+  unsigned o0 = 0, o1 = SS, o2 = 2 * SS;
+  auto adv = [](unsigned o) { return o + SS == NB * SS ? 0u : o + SS; };
+#pragma unroll 1
+  for (; s < KT; s += 2) {
+    stage(s, o0, o1, b0, b1, false);
+    if (s + 1 < KT) stage(s + 1, o1, o2, b1, b0, false);
+    o0 = o2; o1 = adv(o2); o2 = adv(o1);
+  }
+  vm_wait<0>();
+  lgkm(std::integral_constant<int, 0>{});
 
   // epilogue: lane holds C[m][n .. n+3], m = m0 + am0 + 16 i + (l & 15), n = n0 + bn0 + 16 j + 4 (l >> 4)
   const int mr = l & 15, nc = 4 * (l >> 4);
@@ -611,6 +858,19 @@ int gemm_pipe_waves() {
 }
 void set_gemm_pipe_waves(int w) { g_pipe_waves = (w == 4) ? 4 : 8; }
 
+// LDS slots of the split-K XC . XC weight-gradient engine (gemm_wg_k): 0 = route those products to gemm_pipe_k
+// instead; MAMBA_AMD_WG_NB sets the process default, set_gemm_wg_nb overrides it
+static int g_wg_nb = -1;
+int gemm_wg_nb() {
+  if (g_wg_nb < 0) {
+    const char* e = getenv("MAMBA_AMD_WG_NB");
+    const int v = e ? atoi(e) : 4;  // 4 slots measured fastest (profiles/r5/wg_engine_ab.txt)
+    g_wg_nb = (v == 4 || v == 5) ? v : 0;
+  }
+  return g_wg_nb;
+}
+void set_gemm_wg_nb(int nb) { g_wg_nb = (nb == 4 || nb == 5) ? nb : 0; }
+
 bool gemm_pipe_supported(int la, int lb, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc) {
   if (M <= 0 || N <= 0 || K <= 0) return false;
   if (lda % 8 || ldb % 8 || ldc % 4 || N % 4) return false;
@@ -630,6 +890,16 @@ int gemm_pipe_splits(int M, int N, int K) {
   return split_k_count(((int64_t)(M + 255) / 256) * ((N + 255) / 256), M, N, K, 8 * GP_BK);
 }
 
+// gemm_wg_k's 32-bit DMA byte offsets: XC up to one stage past K, KC up to one 256-row tile past the rows, and
+// below the out-of-range sentinel
+static bool gemm_wg_offsets_ok(int la, int lb, int M, int N, int K, int64_t lda, int64_t ldb) {
+  const int64_t lim = ((int64_t)1 << 32) - 64;
+  auto ok = [&](int L, int rows, int64_t ld) {
+    return (L ? ((int64_t)K + 64) * ld : ((int64_t)rows + 256) * ld + K + 64) * 2 < lim;
+  };
+  return ok(la, M, lda) && ok(lb, N, ldb);
+}
+
 hipError_t launch_gemm_pipe(int la, int lb, const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
                             int64_t ldc, int M, int N, int K, int splits, int64_t split_stride, int epi, int bm,
                             hipStream_t st) {
@@ -642,6 +912,26 @@ hipError_t launch_gemm_pipe(int la, int lb, const void* A, int64_t lda, const vo
   a.M = M; a.N = N; a.K = K; a.splits = splits;
   a.kslice = ((K + splits - 1) / splits + GP_BK - 1) / GP_BK * GP_BK;
   const int nwg = ((M + bm - 1) / bm) * ((N + 255) / 256) * splits;
+  if (gemm_wg_nb() != 0 && gemm_wg_offsets_ok(la, lb, M, N, K, lda, ldb)) {
+    // the staged-ring engine (32-deep stages, 4-slot ring); split slices on the 64-token grid
+    a.kslice = ((K + splits - 1) / splits + GP_BK - 1) / GP_BK * GP_BK;
+    a.nbA = (unsigned)((la ? (int64_t)(K - 1) * lda + M : (int64_t)(M - 1) * lda + K) * 2);
+    a.nbB = (unsigned)((lb ? (int64_t)(K - 1) * ldb + N : (int64_t)(N - 1) * ldb + K) * 2);
+    const int mi = bm == 128 ? 4 : 8;
+#define WG_L(LA_, LB_, E_, MI_) hipLaunchKernelGGL((gemm_wg_k<LA_, LB_, E_, 4, MI_>), dim3(nwg), dim3(512), 0, st, a)
+#define WG_E(LA_, LB_)                                          \
+  if (mi == 4) WG_L(LA_, LB_, 0, 4);                            \
+  else if (epi == 0) WG_L(LA_, LB_, 0, 8);                      \
+  else if (epi == 1) WG_L(LA_, LB_, 1, 8);                      \
+  else WG_L(LA_, LB_, 2, 8);
+    if (la == 0 && lb == 0) { WG_E(0, 0) }
+    else if (la == 0 && lb == 1) { WG_E(0, 1) }
+    else if (la == 1 && lb == 1) { WG_E(1, 1) }
+    else { WG_E(1, 0) }
+#undef WG_E
+#undef WG_L
+    return hipGetLastError();
+  }
   if (bm == 128) {
     if (la == 0) hipLaunchKernelGGL((gemm_pipe_k<0, 1, 0, 4, 4>), dim3(nwg), dim3(GP_NT), 0, st, a);
     else hipLaunchKernelGGL((gemm_pipe_k<1, 1, 0, 4, 4>), dim3(nwg), dim3(GP_NT), 0, st, a);

@@ -129,6 +129,9 @@ int gemm_pk_graph_counter_capacity();
 // the split-K engine's workgroup shape: 8 waves (128 x 64 per wave) or 4 waves (128 x 128 per wave)
 int gemm_pipe_waves();
 void set_gemm_pipe_waves(int w);
+// LDS slots (4 or 5) of the XC . XC fp32 weight-gradient engine gemm_wg_k, or 0: those products on gemm_pipe_k
+int gemm_wg_nb();
+void set_gemm_wg_nb(int nb);
 // out[i] (+)= sum_s part[s * stride + i], fixed order
 hipError_t launch_transpose_bf16(const void* x, int64_t ldx, void* y, int64_t ldy, int R, int C, hipStream_t st);
 hipError_t launch_gp_reduce(const float* part, int S, int64_t stride, int64_t n, float* out, bool accumulate,

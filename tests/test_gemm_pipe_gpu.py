@@ -227,3 +227,54 @@ def test_gp_narrow_128_row_tiles(cuda, la, M):
     assert _rel(C, ref) < 8e-3, _rel(C, ref)
     assert (out[M:] == 0).all()
     assert torch.equal(C, ops.gp_mm(A, B, None, la, 1, 0, 1, 256))  # same K order as the 256-row tiles
+
+
+# ---- split-K weight-gradient engine (gemm_wg_k: XC . XC, fp32 slabs, 32-deep stages in an NB-slot ring) -------
+@pytest.fixture
+def wg_engine():
+    ops = _ops()
+    old = ops.gp_wg_nb(-1)
+    yield ops
+    ops.gp_wg_nb(old)
+
+
+@pytest.mark.parametrize("nb", [4, 5])
+@pytest.mark.parametrize("M,N,T", [(264, 136, 318), (256, 256, 32), (520, 776, 4160), (3352, 768, 9000),
+                                   (8, 8, 1), (776, 1536, 65)])
+def test_gp_wg_engine(cuda, wg_engine, nb, M, N, T):
+    """Ragged rows / columns / token counts (stages past K read zeros through the buffer descriptor), every split
+    count the slab layout takes, fp32 store and += epilogues, bitwise determinism, and bitwise agreement with the
+    gemm_pipe_k engine it replaces (same k order: one MFMA per 32 tokens, in sequence)."""
+    ops = wg_engine
+    g = torch.Generator(device=cuda).manual_seed(M + N + T)
+    A, B = _mk(M, T, 1, cuda, g), _mk(N, T, 1, cuda, g)
+    ref = _ref(A, B, 1, 1)
+    for S in sorted({1, 2, 5, ops.gp_splits(M, N, T)}):
+        ops.gp_wg_nb(0)
+        base = ops.gp_mm(A, B, None, 1, 1, 1, S, 256)
+        ops.gp_wg_nb(nb)
+        assert ops.gp_wg_nb(-1) == nb
+        part = ops.gp_mm(A, B, None, 1, 1, 1, S, 256)
+        out = torch.zeros(M, N, device=cuda)
+        ops.gp_reduce(part, out, False)
+        assert _rel(out, ref) < 1e-5, (S, _rel(out, ref))
+        assert torch.equal(part, ops.gp_mm(A, B, None, 1, 1, 1, S, 256)), S
+        assert torch.equal(part, base), (S, (part - base).abs().max().item())
+        acc = torch.randn(S, M, N, device=cuda, generator=g)
+        acc0 = acc.clone()
+        ops.gp_mm(A, B, acc, 1, 1, 2, S, 256)
+        assert torch.equal(acc, acc0 + part), S
+
+
+def test_gp_wg_engine_default_path(cuda):
+    """The weight-gradient engine the process runs by default (MAMBA_AMD_WG_NB) on the headline in_proj shape."""
+    ops = _ops()
+    g = torch.Generator(device=cuda).manual_seed(9)
+    T, dp, d = 16384, 3392, 768
+    A = (torch.randn(T, dp, device=cuda, generator=g) * 0.5).to(torch.bfloat16)
+    B = (torch.randn(T, d, device=cuda, generator=g) * 0.5).to(torch.bfloat16)
+    S = ops.gp_splits(dp, d, T)
+    part = ops.gp_mm(A, B, None, 1, 1, 1, S, 256)
+    out = torch.zeros(dp, d, device=cuda)
+    ops.gp_reduce(part, out, False)
+    assert _rel(out, _ref(A, B, 1, 1)) < 1e-5
