@@ -912,7 +912,9 @@ hipError_t launch_gemm_pipe(int la, int lb, const void* A, int64_t lda, const vo
   a.M = M; a.N = N; a.K = K; a.splits = splits;
   a.kslice = ((K + splits - 1) / splits + GP_BK - 1) / GP_BK * GP_BK;
   const int nwg = ((M + bm - 1) / bm) * ((N + 255) / 256) * splits;
-  if (gemm_wg_nb() != 0 && gemm_wg_offsets_ok(la, lb, M, N, K, lda, ldb)) {
+  // every layout with an XC operand or an fp32 output: the ring measured faster on each of them
+  // (wg_engine_ab.txt, wg_engine_m1.txt); KC . KC bf16 stays here (pk_ring_rejected.txt)
+  if (gemm_wg_nb() != 0 && !(la == 0 && lb == 0 && epi == 0) && gemm_wg_offsets_ok(la, lb, M, N, K, lda, ldb)) {
     // the staged-ring engine (32-deep stages, 4-slot ring); split slices on the 64-token grid
     a.kslice = ((K + splits - 1) / splits + GP_BK - 1) / GP_BK * GP_BK;
     a.nbA = (unsigned)((la ? (int64_t)(K - 1) * lda + M : (int64_t)(M - 1) * lda + K) * 2);
@@ -1046,7 +1048,7 @@ hipError_t launch_gemm_pk(int la, int lb, const void* A, int64_t lda, const void
   const bool tail = K % 64 != 0 || a.kte * 64 != K;
   const int nwg = std::min(a.ntiles, ncu);
 #define PK_L(MI_, NJ_, RS_)                                                                              \
-  if (tail) hipLaunchKernelGGL((gemm_pk_k<MI_, NJ_, RS_, true>), dim3(nwg), dim3(512), 0, st, a);          \
+  if (tail) hipLaunchKernelGGL((gemm_pk_k<MI_, NJ_, RS_, true>), dim3(nwg), dim3(512), 0, st, a);     \
   else hipLaunchKernelGGL((gemm_pk_k<MI_, NJ_, RS_, false>), dim3(nwg), dim3(512), 0, st, a)
   if (bn == 192) {
     if (rowscale) { PK_L(8, 3, true); } else { PK_L(8, 3, false); }

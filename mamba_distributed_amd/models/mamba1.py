@@ -173,8 +173,7 @@ def _wgrad_native(p, dY, X, dy_cm, x_cm):
             side.wait_stream(torch.cuda.current_stream(dY.device))
             with torch.cuda.stream(side):
                 _ext.ops().gemm_wgrad_cm(dY, X, p.grad, True, dy_cm, x_cm)
-            dY.record_stream(side)
-            X.record_stream(side)
+            grad_accum.side_keep(dY.device, dY, X)
         return True, None
     return True, grad_accum.defer(p, _ext.ops().gemm_wgrad_cm(dY, X, None, False, dy_cm, x_cm).to(p.dtype))
 

@@ -104,7 +104,49 @@ def join_side() -> None:
         return
     for idx in list(_side_dirty):
         torch.cuda.current_stream(idx).wait_stream(_side[idx])
+        _kept.pop(idx, None)  # every kept operand's side-stream use is now ordered before the main stream
     _side_dirty.clear()
+
+
+_kept = {}     # device index -> deque of (side-stream event, operands kept alive for it)
+_KEEP_BATCH = 8
+
+
+def _keep_lag() -> int:
+    """Side-stream launches whose operands stay referenced (MAMBA_AMD_SIDE_LAG; < 0: record_stream instead)."""
+    import os
+    return int(os.environ.get("MAMBA_AMD_SIDE_LAG", "16"))
+
+
+def side_keep(device: torch.device, *tensors) -> None:
+    """Keep the main-stream operands of the side-stream work just queued alive, stream-ordered, instead of
+    ``record_stream``.  record_stream defers every reuse of the block to a HOST-side event query, and the host runs
+    a whole micro-batch ahead, so each backward's freed activations stayed unusable while the next forward
+    allocated fresh ones: 239 GB reserved for 124 GB allocated at the Mamba-2 280M bench shape.  Here the side
+    stream records an event after the work; once more than MAMBA_AMD_SIDE_LAG (16) launches are queued, the main stream waits for
+    the oldest one's event (a GPU-side wait that is normally long satisfied) and its references are dropped, so any
+    later main-stream reuse of that memory is ordered after the side-stream reads."""
+    from collections import deque
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    side = _side[idx]
+    lag = _keep_lag()
+    if lag < 0:  # the old form (A/B): the allocator defers each block's reuse to a host-side event query
+        for t in tensors:
+            t.record_stream(side)
+        return
+    ev = torch.cuda.Event()
+    ev.record(side)
+    q = _kept.get(idx)
+    if q is None:
+        q = _kept[idx] = deque()
+    q.append((ev, tensors))
+    if len(q) > lag + _KEEP_BATCH:
+        # release the oldest _KEEP_BATCH entries behind ONE main-stream wait (on the newest of them: the side stream
+        # runs in order, so it covers the older ones): a wait per launch cost ~0.5 % of the step
+        last = None
+        for _ in range(_KEEP_BATCH):
+            last, _t = q.popleft()
+        torch.cuda.current_stream(idx).wait_event(last)
 
 
 def deferred(param, tag: str, shape, device, force: bool = False):

@@ -55,8 +55,7 @@ def _wgrad_native(p, dy2: torch.Tensor, x2: torch.Tensor, lb: int = 1):
             side.wait_stream(torch.cuda.current_stream(dy2.device))
             with torch.cuda.stream(side):
                 ops.gemm_wgrad(dy2, x2, p.grad, True)
-            dy2.record_stream(side)
-            x2.record_stream(side)
+            grad_accum.side_keep(dy2.device, dy2, x2)
         return None
     if d is None:  # outside an accumulation scope / sync micro-step: transient slabs, reduce now
         part = ops.gp_mm(dy2, x2, None, 1, lb, 1, S, 256)
@@ -75,8 +74,7 @@ def _wgrad_native(p, dy2: torch.Tensor, x2: torch.Tensor, lb: int = 1):
             side.wait_stream(torch.cuda.current_stream(dy2.device))
             with torch.cuda.stream(side):
                 ops.gp_mm(dy2, x2, buf, 1, lb, slab_mode, S, 256)
-            dy2.record_stream(side)
-            x2.record_stream(side)
+            grad_accum.side_keep(dy2.device, dy2, x2)
         return None
     ops.gp_mm(dy2, x2, buf, 1, lb, slab_mode, S, 256)
     dw = torch.empty(P, Q, device=dy2.device, dtype=torch.float32)
@@ -92,9 +90,10 @@ def _wgrad_inplace(dev) -> bool:
     transient fp32 slabs on the persistent engine, reduced on the main stream. MAMBA_AMD_WGRAD_INPLACE=1/0 forces
     either; auto takes the side stream while the allocated peak stays under 70% of the device, the reserved peak
     under 96%, and the caching allocator has never had to retry (re-checked every 64 calls: memory_stats() is not free). The side-stream form
-    keeps dy/x alive (record_stream) past the main stream's frees; near capacity that turns into allocator
-    retries, which synchronise the device: Mamba-2 2.8B @ 8192 (222 GiB peak) ran 29.6k tok/s with it (17
-    retries) vs 46.8k without, while 1.4B @ 1024 (130 GiB) gains ~8% from it (profiles/r3/ab15_*)."""
+    keeps dy/x alive past the main stream's frees (grad_accum.side_keep: a few launches, stream-ordered; with
+    record_stream it was a whole micro-batch, and near capacity that turned into allocator retries, which
+    synchronise the device: Mamba-2 2.8B @ 8192 (222 GiB peak) ran 29.6k tok/s with it (17 retries) vs 46.8k
+    without, while 1.4B @ 1024 (130 GiB) gains ~8% from it, profiles/r3/ab15_*)."""
     import os
     env = os.environ.get("MAMBA_AMD_WGRAD_INPLACE", "auto")
     if env in ("0", "1"):

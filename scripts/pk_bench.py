@@ -80,8 +80,11 @@ def main():
             for _ in range(a.rounds):
                 t["pk"].append(timeit(lambda: ops.gp_pk(A, B), a.reps))
                 t["lib"].append(timeit(lambda: torch.nn.functional.linear(A, B), a.reps))
-                if name in ("in_fwd", "out_fwd"):
-                    t["gp_mm"].append(timeit(lambda: ops.gp_mm(A, B, None, 0, 0, 0, 1, 256), a.reps))
+                # the non-persistent engines: the staged ring (gemm_wg_k, default) and gemm_pipe_k (nb 0)
+                t["gp_mm"].append(timeit(lambda: ops.gp_mm(A, B, None, 0, 0, 0, 1, 256), a.reps))
+                ops.gp_wg_nb(0)
+                t.setdefault("gp_pipe", []).append(timeit(lambda: ops.gp_mm(A, B, None, 0, 0, 0, 1, 256), a.reps))
+                ops.gp_wg_nb(4)
             for k, v in t.items():
                 if v:
                     res[k + "_us"] = round(min(v), 1)

@@ -36,16 +36,65 @@ def timeit(fn, reps):
     return s.elapsed_time(e) / reps * 1e3
 
 
+def m1_cases(T=65536, d=768, di=1536, R=48, N=16):
+    """The gp_mm products of one Mamba-1 280M layer (models/mamba1.py, ops/linear.py), as (name, A, B, la, lb, mode,
+    splits, bm, flop).  Channel-major activations are (features, tokens)."""
+    g = torch.Generator(device="cuda").manual_seed(1)
+    rnd = lambda *s: (torch.randn(*s, device="cuda", generator=g) * 0.5).to(torch.bfloat16)  # noqa: E731
+    dxz, w_in, h2 = rnd(2 * di, T), rnd(2 * di, d), rnd(T, d)
+    wx, co2, wdt, dd2 = rnd(R + 2 * N, di), rnd(di, T), rnd(di, R), rnd(di, T)
+    y2, w_out, dout = rnd(di, T), rnd(d, di), rnd(T, d)
+    dxdbl = rnd(R + 2 * N, T)
+    return [
+        ("m1_in_dgrad XC.XC bf16", dxz, w_in, 1, 1, 0, 1, 256, 2.0 * T * d * 2 * di),
+        ("m1_x_proj KC.XC 128-row", wx, co2, 0, 1, 0, 1, 128, 2.0 * T * di * (R + 2 * N)),
+        ("m1_dxdbl XC.XC 128-row", wdt, dd2, 1, 1, 0, 1, 128, 2.0 * T * di * R),
+        ("m1_out_fwd XC.KC bf16", y2, w_out, 1, 0, 0, 1, 256, 2.0 * T * di * d),
+        ("m1_out_wgrad XC.KC slabs", dout, y2, 1, 0, 1, 0, 256, 2.0 * T * di * d),
+        ("m1_in_wgrad KC.XC slabs", dxz, h2, 0, 1, 1, 0, 256, 2.0 * T * d * 2 * di),
+        ("m1_x_wgrad KC.KC slabs", dxdbl, co2, 0, 0, 1, 0, 256, 2.0 * T * di * (R + 2 * N)),
+    ]
+
+
+def run_m1(a, ops, nbs):
+    for name, A, B, la, lb, mode, S, bm, fl in m1_cases():
+        M = A.shape[0] if la == 0 else A.shape[1]
+        N = B.shape[0] if lb == 0 else B.shape[1]
+        K = A.shape[1] if la == 0 else A.shape[0]
+        if S == 0:
+            S = ops.gp_splits(M, N, K)
+        out = torch.empty(S, M, N, device="cuda") if mode else torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        res = {nb: [] for nb in nbs}
+        outs = {}
+        for _ in range(a.rounds):
+            for nb in nbs:
+                ops.gp_wg_nb(nb)
+                res[nb].append(timeit(lambda: ops.gp_mm(A, B, out, la, lb, mode, S, bm), a.reps))
+                outs[nb] = out.clone()
+        ops.gp_wg_nb(4)
+        r = {"case": name, "M": M, "N": N, "K": K, "splits": S}
+        for nb in nbs:
+            t = min(res[nb])
+            r[f"nb{nb}_us"] = round(t, 1)
+            r[f"nb{nb}_tflops"] = round(fl / t / 1e6, 1)
+            r[f"nb{nb}_equal_nb{nbs[0]}"] = bool(torch.equal(outs[nb], outs[nbs[0]]))
+        print(json.dumps(r), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--only", default="")
-    ap.add_argument("--nb", default="0,4,5")
+    ap.add_argument("--nb", default="0,4")
+    ap.add_argument("--m1", action="store_true", help="the Mamba-1 layer's gp_mm products instead")
     a = ap.parse_args()
     assert _ext.load(), _ext.error()
     ops = _ext.ops()
     nbs = [int(v) for v in a.nb.split(",")]
+    if a.m1:
+        run_m1(a, ops, nbs)
+        return
     g = torch.Generator(device="cuda").manual_seed(0)
     for name, (P, Q, T) in SHAPES.items():
         if a.only and name not in a.only.split(","):
@@ -61,7 +110,7 @@ def main():
                 ops.gp_wg_nb(nb)
                 res[nb].append(timeit(lambda: ops.gp_mm(dY, X, part, 1, 1, 1, S, 256), a.reps))
                 outs[nb] = part.clone()
-        ops.gp_wg_nb(0)
+        ops.gp_wg_nb(4)
         fl = 2.0 * P * Q * T
         out = {"shape": name, "P": P, "Q": Q, "T": T, "splits": S}
         for nb in nbs:
