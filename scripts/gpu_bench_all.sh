@@ -7,6 +7,6 @@ for c in mamba2-280m:auto:1024 mamba1-280m:auto:1024 mamba1-370m:auto:1024 mamba
   IFS=: read -r m B T <<< "$c"
   echo "== $m B=$B T=$T"
   timeout -k 10 600 python bench.py --model $m --B $B --T $T --steps ${STEPS:-3} --warmup 1 > gpurun_out/bench_$m.log 2>&1; rc=$?
-  grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*\|"micro_batch": [0-9]*\|"peak_mem_gb": [0-9.]*' gpurun_out/bench_$m.log | tr '\n' ' '; echo
+  grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*\|"micro_batch": [0-9]*\|"peak_mem_gb": [0-9.]*\|"peak_reserved_gb": [0-9.]*' gpurun_out/bench_$m.log | tr '\n' ' '; echo
   [ $rc -eq 0 ] || { tail -5 gpurun_out/bench_$m.log; exit $rc; }
 done
