@@ -164,8 +164,7 @@ def main():
             loss_acc = run_micro_batches(dmodel, loader.next_batch, accum, compute_loss,
                                          overlap=overlap)
         all_reduce_avg(loss_acc)
-        norm = ddp_mod.clip_grad_norm_(dmodel, 1.0)
-        opt.step()
+        norm = ddp_mod.clip_and_step(dmodel, opt, 1.0)
         if a.trace_loss and info.master:
             print(f"step loss {loss_acc.item():.5f} grad_norm {norm.item():.4f}", flush=True)
         return loss_acc

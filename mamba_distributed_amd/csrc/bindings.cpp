@@ -1012,6 +1012,49 @@ int64_t wgrad_splits(int64_t M, int64_t P, int64_t Q) { return mamba_amd::gemm_w
 int64_t gp_splits(int64_t M, int64_t N, int64_t K) { return mamba_amd::gemm_pipe_splits((int)M, (int)N, (int)K); }
 
 
+// column sums of a (rows, cols) fp32 partial block, as the backward ops reduce their per-workgroup partial rows
+// (clobbers part); exposed for the numerics / determinism tests of launch_colsum
+Tensor colsum(Tensor part) {
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.dim() == 2 && part.is_contiguous(),
+              "colsum: contiguous 2-D fp32 CUDA tensor");
+  auto out = at::empty({part.size(1)}, part.options());
+  HIPCHK(mamba_amd::launch_colsum(part.data_ptr<float>(), (int)part.size(0), (int)part.size(1), out.data_ptr<float>(),
+                                  cur_stream()));
+  return out;
+}
+
+// ---- native optimizer step (ops/optim.py): tab = uint8 OptSeg table, blk = int64 (nblk, 2) chunk table ----
+static void check_opt_tables(const Tensor& tab, const Tensor& blk) {
+  TORCH_CHECK(tab.is_cuda() && tab.scalar_type() == at::kByte && tab.is_contiguous() && tab.numel() % 64 == 0,
+              "optimizer segment table: contiguous uint8 CUDA tensor of 64-byte rows");
+  TORCH_CHECK(blk.is_cuda() && blk.scalar_type() == at::kLong && blk.is_contiguous() && blk.dim() == 2 &&
+              blk.size(1) == 2 && blk.size(0) > 0, "optimizer block table: (nblk, 2) int64 CUDA tensor");
+}
+
+// [|| g / divisor ||_2, clip coefficient / divisor] as a 2-element fp32 tensor (max_norm <= 0: coefficient 1)
+Tensor opt_grad_norm(Tensor tab, Tensor blk, double max_norm, double divisor) {
+  check_opt_tables(tab, blk);
+  const int nblk = (int)blk.size(0);
+  auto partial = at::empty({nblk}, blk.options().dtype(at::kFloat));
+  auto out = at::empty({2}, blk.options().dtype(at::kFloat));
+  HIPCHK(mamba_amd::launch_grad_norm(tab.data_ptr(), blk.data_ptr<int64_t>(), nblk, partial.data_ptr<float>(),
+                                     (float)max_norm, (float)divisor, out.data_ptr<float>(), cur_stream()));
+  return out;
+}
+
+void opt_adamw(Tensor tab, Tensor blk, c10::optional<Tensor> gscale, double b1, double b2, double eps) {
+  check_opt_tables(tab, blk);
+  const float* gs = nullptr;
+  if (gscale.has_value() && gscale->defined()) {
+    TORCH_CHECK(gscale->is_cuda() && gscale->scalar_type() == at::kFloat && gscale->numel() >= 2, "gscale: fp32[2]");
+    gs = gscale->data_ptr<float>();
+  }
+  HIPCHK(mamba_amd::launch_adamw(tab.data_ptr(), blk.data_ptr<int64_t>(), (int)blk.size(0), gs, (float)b1, (float)b2,
+                                 (float)eps, cur_stream()));
+}
+
+int64_t opt_chunk() { return mamba_amd::opt_chunk(); }
+
 // out (+)= sum over the leading dim of part (S, ...) in fixed order; out fp32 contiguous, numel(out) = numel(part[0])
 void gp_reduce(Tensor part, Tensor out, bool accumulate) {
   check_cuda(part, "part");
@@ -1153,6 +1196,10 @@ TORCH_LIBRARY(mamba_amd, m) {
   m.def("part_rows(str kind, int a, int b=0) -> int", &part_rows);
   m.def("gp_reduce(Tensor part, Tensor(a!) out, bool accumulate=False) -> ()");
   m.def("transpose_bf16(Tensor X) -> Tensor");
+  m.def("colsum(Tensor(a!) part) -> Tensor");
+  m.def("opt_grad_norm(Tensor tab, Tensor blk, float max_norm, float divisor) -> Tensor");
+  m.def("opt_adamw(Tensor tab, Tensor blk, Tensor? gscale, float b1, float b2, float eps) -> ()");
+  m.def("opt_chunk() -> int", &opt_chunk);
   m.def("gemm_skinny(Tensor A, Tensor B, Tensor(a!)? out=None, bool accumulate=False) -> Tensor");
   m.def("ssm_state_update(Tensor(a!) state, Tensor x, Tensor dt, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? z, "
         "Tensor? dt_bias, bool softplus) -> Tensor");
@@ -1173,6 +1220,9 @@ TORCH_LIBRARY_IMPL(mamba_amd, CUDA, m) {
   m.impl("gp_pk", &gp_pk);
   m.impl("gp_reduce", &gp_reduce);
   m.impl("transpose_bf16", &transpose_bf16);
+  m.impl("colsum", &colsum);
+  m.impl("opt_grad_norm", &opt_grad_norm);
+  m.impl("opt_adamw", &opt_adamw);
   m.impl("add_rmsnorm_bwd", &add_rmsnorm_bwd);
   m.impl("gated_rmsnorm_fwd", &gated_rmsnorm_fwd);
   m.impl("gated_rmsnorm_bwd", &gated_rmsnorm_bwd);

@@ -134,6 +134,12 @@ int gemm_wg_nb();
 void set_gemm_wg_nb(int nb);
 // out[i] (+)= sum_s part[s * stride + i], fixed order
 hipError_t launch_transpose_bf16(const void* x, int64_t ldx, void* y, int64_t ldy, int R, int C, hipStream_t st);
+// native optimizer step (optim.hip): segs = OptSeg table (64 B per parameter), blk = (segment, offset) per chunk
+int opt_chunk();
+hipError_t launch_grad_norm(const void* segs, const int64_t* blk, int nblk, float* partial, float max_norm,
+                            float divisor, float* out, hipStream_t st);
+hipError_t launch_adamw(const void* segs, const int64_t* blk, int nblk, const float* gscale, float b1, float b2,
+                        float eps, hipStream_t st);
 hipError_t launch_gp_reduce(const float* part, int S, int64_t stride, int64_t n, float* out, bool accumulate,
                             hipStream_t st);
 

@@ -313,6 +313,9 @@ __global__ __launch_bounds__(256) void colsum_split_k(float* __restrict__ part, 
 // Column sums of a (nrows, ncols) fp32 partial block (clobbers `part`).  Tall blocks with few column
 // tiles (norm weight grads: 2048 x 768 -> 12 tiles) are split over >= ~512 workgroups first, so the
 // sum is bandwidth- rather than latency-bound; the second stage reduces the RS split sums.
+// (A single-launch form -- each tile's last block summing the splits behind an agent-scope release/acquire
+// handoff -- measured 39-43 us against 6.5-10.6 us for the two launches at the backward's shapes: the device-scope
+// release writes back the XCD's L2 (profiles/r5/colsum_single_launch_rejected.txt).)
 hipError_t launch_colsum(float* part, int nrows, int ncols, float* out, hipStream_t st) {
   const int tiles = (ncols + 63) / 64;
   int RS = std::min((nrows + 15) / 16, std::max(1, 512 / tiles));

@@ -155,5 +155,12 @@ class LMHeadModel(MambaLMHeadModel):
         use_fused = fused_available and device_type == "cuda"
         if master_process:
             print(f"using fused AdamW: {use_fused}")
+        # on the GPU the native multi-tensor AdamW (ops/optim.py: same update, clip and bf16 weight images folded
+        # in); MAMBA_AMD_NATIVE_ADAMW=0 keeps torch's fused AdamW
+        import os
+        from .ops.optim import NativeAdamW, native_available
+        if (use_fused and os.environ.get("MAMBA_AMD_NATIVE_ADAMW", "1") != "0"
+                and native_available(decay_params + nodecay_params)):
+            return NativeAdamW(optim_groups, lr=learning_rate, betas=betas, eps=eps)
         return torch.optim.AdamW(optim_groups, lr=learning_rate, betas=betas, eps=eps, fused=use_fused)
 

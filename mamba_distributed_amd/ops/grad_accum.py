@@ -190,6 +190,7 @@ def release_buffers() -> None:
         raise RuntimeError("grad_accum.release_buffers() inside an accumulation_scope")
     _bufs.clear()
     _wcache.clear()
+    drop_images()
 
 
 def in_scope() -> bool:
@@ -200,30 +201,72 @@ def direct() -> bool:
     return _direct and _scope_depth > 0
 
 
+# ---- bf16 weight images written by the native optimizer step (ops/optim.py) ----------------------------------
+# The scope records which images of which parameters its GEMMs asked for (``image_demand``); the native AdamW writes
+# exactly those images in its update pass (same bytes the per-step cast / zero-padded copy would produce) and
+# ``provide_image`` registers them; the next scope takes them instead of casting again.  An image is valid while the
+# parameter's version counter is unchanged (the optimizer's raw-pointer update does not bump it; any other in-place
+# write -- load_state_dict, a manual edit -- does, and the image is ignored from then on).
+_demand: Dict[Tuple[int, tuple], Tuple[torch.Tensor, tuple]] = {}
+_images: Dict[Tuple[int, tuple], Tuple[torch.Tensor, torch.Tensor, int]] = {}
+
+
+def _want(w: torch.Tensor, kind: tuple):
+    """Record the demand for image ``kind`` of parameter ``w``; return the provided image if it is fresh."""
+    if not (isinstance(w, torch.nn.Parameter) and w.requires_grad and w.is_cuda):
+        return None
+    key = (id(w), kind)
+    _demand[key] = (w, kind)
+    ent = _images.get(key)
+    if ent is not None and ent[0] is w and ent[2] == w._version:
+        return ent[1]
+    return None
+
+
+def image_demand() -> List[Tuple[torch.Tensor, tuple]]:
+    """(parameter, kind) pairs the GEMMs asked for since the process started; kind = ("cast", dtype) or
+    ("pad_rows", dtype, rows)."""
+    return list(_demand.values())
+
+
+def provide_image(w: torch.Tensor, kind: tuple, img: torch.Tensor) -> None:
+    _images[(id(w), kind)] = (w, img, w._version)
+
+
+def drop_images() -> None:
+    _images.clear()
+    _demand.clear()
+
+
 def cached_cast(w: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
-    """``w.to(dtype)``, reused across the micro-steps of the current scope."""
+    """``w.to(dtype)``, reused across the micro-steps of the current scope (or the optimizer's fresh image)."""
     if w.dtype == dtype or _scope_depth == 0:
         return w.to(dtype)
     key = (id(w), dtype)
     ent = _wcache.get(key)
     if ent is not None and ent[0] is w:
         return ent[1]
-    t = w.to(dtype)
+    t = _want(w, ("cast", dtype))
+    if t is None:
+        t = w.to(dtype)
     _wcache[key] = (w, t)  # holding w keeps id(w) unique for the scope's lifetime
     return t
 
 
-def cached_value(w: torch.Tensor, tag: str, fn):
+def cached_value(w: torch.Tensor, tag, fn):
     """``fn(w)`` (a function of a parameter only, e.g. A = -exp(A_log)), computed once per scope like
-    ``cached_cast``; outside a scope it is computed every call."""
+    ``cached_cast``; outside a scope it is computed every call.  ("pad_rows", dtype, rows) tags may come from the
+    optimizer's images."""
     if _scope_depth == 0:
         return fn(w)
     key = (id(w), tag)
     ent = _wcache.get(key)
     if ent is not None and ent[0] is w:
         return ent[1]
-    with torch.no_grad():
-        t = fn(w)
+    t = _want(w, tag) if isinstance(tag, tuple) and tag and tag[0] == "pad_rows" else None
+    if t is None:
+        with torch.no_grad():
+            t = fn(w)
     _wcache[key] = (w, t)
     return t
 

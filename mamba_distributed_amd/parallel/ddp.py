@@ -108,6 +108,26 @@ def clip_grad_norm_(model, max_norm: float) -> torch.Tensor:
     return total
 
 
+def clip_and_step(model, optimizer, max_norm: float) -> torch.Tensor:
+    """``clip_grad_norm_(model, max_norm)`` then ``optimizer.step()`` (reference train.py:222, :227).  With the
+    native AdamW (ops/optim.py) the two are one norm pass and one update pass with the clip coefficient folded into
+    the update's gradient read; under the native reducer the 1/world average rides on the same coefficient from the
+    second step on (the reducer stops scaling its flat buffer: one full pass over it less per step)."""
+    from ..ops.optim import NativeAdamW
+    if not isinstance(optimizer, NativeAdamW):
+        norm = clip_grad_norm_(model, max_norm)
+        optimizer.step()
+        return norm
+    r = _reducer(model)
+    norm = optimizer.clip_and_step(max_norm)
+    if r is not None and r.world > 1 and r.comm_dtype is None:
+        # the first step's gradients were averaged by the reducer; from the next step on it leaves them summed
+        # and the optimizer divides (so nothing else may read .grad between finish() and this call)
+        r.average_in_finish = False
+        optimizer.fold_average = float(r.world)
+    return norm
+
+
 def finish_grad_sync(model) -> None:
     """Wait for the native reducer's bucket all-reduces (no-op for DDP / single process)."""
     r = _reducer(model)

@@ -62,6 +62,9 @@ class GradReducer:
             self._attach(p)
         self._hooks = [p.register_post_accumulate_grad_hook(self._hook) for p in params]
         self._armed = False
+        # finish() divides the summed gradients by the world size; parallel/ddp.py::clip_and_step turns this off when
+        # the native optimizer folds the 1/world factor into its update
+        self.average_in_finish = True
         self._main = None  # the stream that called arm() (the caller's / main micro-batch stream)
         # exposed all-reduce time per sync step: stream time from the end of the last backward
         # (finish() entry, in stream order) to the averaged gradients being ready (finish() exit)
@@ -148,7 +151,7 @@ class GradReducer:
                 w[0].wait()
                 if w[1] is not None:
                     w[1].copy_(w[2])
-        if self.world > 1 and self.comm_dtype is None:
+        if self.world > 1 and self.comm_dtype is None and self.average_in_finish:
             self.flat.mul_(1.0 / self.world)
         if t0 is not None:
             self._exposed.append((t0, self._stamp()))

@@ -272,15 +272,16 @@ class Trainer:
             loss_accum = run_micro_batches(self.model, lambda: self._batch(self.train_loader), self.grad_accum_steps,
                                            compute_loss, overlap=overlap)
         all_reduce_avg(loss_accum)
-        if self.parallel:
-            sync_tp_grads(self.model, self.groups)
-            norm = par_clip_grad_norm_(self.model, self.a.grad_clip, self.groups)
-        else:
-            norm = ddp_mod.clip_grad_norm_(self.model, self.a.grad_clip)
         lr = self.lr(step)
         for g in self.optimizer.param_groups:
             g["lr"] = lr
-        self.optimizer.step()
+        if self.parallel:
+            sync_tp_grads(self.model, self.groups)
+            norm = par_clip_grad_norm_(self.model, self.a.grad_clip, self.groups)
+            self.optimizer.step()
+        else:
+            # clip + AdamW (one norm pass and one update pass on the native optimizer, parallel/ddp.py)
+            norm = ddp_mod.clip_and_step(self.model, self.optimizer, self.a.grad_clip)
         return loss_accum, norm, lr
 
     def save(self, step, val_loss):
