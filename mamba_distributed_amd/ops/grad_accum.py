@@ -212,8 +212,10 @@ _images: Dict[Tuple[int, tuple], Tuple[torch.Tensor, torch.Tensor, int]] = {}
 
 
 def _want(w: torch.Tensor, kind: tuple):
-    """Record the demand for image ``kind`` of parameter ``w``; return the provided image if it is fresh."""
-    if not (isinstance(w, torch.nn.Parameter) and w.requires_grad and w.is_cuda):
+    """Record the demand for image ``kind`` of parameter ``w``; return the provided image if it is fresh.  Only
+    where autograd is off (inside a custom Function's forward, which computes the weight gradient itself): an image
+    is a plain tensor, so a differentiable use (F.linear on it in module code) would lose the weight's gradient."""
+    if not (isinstance(w, torch.nn.Parameter) and w.requires_grad and w.is_cuda) or torch.is_grad_enabled():
         return None
     key = (id(w), kind)
     _demand[key] = (w, kind)

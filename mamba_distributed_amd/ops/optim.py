@@ -40,6 +40,12 @@ def native_available(params) -> bool:
             and _ext.load())
 
 
+def _images_enabled() -> bool:
+    """MAMBA_AMD_OPT_IMAGES=0: the update writes no bf16 weight images (the GEMMs cast per step as before)."""
+    import os
+    return os.environ.get("MAMBA_AMD_OPT_IMAGES", "1") != "0"
+
+
 class NativeAdamW(torch.optim.Optimizer):
     """AdamW (decoupled weight decay) over fp32 CUDA parameters on the native multi-tensor kernel."""
 
@@ -125,8 +131,9 @@ class NativeAdamW(torch.optim.Optimizer):
         self._ensure_flat()
         chunk = int(_ext.ops().opt_chunk())
         wanted: Dict[int, List[tuple]] = {}
-        for p, kind in grad_accum.image_demand():
-            wanted.setdefault(id(p), []).append(kind)
+        if _images_enabled():
+            for p, kind in grad_accum.image_demand():
+                wanted.setdefault(id(p), []).append(kind)
         out = {}
         for gi, group in enumerate(self.param_groups):
             lr, wd = group["lr"], group["weight_decay"]

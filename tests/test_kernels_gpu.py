@@ -893,11 +893,14 @@ def test_microbatch_overlap_is_bitwise_identical(cuda, layer):
     ("Mamba2", "fp32", 3, "native"), ("Mamba1", "fp32", 3, "native"), ("Mamba2", "bf16", 3, "native"),
     # the 8-GPU per-rank regime (accum 2: forward 0 on the second stream) and the degenerate accum 1
     ("Mamba2", "fp32", 2, "native"), ("Mamba2", "fp32", 1, "native"), ("Mamba1", "fp32", 2, "native"),
-    ("Mamba2", "fp32", 2, "ddp"), ("Mamba2", "fp32", 1, "ddp")])
+    ("Mamba2", "fp32", 2, "ddp"), ("Mamba2", "fp32", 1, "ddp"),
+    # three optimizer steps through clip_and_step: the native AdamW with the reducer's average folded in
+    ("Mamba2", "fp32", 1, "optim"), ("Mamba1", "fp32", 2, "optim")])
 def test_native_reducer_two_ranks_one_gpu(cuda, layer, comm, accum, impl):
     """parallel/reducer.py (and torch DDP) on real HIP streams: two gloo ranks on cuda:0, overlapped
     micro-batches, tiny buckets; the averaged gradients match the single-process global-batch gradients
-    (tests/reducer_worker.py), at accum 1, 2 (the 8-GPU per-rank regime) and 3."""
+    (tests/reducer_worker.py), at accum 1, 2 (the 8-GPU per-rank regime) and 3; "optim": parameters after three
+    clip + native-AdamW steps match a single process on torch's AdamW."""
     import socket
     import subprocess
     import sys
@@ -909,7 +912,7 @@ def test_native_reducer_two_ranks_one_gpu(cuda, layer, comm, accum, impl):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port),
            os.path.join(root, "tests", "reducer_worker.py"), "--layer", layer, "--comm-dtype", comm,
-           "--accum", str(accum), "--impl", impl]
+           "--accum", str(accum)] + (["--optim"] if impl == "optim" else ["--impl", impl])
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=110,
                        env=dict(os.environ, PYTHONPATH=root, OMP_NUM_THREADS="4"))
     if r.returncode != 0:  # the launcher's banner hides the worker's error at the end of stderr

@@ -85,13 +85,16 @@ def test_native_adamw_writes_bf16_images():
     ps = _params(5)
     w_cast, w_pad = ps[0], ps[1]
     opt = NativeAdamW(_groups(ps), lr=1e-3)
-    with grad_accum.accumulation_scope():
+    # the ops take images inside their autograd Functions' forwards, where grad mode is off
+    with grad_accum.accumulation_scope(), torch.no_grad():
         c0 = grad_accum.cached_cast(w_cast, torch.bfloat16)
         p0 = grad_accum.cached_value(w_pad, ("pad_rows", torch.bfloat16, 3456), lambda t: None)  # demand recorded
     assert c0.dtype == torch.bfloat16 and p0 is None
     _grads(ps, 0)
     opt.clip_and_step(1.0)
-    with grad_accum.accumulation_scope():
+    with grad_accum.accumulation_scope():  # differentiable context: never an image (it would drop the gradient)
+        assert grad_accum.cached_cast(w_cast, torch.bfloat16).grad_fn is not None
+    with grad_accum.accumulation_scope(), torch.no_grad():
         c1 = grad_accum.cached_cast(w_cast, torch.bfloat16)
         p1 = grad_accum.cached_value(w_pad, ("pad_rows", torch.bfloat16, 3456), lambda t: None)
     assert torch.equal(c1, w_cast.detach().to(torch.bfloat16))
@@ -100,7 +103,7 @@ def test_native_adamw_writes_bf16_images():
     assert not p1[3392:].any()
     with torch.no_grad():
         w_cast.mul_(2.0)  # bumps the version: the image is stale
-    with grad_accum.accumulation_scope():
+    with grad_accum.accumulation_scope(), torch.no_grad():
         c2 = grad_accum.cached_cast(w_cast, torch.bfloat16)
     assert torch.equal(c2, w_cast.detach().to(torch.bfloat16))
     grad_accum.drop_images()
