@@ -74,14 +74,13 @@ def auto_overlap(cfg, micro_tokens: int = 32768) -> bool:
 
 
 def auto_defer_reduce(cfg) -> bool:
-    """Default for the deferred partial reductions (ops/grad_accum.py::deferred), by model width.
-    Measured on one MI355X (interleaved runs): Mamba-2 280M 272k -> 283k tok/s with deferral, but
-    Mamba-2 1.4B (d_model 2048, overlap off) 88k -> 41k: there the deferred projection slabs are
-    full-size K-split GEMMs on the weight-gradient side stream, and next to the main stream's
-    chip-filling GEMMs they serialise.  So: on for d_model <= 1024 (same crossover as overlap).  Mamba-1 keeps
-    them off: its channel-major projections reduce their own split-K slabs, and with the deferred norm /
-    out_proj partials the 280M step measured 208k against 214-218k without (profiles/r3/ab3_mamba1_deferral.txt)."""
-    return getattr(cfg, "d_model", 0) <= 1024 and getattr(cfg, "layer_type", "Mamba2") != "Mamba1"
+    """Default for the deferred partial reductions (ops/grad_accum.py::deferred), by model width.  Round 3 measured
+    Mamba-2 1.4B at 88k -> 41k and Mamba-1 280M -1% with deferral: both were the allocator pressure of the side
+    stream's record_stream lifetimes, gone since the stream-ordered keep-alive (ops/grad_accum.py::side_keep).
+    Re-measured on one MI355X, interleaved (profiles/r5/defer_reduce_ab.txt): 1.4B +0.5% (172.8 vs 148.8 GB
+    reserved), Mamba-1 280M +0.5%.  So: on up to d_model 2048; off above (2.8B, whose persistent fp32 K-split slabs
+    would add ~30 GB to a 230 GB peak)."""
+    return getattr(cfg, "d_model", 0) <= 2048
 
 
 def resolve_overlap(mode, cfg, micro_tokens: int = 32768) -> bool:

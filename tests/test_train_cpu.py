@@ -79,14 +79,16 @@ def test_overlap_policy_by_width():
 
 
 def test_defer_reduce_policy_by_width(monkeypatch):
-    """auto_defer_reduce: on for d_model <= 1024; accumulation_scope(defer_reduce=...) gates
+    """auto_defer_reduce: on for d_model <= 2048 (both mixers); accumulation_scope(defer_reduce=...) gates
     grad_accum.deferred, and MAMBA_AMD_DEFER_REDUCE=0/1 overrides it."""
     import torch
     from mamba_distributed_amd import preset
     from mamba_distributed_amd.ops import grad_accum
     from mamba_distributed_amd.parallel.microbatch import auto_defer_reduce
     assert auto_defer_reduce(preset("mamba2-280m")) is True
-    assert auto_defer_reduce(preset("mamba2-1.4b")) is False
+    assert auto_defer_reduce(preset("mamba1-280m")) is True
+    assert auto_defer_reduce(preset("mamba2-1.4b")) is True
+    assert auto_defer_reduce(preset("mamba2-2.8b")) is False
     p = torch.nn.Parameter(torch.zeros(4))
     monkeypatch.delenv("MAMBA_AMD_DEFER_REDUCE", raising=False)
     try:
