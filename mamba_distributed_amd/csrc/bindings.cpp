@@ -829,15 +829,32 @@ static bool staged_wgrad(const Tensor& dY, int la, const Tensor& X, int lb, int6
                          Tensor& C, bool accumulate) {
   if (mamba_amd::gemm_wg_nb() == 0) return false;
   const int64_t lda = dY.size(0) == 1 ? dY.size(1) : dY.stride(0), ldb = X.size(0) == 1 ? X.size(1) : X.stride(0);
-  if (!mamba_amd::gemm_pipe_supported(la, lb, (int)P, (int)Q, (int)M, lda, ldb, Q)) return false;
-  const int S = mamba_amd::gemm_pipe_splits((int)P, (int)Q, (int)M);
-  auto part = at::empty({S, P, Q}, dY.options().dtype(at::kFloat));
-  const hipError_t e = mamba_amd::launch_gemm_pipe(la, lb, dY.data_ptr(), lda, X.data_ptr(), ldb, part.data_ptr(), Q,
-                                                   (int)P, (int)Q, (int)M, S, P * Q, 1, 256, cur_stream());
+  // narrow outputs: the output dimension the engine tiles by rows (128-row tile form) should be the narrow one --
+  // the Mamba-1 x_proj (80 x 1536) as is, the dt_proj (1536 x 48) as its transpose (48 x 1536), reduced into a
+  // (Q, P) buffer and added transposed (256-column tiles would compute 81% zeros there)
+  const bool swap = P > 128 && Q <= 128;
+  const int64_t R = swap ? Q : P, Cc = swap ? P : Q;
+  if (!(swap ? mamba_amd::gemm_pipe_supported(lb, la, (int)R, (int)Cc, (int)M, ldb, lda, Cc)
+             : mamba_amd::gemm_pipe_supported(la, lb, (int)R, (int)Cc, (int)M, lda, ldb, Cc)))
+    return false;
+  const int S = mamba_amd::gemm_pipe_splits((int)R, (int)Cc, (int)M);
+  const int bm = R <= 128 ? 128 : 256;
+  auto part = at::empty({S, R, Cc}, dY.options().dtype(at::kFloat));
+  const hipError_t e = swap ? mamba_amd::launch_gemm_pipe(lb, la, X.data_ptr(), ldb, dY.data_ptr(), lda, part.data_ptr(),
+                                                          Cc, (int)R, (int)Cc, (int)M, S, R * Cc, 1, bm, cur_stream())
+                            : mamba_amd::launch_gemm_pipe(la, lb, dY.data_ptr(), lda, X.data_ptr(), ldb, part.data_ptr(),
+                                                          Cc, (int)R, (int)Cc, (int)M, S, R * Cc, 1, bm, cur_stream());
   if (e == hipErrorInvalidValue) return false;
   HIPCHK(e);
-  HIPCHK(mamba_amd::launch_gp_reduce(part.data_ptr<float>(), S, P * Q, P * Q, C.data_ptr<float>(), accumulate,
-                                     cur_stream()));
+  if (!swap) {
+    HIPCHK(mamba_amd::launch_gp_reduce(part.data_ptr<float>(), S, P * Q, P * Q, C.data_ptr<float>(), accumulate,
+                                       cur_stream()));
+    return true;
+  }
+  auto ct = at::empty({Q, P}, dY.options().dtype(at::kFloat));
+  HIPCHK(mamba_amd::launch_gp_reduce(part.data_ptr<float>(), S, P * Q, P * Q, ct.data_ptr<float>(), false, cur_stream()));
+  if (accumulate) C.add_(ct.t());
+  else C.copy_(ct.t());
   return true;
 }
 

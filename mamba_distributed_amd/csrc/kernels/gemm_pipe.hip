@@ -905,7 +905,6 @@ hipError_t launch_gemm_pipe(int la, int lb, const void* A, int64_t lda, const vo
                             hipStream_t st) {
   if (!gemm_pipe_supported(la, lb, M, N, K, lda, ldb, ldc)) return hipErrorInvalidValue;
   if (splits < 1 || (splits > 1 && epi == 0) || (bm != 256 && bm != 128)) return hipErrorInvalidValue;
-  if (bm == 128 && (epi != 0 || lb != 1)) return hipErrorInvalidValue;  // instantiated: narrow A . XC B, bf16 out
   GemmPipeArgs a;
   a.A = (const bf16_t*)A; a.lda = lda; a.B = (const bf16_t*)B; a.ldb = ldb;
   a.C = C; a.ldc = ldc; a.split_stride = split_stride;
@@ -921,19 +920,23 @@ hipError_t launch_gemm_pipe(int la, int lb, const void* A, int64_t lda, const vo
     a.nbB = (unsigned)((lb ? (int64_t)(K - 1) * ldb + N : (int64_t)(N - 1) * ldb + K) * 2);
     const int mi = bm == 128 ? 4 : 8;
 #define WG_L(LA_, LB_, E_, MI_) hipLaunchKernelGGL((gemm_wg_k<LA_, LB_, E_, 4, MI_>), dim3(nwg), dim3(512), 0, st, a)
+#define WG_M(LA_, LB_, MI_)                                     \
+  if (epi == 0) WG_L(LA_, LB_, 0, MI_);                         \
+  else if (epi == 1) WG_L(LA_, LB_, 1, MI_);                    \
+  else WG_L(LA_, LB_, 2, MI_);
 #define WG_E(LA_, LB_)                                          \
-  if (mi == 4) WG_L(LA_, LB_, 0, 4);                            \
-  else if (epi == 0) WG_L(LA_, LB_, 0, 8);                      \
-  else if (epi == 1) WG_L(LA_, LB_, 1, 8);                      \
-  else WG_L(LA_, LB_, 2, 8);
+  if (mi == 4) { WG_M(LA_, LB_, 4) }                            \
+  else { WG_M(LA_, LB_, 8) }
     if (la == 0 && lb == 0) { WG_E(0, 0) }
     else if (la == 0 && lb == 1) { WG_E(0, 1) }
     else if (la == 1 && lb == 1) { WG_E(1, 1) }
     else { WG_E(1, 0) }
 #undef WG_E
+#undef WG_M
 #undef WG_L
     return hipGetLastError();
   }
+  if (bm == 128 && (epi != 0 || lb != 1)) return hipErrorInvalidValue;  // gemm_pipe_k: narrow A . XC B, bf16 out
   if (bm == 128) {
     if (la == 0) hipLaunchKernelGGL((gemm_pipe_k<0, 1, 0, 4, 4>), dim3(nwg), dim3(GP_NT), 0, st, a);
     else hipLaunchKernelGGL((gemm_pipe_k<1, 1, 0, 4, 4>), dim3(nwg), dim3(GP_NT), 0, st, a);

@@ -53,6 +53,9 @@ def m1_cases(T=65536, d=768, di=1536, R=48, N=16):
         ("m1_out_wgrad XC.KC slabs", dout, y2, 1, 0, 1, 0, 256, 2.0 * T * di * d),
         ("m1_in_wgrad KC.XC slabs", dxz, h2, 0, 1, 1, 0, 256, 2.0 * T * d * 2 * di),
         ("m1_x_wgrad KC.KC slabs", dxdbl, co2, 0, 0, 1, 0, 256, 2.0 * T * di * (R + 2 * N)),
+        ("m1_x_wgrad KC.KC slabs 128-row", dxdbl, co2, 0, 0, 1, 0, 128, 2.0 * T * di * (R + 2 * N)),
+        ("m1_dt_wgrad KC.KC slabs (1536 x 48)", dd2, dxdbl[:R], 0, 0, 1, 0, 256, 2.0 * T * di * R),
+        ("m1_dt_wgrad^T KC.KC slabs 128-row (48 x 1536)", dxdbl[:R], dd2, 0, 0, 1, 0, 128, 2.0 * T * di * R),
     ]
 
 

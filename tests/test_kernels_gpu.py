@@ -1037,10 +1037,13 @@ def test_gemm_wgrad_channel_major(cuda, P, M, Q, acc):
 
 
 @pytest.mark.parametrize("dy_cm,x_cm", [(False, True), (True, True)])
-@pytest.mark.parametrize("P,M,Q", [(768, 32768, 1536), (200, 1024, 136)])
+@pytest.mark.parametrize("P,M,Q", [(768, 32768, 1536), (200, 1024, 136),
+                                   # the Mamba-1 x_proj (80 rows: 128-row tiles) and dt_proj (48 columns: computed
+                                   # transposed on 128-row tiles, added back transposed) weight gradients
+                                   (80, 32768, 1536), (1536, 32768, 48), (1536, 4096, 80)])
 def test_gemm_wgrad_channel_major_x(cuda, dy_cm, x_cm, P, M, Q):
     """gemm_wgrad_cm with a channel-major X (Mamba-1 out_proj dW = dout^T y^T from the (di, b*l) scan
-    output) and with both operands channel-major, accumulating into fp32."""
+    output) and with both operands channel-major, accumulating into fp32; deterministic run to run."""
     from mamba_distributed_amd.ops import _ext
     g = torch.Generator(device=cuda).manual_seed(1)
     dY = torch.randn(P, M, device=cuda, generator=g).to(torch.bfloat16)   # logical (P, M)
@@ -1052,6 +1055,9 @@ def test_gemm_wgrad_channel_major_x(cuda, dy_cm, x_cm, P, M, Q):
     _ext.ops().gemm_wgrad_cm(dY_arg, X_arg, out, True, dy_cm, x_cm)
     ref = dY.float() @ X.float().t() + base
     assert rel(out, ref) < 2e-3, rel(out, ref)
+    again = base.clone()
+    _ext.ops().gemm_wgrad_cm(dY_arg, X_arg, again, True, dy_cm, x_cm)
+    assert torch.equal(again, out)
 
 
 @pytest.mark.parametrize("sl_extra", [-1, 0, 3])
