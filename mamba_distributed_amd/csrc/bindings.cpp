@@ -608,14 +608,27 @@ void selscan_common(mamba_amd::SelScanArgs& a, const Tensor& u, const Tensor& de
   }
 }
 
-std::tuple<Tensor, Tensor, Tensor> selscan_fwd(Tensor u, Tensor delta, Tensor A, Tensor Bm, Tensor Cm,
-                                               optional<Tensor> D, optional<Tensor> z, optional<Tensor> delta_bias,
-                                               bool softplus) {
+// fused dt_proj (kernels/selective_scan.hip DTF): delta_raw = dtw (D, R) . dtx (R, B L) is computed inside the scan
+// kernels; the (b, d, l) delta tensor is never formed.  u stands in for delta in the shared layout checks.
+void selscan_dt_args(mamba_amd::SelScanArgs& a, const Tensor& dtw, const Tensor& dtx) {
+  TORCH_CHECK(dtw.dim() == 2 && dtw.is_contiguous() && dtw.scalar_type() == at::kBFloat16 && dtw.size(0) == a.D,
+              "dtw must be a contiguous bf16 (D, R) weight");
+  TORCH_CHECK(dtx.dim() == 2 && dtx.size(0) == dtw.size(1) && dtx.size(1) == (int64_t)a.B * a.L && dtx.stride(1) == 1 &&
+              dtx.scalar_type() == at::kBFloat16, "dtx must be (R, B L) bf16 rows with unit column stride");
+  a.delta_ = nullptr;
+  a.dtw_ = dtw.data_ptr(); a.dtx_ = dtx.data_ptr(); a.sdtx = dtx.stride(0); a.R = (int)dtw.size(1);
+}
+
+std::tuple<Tensor, Tensor, Tensor> selscan_fwd_impl(Tensor u, Tensor delta, Tensor A, Tensor Bm, Tensor Cm,
+                                                    optional<Tensor> D, optional<Tensor> z, optional<Tensor> delta_bias,
+                                                    bool softplus, optional<Tensor> dtw = c10::nullopt,
+                                                    optional<Tensor> dtx = c10::nullopt) {
   check_cuda(u, "u");
   at::hip::HIPGuardMasqueradingAsCUDA guard(u.device());
   mamba_amd::SelScanArgs a{};
   Tensor zz = z.has_value() && z->defined() ? *z : Tensor();
   selscan_common(a, u, delta, A, Bm, Cm, zz, softplus);
+  if (dtw.has_value()) selscan_dt_args(a, *dtw, *dtx);
   Tensor Af = f32c(A), Df = f32c_opt(D), bf = f32c_opt(delta_bias);
   a.A = Af.data_ptr<float>(); a.D_ = fptr(Df); a.delta_bias = fptr(bf);
   auto out = at::empty({a.D, a.B, a.L}, u.options()).permute({1, 0, 2});
@@ -628,20 +641,36 @@ std::tuple<Tensor, Tensor, Tensor> selscan_fwd(Tensor u, Tensor delta, Tensor A,
                                                            : at::empty({a.B, a.nct, a.D, a.N}, fo).permute({0, 2, 1, 3});
   auto last = at::empty({a.B, a.D, a.N}, fo);
   a.carries = carries.data_ptr<float>(); a.last_state = last.data_ptr<float>();
+  TORCH_CHECK(!a.dtw_ || mamba_amd::selscan_dt_fusable(a), "selscan_fwd_dt: shape not supported by the fused walk "
+              "(bf16, d_state 16, D % 64 == 0, L % 16 == 0, B D >= 32768, dt_rank % 8 == 0 and <= 128)");
   HIPCHK(mamba_amd::launch_selscan_fwd(a, cur_stream()));
   return {out, carries, last};
+}
+
+std::tuple<Tensor, Tensor, Tensor> selscan_fwd(Tensor u, Tensor delta, Tensor A, Tensor Bm, Tensor Cm,
+                                               optional<Tensor> D, optional<Tensor> z, optional<Tensor> delta_bias,
+                                               bool softplus) {
+  return selscan_fwd_impl(u, delta, A, Bm, Cm, D, z, delta_bias, softplus);
+}
+
+std::tuple<Tensor, Tensor, Tensor> selscan_fwd_dt(Tensor u, Tensor dtw, Tensor dtx, Tensor A, Tensor Bm, Tensor Cm,
+                                                  optional<Tensor> D, optional<Tensor> z, optional<Tensor> delta_bias,
+                                                  bool softplus) {
+  return selscan_fwd_impl(u, u, A, Bm, Cm, D, z, delta_bias, softplus, dtw, dtx);
 }
 
 std::vector<Tensor> selscan_bwd_impl(Tensor dout, Tensor u, Tensor delta, Tensor A, Tensor Bm, Tensor Cm,
                                      optional<Tensor> D, optional<Tensor> z, optional<Tensor> delta_bias, Tensor carries,
                                      bool softplus, optional<Tensor> dz_out, optional<Tensor> dB_out,
                                      optional<Tensor> dC_out, optional<Tensor> part_buf = c10::nullopt,
-                                     int64_t part_mode_ = 0) {
+                                     int64_t part_mode_ = 0, optional<Tensor> dtw = c10::nullopt,
+                                     optional<Tensor> dtx = c10::nullopt) {
   check_cuda(u, "u");
   at::hip::HIPGuardMasqueradingAsCUDA guard(u.device());
   mamba_amd::SelScanArgs a{};
   Tensor zz = z.has_value() && z->defined() ? *z : Tensor();
   selscan_common(a, u, delta, A, Bm, Cm, zz, softplus);
+  if (dtw.has_value()) selscan_dt_args(a, *dtw, *dtx);
   if (dout.stride(2) != 1 || dout.scalar_type() != u.scalar_type()) dout = dout.to(u.scalar_type()).contiguous();
   TORCH_CHECK(dout.sizes() == u.sizes(), "dout shape");
   // the carry granularity is the forward's choice: 16 steps (wave-per-state-group kernels) or 512
@@ -677,6 +706,8 @@ std::vector<Tensor> selscan_bwd_impl(Tensor dout, Tensor u, Tensor delta, Tensor
   a.dC_ = dC.data_ptr(); a.sdCb = dC.stride(0); a.sdCg = dC.stride(1); a.sdCn = dC.stride(2);
   auto fo = u.options().dtype(at::kFloat);
   a.Kc = mamba_amd::selscan_bwd_kc(a);
+  TORCH_CHECK(!a.dtw_ || (mamba_amd::selscan_bwd_sequential(a) && mamba_amd::selscan_dt_fusable(a)),
+              "selscan_bwd_dt: shape / layout not supported by the fused sequential backward");
   const int ndg = (a.D + a.Kc - 1) / a.Kc;
   auto part_bc = at::empty({2, a.B, ndg, a.N, a.L}, fo);
   a.part_dB = part_bc[0].data_ptr<float>(); a.part_dC = part_bc[1].data_ptr<float>();
@@ -720,6 +751,14 @@ std::vector<Tensor> selscan_bwd_into(Tensor dout, Tensor u, Tensor delta, Tensor
                                      optional<Tensor> part_buf, int64_t part_mode) {
   return selscan_bwd_impl(dout, u, delta, A, Bm, Cm, D, z, delta_bias, carries, softplus, dz_out, dB_out, dC_out,
                           part_buf, part_mode);
+}
+
+std::vector<Tensor> selscan_bwd_dt_into(Tensor dout, Tensor u, Tensor dtw, Tensor dtx, Tensor A, Tensor Bm, Tensor Cm,
+                                        optional<Tensor> D, optional<Tensor> z, optional<Tensor> delta_bias,
+                                        Tensor carries, bool softplus, Tensor dz_out, Tensor dB_out, Tensor dC_out,
+                                        optional<Tensor> part_buf, int64_t part_mode) {
+  return selscan_bwd_impl(dout, u, u, A, Bm, Cm, D, z, delta_bias, carries, softplus, dz_out, dB_out, dC_out, part_buf,
+                          part_mode, dtw, dtx);
 }
 
 // decode-time recurrent update; Mamba-1: state (b,d,n), x/dt/z (b,d), A (d,n), B/C (b,n), D (d)
@@ -1199,6 +1238,11 @@ TORCH_LIBRARY(mamba_amd, m) {
   m.def("selscan_bwd_into(Tensor dout, Tensor u, Tensor delta, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? z, "
         "Tensor? delta_bias, Tensor carries, bool softplus, Tensor(a!) dz_out, Tensor(b!) dB_out, Tensor(c!) dC_out, "
         "Tensor(z!)? part_buf=None, int part_mode=0) -> Tensor[]");
+  m.def("selscan_fwd_dt(Tensor u, Tensor dtw, Tensor dtx, Tensor A, Tensor B, Tensor C, Tensor? D, Tensor? z, "
+        "Tensor? delta_bias, bool softplus) -> (Tensor, Tensor, Tensor)");
+  m.def("selscan_bwd_dt_into(Tensor dout, Tensor u, Tensor dtw, Tensor dtx, Tensor A, Tensor B, Tensor C, Tensor? D, "
+        "Tensor? z, Tensor? delta_bias, Tensor carries, bool softplus, Tensor(a!) dz_out, Tensor(b!) dB_out, "
+        "Tensor(c!) dC_out, Tensor(z!)? part_buf=None, int part_mode=0) -> Tensor[]");
   m.def("gemm_tn(Tensor A, Tensor B, Tensor(a!)? out=None) -> Tensor");
   m.def("gemm_wgrad(Tensor dY, Tensor X, Tensor(a!)? out=None, bool accumulate=False) -> Tensor");
   m.def("gemm_wgrad_cm(Tensor dY, Tensor X, Tensor(a!)? out=None, bool accumulate=False, bool dy_cm=True, "
@@ -1257,6 +1301,8 @@ TORCH_LIBRARY_IMPL(mamba_amd, CUDA, m) {
   m.impl("selscan_fwd", &selscan_fwd);
   m.impl("selscan_bwd", &selscan_bwd);
   m.impl("selscan_bwd_into", &selscan_bwd_into);
+  m.impl("selscan_fwd_dt", &selscan_fwd_dt);
+  m.impl("selscan_bwd_dt_into", &selscan_bwd_dt_into);
   m.impl("ssm_state_update", &ssm_state_update);
   m.impl("decode_inproj", &decode_inproj);
   m.impl("decode_ssm", &decode_ssm);

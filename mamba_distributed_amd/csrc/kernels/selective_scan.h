@@ -34,6 +34,10 @@ struct SelScanArgs {
   float* part_dA;                                   // (B, D, N)   zero-initialised
   float* part_dD; float* part_dbias;                // (B, D)      zero-initialised
   bool pacc;  // sequential backward only: add into part_dA / part_dD / part_dbias (deferred reduction)
+  // fused dt_proj (Mamba-1, wave-per-state-group kernels only): delta_raw[b, d, t] = sum_r dtw[d, r] dtx[r, b L + t],
+  // computed per 16-step tile with MFMA inside the scan (delta_ unused, never materialised).  dtw (D, R) bf16
+  // contiguous, dtx (R, B L) bf16 rows (row stride sdtx, unit column stride); R % 8 == 0, R <= 128.
+  const void* dtw_; const void* dtx_; int64_t sdtx; int R;
 };
 
 struct SSMUpdateArgs {
@@ -55,6 +59,7 @@ hipError_t launch_selscan_bwd(const SelScanArgs& a, hipStream_t st);
 int selscan_carry_t(const SelScanArgs& a);
 // channels per backward workgroup (SelScanArgs::Kc; sizes the dB / dC partials); needs carry_t set
 int selscan_bwd_kc(const SelScanArgs& a);
+bool selscan_dt_fusable(const SelScanArgs& a);  // fused dt_proj (dtw_ / dtx_) supported for this shape
 bool selscan_bwd_sequential(const SelScanArgs& a);  // the wave-per-state-group kernel runs (supports pacc)
 hipError_t launch_ssm_update(const SSMUpdateArgs& a, hipStream_t st);
 

@@ -13,6 +13,7 @@
 //    run the adjoint as a DPP suffix scan; dB/dC sums over channels stay in registers.
 //  * deterministic everywhere: every partial has exactly one writer, reductions run in fixed order.
 #include "common.h"
+#include "mfma.h"
 #include "selective_scan.h"
 #include <cstdlib>
 #include <type_traits>
@@ -271,15 +272,28 @@ typedef float ss_f2 __attribute__((ext_vector_type(2)));
 // nothing per lane but dt and dt*u (staged once per tile in LDS for the 4 waves).  Per step and lane:
 // 2 v_pk_mul (dt A), 4 exp, 2 v_pk_mul (dt u B), 2 v_pk_fma (h), 2 v_pk_fma (C h).  The 4 waves' partial
 // y meet in LDS at the end of the tile; (y + D u) silu(z) leaves as coalesced rows.
+//
+// DTF (fused dt_proj, Mamba-1): delta is not read but computed per tile, delta_raw (64 channels x 16 steps) =
+// W_dt[d0 .. d0+63, :R] . x_dbl[:R, tile] as one 16x16x32 MFMA chain per wave (wave w: channels 16 w .. 16 w + 15,
+// K = R padded to 32 with zero weight columns and zero x rows).  The x_dbl tile (R rows x 16 steps, bf16) is staged in
+// LDS over the yS buffer (not live then) and read as the hardware-transposed B operand; each lane finishes its 4
+// channels x 1 step (bias, softplus, dt u) into dlS / duS behind one extra barrier.  The (B, D, L) delta tensor --
+// written by a separate GEMM and read here and in the backward -- no longer exists.
 constexpr int SG_T = 16, SG_D = 3;  // tile length, tiles of u / delta / z in flight
+constexpr int DTF_RMAX = 128;        // largest fused dt_rank (4 MFMA K-steps)
+template <int KS>  // KS = 0: delta read from memory; KS > 0: fused dt_proj with KS = ceil(R / 32) MFMA K-steps
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void selscan_fwd_sg_k(SelScanArgs a) {
   constexpr int N = 16;
+  constexpr bool DTF = KS > 0;
+  // ring depth: DTF drops to 2 tiles (a tile of the walk takes microseconds) to stay within 128 VGPRs
+  constexpr int SGD = DTF ? 2 : SG_D;
   __shared__ __attribute__((aligned(16))) float dlS[64][SG_T + 4], duS[64][SG_T + 4];
   __shared__ __attribute__((aligned(16))) float yS[4][64][SG_T + 4];
   __shared__ __attribute__((aligned(16))) bf16_t uS[64][SG_T];
   // this tile's B / C in fp32, per step t: wave w's 4 states of B then C at [t][8 w .. 8 w + 7]; a 36-float
   // row stride puts the 64 lanes' staging writes (steps 2j / 2j+1, state n, B or C) on 64 distinct banks
   __shared__ __attribute__((aligned(16))) float bcS[SG_T][36];
+  bf16_t* const xS = reinterpret_cast<bf16_t*>(&yS[0][0][0]);  // DTF: x_dbl tile [32 ceil(R / 32)][16]
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int wgs_per_b = a.D / 64;
   const int b = blockIdx.x / wgs_per_b, d0 = (blockIdx.x % wgs_per_b) * 64;
@@ -288,7 +302,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
   // staging / epilogue role: channel sr = tid >> 2, 4 steps at 4 * (tid & 3)
   const int sr = threadIdx.x >> 2, sc = (threadIdx.x & 3) * 4;
   const bf16_t* urow = ((const bf16_t*)a.u_) + (int64_t)b * a.sub + (int64_t)(d0 + sr) * a.sud;
-  const bf16_t* drow = ((const bf16_t*)a.delta_) + (int64_t)b * a.sdb + (int64_t)(d0 + sr) * a.sdd;
+  const bf16_t* drow = DTF ? nullptr : ((const bf16_t*)a.delta_) + (int64_t)b * a.sdb + (int64_t)(d0 + sr) * a.sdd;
   const bf16_t* zrow = a.z_ ? ((const bf16_t*)a.z_) + (int64_t)b * a.szb + (int64_t)(d0 + sr) * a.szd : nullptr;
   bf16_t* orow = ((bf16_t*)a.out_) + (int64_t)b * a.sob + (int64_t)(d0 + sr) * a.sod;
   const float sbias = a.delta_bias ? a.delta_bias[d0 + sr] : 0.f;
@@ -300,15 +314,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
   for (int p = 0; p < 2; ++p) A2[p] = ss_f2{a.A[d * N + 4 * w + 2 * p], a.A[d * N + 4 * w + 2 * p + 1]} * kLog2e;
   ss_f2 h[2] = {ss_f2{0.f, 0.f}, ss_f2{0.f, 0.f}};
   const int ntile = (a.L + SG_T - 1) / SG_T;
-  // SG_D-deep ring of this thread's u / delta / z pieces (8 B each): each tile's data was requested
-  // SG_D tiles earlier, so the short tiles never wait for HBM
+  // SGD-deep ring of this thread's u / delta / z pieces (8 B each): each tile's data was requested
+  // SGD tiles earlier, so the short tiles never wait for HBM
+  // DTF: thread tid stages 16 B of the x_dbl tile (row tid / 2, steps 8 (tid % 2) ..), the lane's A operand is
+  // its channel's W_dt row (L1-resident), and the lane's accumulator rows are channels 16 w + 4 (lane / 16) + r
+  // (addresses recomputed at each use: registers are the limit of this kernel)
   struct Ring { uint2 u, dl, z; };
-  Ring ring[SG_D];
+  Ring ring[SGD];
   auto fetch = [&](Ring& r, int tile) {  // clamped to L - 4 (L % 8 == 0): always legal
     const int t = min(tile * SG_T + sc, a.L - 4);
     r.u = *reinterpret_cast<const uint2*>(urow + t);
-    r.dl = *reinterpret_cast<const uint2*>(drow + t);
+    if (!DTF) r.dl = *reinterpret_cast<const uint2*>(drow + t);
     r.z = zrow ? *reinterpret_cast<const uint2*>(zrow + t) : make_uint2(0u, 0u);
+  };
+  // DTF: the x_dbl chunk one tile ahead (a tile of the walk takes microseconds; x_dbl is small and cache-resident),
+  // outside the SGD-deep ring to stay within the 128 VGPRs of 4 waves per SIMD
+  uint4 nx = make_uint4(0u, 0u, 0u, 0u);
+  auto fetch_x = [&](int tile) {  // DTF: L % 16 == 0, tile < ntile
+    const int xr = threadIdx.x >> 1;
+    if (xr < a.R)
+      nx = *reinterpret_cast<const uint4*>((const bf16_t*)a.dtx_ + (int64_t)xr * a.sdtx + (int64_t)b * a.L +
+                                           tile * SG_T + 8 * (threadIdx.x & 1));
   };
   // B / C rows (this wave's 4 states x 16 steps = 64 dwords) of the NEXT tile in flight during the
   // current one, one dword per lane (lane = 16 n + 8 [C] + j), moved to SGPRs with v_readlane
@@ -317,12 +343,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
   uint32_t bc = 0u;
   auto fetch_bc = [&](int tile) { bc = *reinterpret_cast<const uint32_t*>(blrow + min(tile * SG_T, a.L - SG_T)); };
 #pragma unroll
-  for (int k = 0; k < SG_D; ++k) fetch(ring[k], k);
+  for (int k = 0; k < SGD; ++k) fetch(ring[k], k);
   fetch_bc(0);
+  if (DTF) fetch_x(0);
   auto do_tile = [&](Ring& r, int tile) {
     const int t0 = tile * SG_T;
     __syncthreads();  // the previous tile's readers are done
-    {
+    // DTF: this lane's W_dt operand (zero past R) and its 4 channels' bias -- L1/L2-resident, issued here so their
+    // latency overlaps the barrier, after the wait for this tile's staged data and before the next tiles' prefetches
+    // (vmcnt retires loads in order); an opaque zero offset keeps the compiler from hoisting the loop-invariant
+    // loads out of the walk (they would hold registers through the step loop)
+    bf16x8 wk[KS > 0 ? KS : 1];
+    float bias4[4];
+    if (DTF) {
+      *reinterpret_cast<uint2*>(&uS[sr][sc]) = r.u;
+      if (threadIdx.x < 2 * 32 * KS)
+        *reinterpret_cast<uint4*>(xS + 8 * threadIdx.x) = (int)(threadIdx.x >> 1) < a.R ? nx : make_uint4(0u, 0u, 0u, 0u);
+      int opq = 0;
+      asm volatile("" : "+v"(opq));
+      const int g16 = lane >> 4, li = lane & 15;
+      const bf16_t* wrow = (const bf16_t*)a.dtw_ + (int64_t)(d0 + 16 * w + li + opq) * a.R + 8 * g16;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+        wk[ks] = 32 * ks + 8 * g16 < a.R ? *reinterpret_cast<const bf16x8*>(wrow + 32 * ks) : bf16x8{};
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4)
+        bias4[r4] = a.delta_bias ? a.delta_bias[d0 + opq + 16 * w + 4 * g16 + r4] : 0.f;
+    } else {
       const float u[4] = {__uint_as_float(r.u.x << 16), __uint_as_float(r.u.x & 0xffff0000u),
                           __uint_as_float(r.u.y << 16), __uint_as_float(r.u.y & 0xffff0000u)};
       const float raw[4] = {__uint_as_float(r.dl.x << 16), __uint_as_float(r.dl.x & 0xffff0000u),
@@ -345,8 +392,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
     bcS[2 * bl_j][8 * w + 4 * bl_m + bl_n] = __uint_as_float(bc << 16);
     bcS[2 * bl_j + 1][8 * w + 4 * bl_m + bl_n] = __uint_as_float(bc & 0xffff0000u);
     __syncthreads();
-    fetch(r, min(tile + SG_D, ntile - 1));
+    if (DTF) {
+      const int g16 = lane >> 4, li = lane & 15;
+      f32x4 acc = zero4();
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) acc = mfma16(wk[ks], frag_tr(xS, 16, 32 * ks, 0), acc);
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) {
+        const int ch = 16 * w + 4 * g16 + r4;
+        const float v = acc[r4] + bias4[r4];
+        const float dl = a.softplus ? softplus_fast(v) : v;
+        dlS[ch][li] = dl;
+        duS[ch][li] = dl * bf2f(uS[ch][li]);
+      }
+    }
+    fetch(r, min(tile + SGD, ntile - 1));
     fetch_bc(min(tile + 1, ntile - 1));
+    if (DTF) {
+      fetch_x(min(tile + 1, ntile - 1));
+      __syncthreads();  // every wave's channels of the tile are in dlS / duS
+    }
     if (a.carries && t0 % a.carry_t == 0)
       *reinterpret_cast<float4*>(a.carries + carry_index(a, b, d, t0 / a.carry_t) + 4 * w) =
           make_float4(h[0].x, h[0].y, h[1].x, h[1].y);
@@ -399,12 +464,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
     }
   };
   int tile = 0;
-  for (; tile + SG_D <= ntile; tile += SG_D) {
+  for (; tile + SGD <= ntile; tile += SGD) {
 #pragma unroll
-    for (int k = 0; k < SG_D; ++k) do_tile(ring[k], tile + k);
+    for (int k = 0; k < SGD; ++k) do_tile(ring[k], tile + k);
   }
 #pragma unroll
-  for (int k = 0; k < SG_D; ++k)
+  for (int k = 0; k < SGD; ++k)
     if (tile + k < ntile) do_tile(ring[k], tile + k);
   if (a.last_state)
     *reinterpret_cast<float4*>(a.last_state + ((int64_t)b * a.D + d) * N + 4 * w) =
@@ -1128,11 +1193,19 @@ __device__ __forceinline__ void lane_sum8x2(const float (&u)[8], const float (&v
   rv = zv;
 }
 
+//
+// DTF (fused dt_proj): as the forward, delta_raw of the tile is recomputed by one MFMA chain per wave from W_dt and
+// the staged x_dbl tile (over sS, which is not live between the finish of one tile and the adjoint of the next), and
+// each lane writes dt, dt u and softplus' of its 4 channels x 1 step behind one extra barrier.  Bitwise the same
+// delta as the forward (same operands, same instruction sequence).
+template <int KS>  // KS = 0: delta read from memory; KS > 0: fused dt_proj, KS = ceil(R / 32) MFMA K-steps
 __global__ __launch_bounds__(256) void selscan_bwd_sg_k(SelScanArgs a) {
   constexpr int N = 16, T = SGB_T, TH = SGB_T / 2;
+  constexpr bool DTF = KS > 0;
   // per step and channel: dt, dt u, dout silu(z) (adjoint) and u, softplus', dout silu'(z) (finish)
   __shared__ float dlS[T][65], duS[T][65], dyS[T][65], uS[T][65], sdS[T][65], gzS[T][65];
-  __shared__ float sS[4][3][T][65];  // per wave: sum_n lam B, A lam a h, C h
+  __shared__ __attribute__((aligned(16))) float sS[4][3][T][65];  // per wave: sum_n lam B, A lam a h, C h
+  bf16_t* const xS = reinterpret_cast<bf16_t*>(&sS[0][0][0][0]);  // DTF: x_dbl tile [32 ceil(R / 32)][16]
   __shared__ __attribute__((aligned(16))) float BCs[4][T][8];  // per wave and step: B of its 4 states, C
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int wgs_per_b = a.D / 64;
@@ -1143,7 +1216,7 @@ __global__ __launch_bounds__(256) void selscan_bwd_sg_k(SelScanArgs a) {
   // as a uniform base (SGPRs) plus a 32-bit per-thread offset (host: every row offset < 2^31).
   const int sr = threadIdx.x >> 2, sp = threadIdx.x & 3;
   const bf16_t* ub = (const bf16_t*)a.u_ + (int64_t)b * a.sub + (int64_t)d0 * a.sud;
-  const bf16_t* db = (const bf16_t*)a.delta_ + (int64_t)b * a.sdb + (int64_t)d0 * a.sdd;
+  const bf16_t* db = DTF ? nullptr : (const bf16_t*)a.delta_ + (int64_t)b * a.sdb + (int64_t)d0 * a.sdd;
   const bf16_t* gb = (const bf16_t*)a.dout_ + (int64_t)b * a.sgb + (int64_t)d0 * a.sgd;
   const bf16_t* zb = a.z_ ? (const bf16_t*)a.z_ + (int64_t)b * a.szb + (int64_t)d0 * a.szd : nullptr;
   bf16_t* dub = (bf16_t*)a.du_ + (int64_t)b * a.sdub + (int64_t)d0 * a.sdud;
@@ -1166,6 +1239,26 @@ __global__ __launch_bounds__(256) void selscan_bwd_sg_k(SelScanArgs a) {
   uint32_t nu[2], nr[2], ng[2], nz[2];
   uint32_t nbc = 0u;
   float4 nh;
+  // DTF: x_dbl tile staging (thread tid: row tid / 2, steps 8 (tid % 2) ..), W_dt operand rows, accumulator channels
+  const int xr = threadIdx.x >> 1, xh = threadIdx.x & 1, g16 = lane >> 4, li = lane & 15;
+  const bool xld = DTF && threadIdx.x < 2 * a.R;
+  const bf16_t* xrow = DTF ? (const bf16_t*)a.dtx_ + (int64_t)min(xr, a.R - 1) * a.sdtx + (int64_t)b * a.L + 8 * xh
+                           : nullptr;
+  // the lane's W_dt operand for every K-step and its 4 channels' bias stay in registers for the whole walk (the
+  // backward has the VGPRs; reloading them per tile put an L2 round trip on every tile's critical path)
+  bf16x8 wf[KS > 0 ? KS : 1];
+  float bias4[4] = {0.f, 0.f, 0.f, 0.f};
+  if (DTF) {
+    const bf16_t* wrow = (const bf16_t*)a.dtw_ + (int64_t)(d0 + 16 * w + li) * a.R + 8 * g16;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      wf[ks] = 32 * ks + 8 * g16 < a.R ? *reinterpret_cast<const bf16x8*>(wrow + 32 * ks) : bf16x8{};
+    if (a.delta_bias) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bias4[r] = a.delta_bias[d0 + 16 * w + 4 * g16 + r];
+    }
+  }
+  uint4 nx = make_uint4(0u, 0u, 0u, 0u);
   const bf16_t* Bw = ((const bf16_t*)a.Bm_) + (int64_t)b * a.sBb + (int64_t)g * a.sBg + (int64_t)(4 * w) * a.sBn;
   const bf16_t* Cw = ((const bf16_t*)a.Cm_) + (int64_t)b * a.sCb + (int64_t)g * a.sCg + (int64_t)(4 * w) * a.sCn;
   const int bl_n = lane >> 4, bl_m = (lane >> 3) & 1, bl_j = lane & 7;
@@ -1177,13 +1270,14 @@ __global__ __launch_bounds__(256) void selscan_bwd_sg_k(SelScanArgs a) {
     for (int hf = 0; hf < 2; ++hf) {
       const int t = tile * T + TH * hf;
       nu[hf] = *reinterpret_cast<const uint32_t*>(ub + t + ou);
-      nr[hf] = *reinterpret_cast<const uint32_t*>(db + t + od);
+      if (!DTF) nr[hf] = *reinterpret_cast<const uint32_t*>(db + t + od);
       ng[hf] = *reinterpret_cast<const uint32_t*>(gb + t + og);
       nz[hf] = zb ? *reinterpret_cast<const uint32_t*>(zb + t + oz) : 0u;
     }
     if (bl_m) nbc = *reinterpret_cast<const uint32_t*>(Cw + tile * T + obc);
     else nbc = *reinterpret_cast<const uint32_t*>(Bw + tile * T + obc);
     nh = *reinterpret_cast<const float4*>(cb + tile * ocj + oc);
+    if (xld) nx = *reinterpret_cast<const uint4*>(xrow + tile * T);
   };
   ss_f2 x[2] = {ss_f2{0.f, 0.f}, ss_f2{0.f, 0.f}};  // adjoint carried into the step after the tile
   ss_f2 dA[2] = {ss_f2{0.f, 0.f}, ss_f2{0.f, 0.f}};
@@ -1201,24 +1295,44 @@ __global__ __launch_bounds__(256) void selscan_bwd_sg_k(SelScanArgs a) {
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         auto upk = [&](uint32_t q) { return __uint_as_float(e ? (q & 0xffff0000u) : (q << 16)); };
-        const float u = upk(nu[hf]), v = upk(nr[hf]) + sbias, go = upk(ng[hf]), zz = upk(nz[hf]);
-        const float dl = a.softplus ? softplus_fast(v) : v;
+        const float u = upk(nu[hf]), go = upk(ng[hf]), zz = upk(nz[hf]);
         const float sg = sigmoid_fast(zz);
         const int tl = TH * hf + 2 * sp + e;
-        dlS[tl][sr] = dl;
-        duS[tl][sr] = dl * u;
+        if (!DTF) {
+          const float v = upk(nr[hf]) + sbias;
+          const float dl = a.softplus ? softplus_fast(v) : v;
+          dlS[tl][sr] = dl;
+          duS[tl][sr] = dl * u;
+          sdS[tl][sr] = a.softplus ? sigmoid_fast(v) : 1.f;
+        }
         dyS[tl][sr] = zb ? go * (zz * sg) : go;
         uS[tl][sr] = u;
-        sdS[tl][sr] = a.softplus ? sigmoid_fast(v) : 1.f;
         gzS[tl][sr] = zb ? go * sg * (1.f + zz * (1.f - sg)) : 0.f;
       }
     }
+    if (DTF && threadIdx.x < 2 * 32 * KS)
+      *reinterpret_cast<uint4*>(xS + 16 * xr + 8 * xh) = xld ? nx : make_uint4(0u, 0u, 0u, 0u);
     // B / C are the same for every lane: broadcast LDS reads in the step loops
     BCs[w][2 * bl_j][4 * bl_m + bl_n] = __uint_as_float(nbc << 16);
     BCs[w][2 * bl_j + 1][4 * bl_m + bl_n] = __uint_as_float(nbc & 0xffff0000u);
     const ss_f2 hst[2] = {ss_f2{nh.x, nh.y}, ss_f2{nh.z, nh.w}};
     __syncthreads();
     if (tile > 0) fetch(tile - 1);
+    if (DTF) {
+      f32x4 acc = zero4();
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) acc = mfma16(wf[ks], frag_tr(xS, 16, 32 * ks, 0), acc);
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) {
+        const int ch = 16 * w + 4 * g16 + r4;
+        const float v = acc[r4] + bias4[r4];
+        const float dl = a.softplus ? softplus_fast(v) : v;
+        dlS[li][ch] = dl;
+        duS[li][ch] = dl * uS[li][ch];
+        sdS[li][ch] = a.softplus ? sigmoid_fast(v) : 1.f;
+      }
+      __syncthreads();  // every wave's channels of the tile are in dlS / duS / sdS
+    }
     auto ldB = [&](int t, ss_f2 (&o)[2]) {
       const float4 q = *reinterpret_cast<const float4*>(&BCs[w][t][0]);
       o[0] = ss_f2{q.x, q.y};
@@ -1396,14 +1510,31 @@ static bool use_bwd_sg(const SelScanArgs& a) {
   return a.carry_t == SGB_T && sg_shape_ok(a) && a.vecg && a.L % SGB_T == 0 && a.nct == a.L / SGB_T && off32;
 }
 int selscan_bwd_kc(const SelScanArgs& a) { return use_bwd_sg(a) ? 64 : SB_KC; }
+// fused dt_proj (DTF): the forward walk with 16-step carries (so the backward is the sequential kernel too), a dt_rank
+// the 4-step MFMA chain covers, 16-B x_dbl / W_dt rows
+bool selscan_dt_fusable(const SelScanArgs& a) {
+  return use_fwd_sg(a) && a.L % SGB_T == 0 && a.R > 0 && a.R % 8 == 0 && a.R <= DTF_RMAX && a.sdtx % 8 == 0 &&
+         (uintptr_t)a.dtx_ % 16 == 0 && (uintptr_t)a.dtw_ % 16 == 0;
+}
 bool selscan_bwd_sequential(const SelScanArgs& a) { return use_bwd_sg(a); }
 
 hipError_t launch_selscan_fwd(const SelScanArgs& a, hipStream_t st) {
   const int64_t rows = (int64_t)a.B * a.D;
   dim3 grid((unsigned)((rows + 3) / 4)), block(256);
   if (a.carries && a.nct != (a.L + a.carry_t - 1) / a.carry_t) return hipErrorInvalidValue;
+  if (a.dtw_) {  // fused dt_proj: the wave-per-state-group walk only
+    if (!selscan_dt_fusable(a)) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)(a.B * (a.D / 64)));
+    switch ((a.R + 31) / 32) {
+      case 1: hipLaunchKernelGGL(selscan_fwd_sg_k<1>, grid, dim3(256), 0, st, a); break;
+      case 2: hipLaunchKernelGGL(selscan_fwd_sg_k<2>, grid, dim3(256), 0, st, a); break;
+      case 3: hipLaunchKernelGGL(selscan_fwd_sg_k<3>, grid, dim3(256), 0, st, a); break;
+      default: hipLaunchKernelGGL(selscan_fwd_sg_k<4>, grid, dim3(256), 0, st, a); break;
+    }
+    return hipGetLastError();
+  }
   if (use_fwd_sg(a)) {
-    hipLaunchKernelGGL(selscan_fwd_sg_k, dim3((unsigned)(a.B * (a.D / 64))), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(selscan_fwd_sg_k<0>, dim3((unsigned)(a.B * (a.D / 64))), dim3(256), 0, st, a);
     return hipGetLastError();
   }
   if (a.carry_t != SB_T) return hipErrorInvalidValue;  // the time-parallel forward saves per 512-step tile
@@ -1418,8 +1549,17 @@ hipError_t launch_selscan_bwd(const SelScanArgs& a, hipStream_t st) {
       a.nct != (a.L + a.carry_t - 1) / a.carry_t)
     return hipErrorInvalidValue;
   if (a.pacc && !use_bwd_sg(a)) return hipErrorInvalidValue;  // only the sequential kernel adds into partials
-  if (use_bwd_sg(a)) {
-    hipLaunchKernelGGL(selscan_bwd_sg_k, dim3((unsigned)(a.B * (a.D / 64))), dim3(256), 0, st, a);
+  if (a.dtw_) {
+    if (!use_bwd_sg(a) || !selscan_dt_fusable(a)) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)(a.B * (a.D / 64)));
+    switch ((a.R + 31) / 32) {
+      case 1: hipLaunchKernelGGL(selscan_bwd_sg_k<1>, grid, dim3(256), 0, st, a); break;
+      case 2: hipLaunchKernelGGL(selscan_bwd_sg_k<2>, grid, dim3(256), 0, st, a); break;
+      case 3: hipLaunchKernelGGL(selscan_bwd_sg_k<3>, grid, dim3(256), 0, st, a); break;
+      default: hipLaunchKernelGGL(selscan_bwd_sg_k<4>, grid, dim3(256), 0, st, a); break;
+    }
+  } else if (use_bwd_sg(a)) {
+    hipLaunchKernelGGL(selscan_bwd_sg_k<0>, dim3((unsigned)(a.B * (a.D / 64))), dim3(256), 0, st, a);
   } else {
     dim3 grid((a.D + SB_KC - 1) / SB_KC, a.B), block(64 * SB_W);
     const bool v = a.dtype == kBF16 && a.vec && a.vecbc && a.vecg && (!a.z_ || a.vecz) && a.L % 8 == 0;

@@ -240,10 +240,15 @@ class _Mamba1InnerFn(torch.autograd.Function):
         co2 = _flat(conv_out)
         Wx, Wdt = grad_accum.cached_cast(W_x, cd), grad_accum.cached_cast(W_dt, cd)  # once per optimizer step
         x_dbl = _mm_cm(Wx, co2)                                             # (R+2N, b*l)
-        delta = _mm_cm(Wdt, x_dbl[:R])                                      # (di, b*l)
         Bm = _cm(x_dbl[R:R + N], b, l).unsqueeze(1)                         # (b,1,N,l)
         Cm = _cm(x_dbl[R + N:], b, l).unsqueeze(1)
-        y, carries, _ = ops.selscan_fwd(conv_out, _cm(delta, b, l), A, Bm, Cm, D, z, dt_bias, True)
+        if _dt_fused_ok(b, l, di, N, Wdt, x_dbl, conv_out, z):
+            # dt_proj inside the scan walk (MFMA per 16-step tile): delta is never written or re-read
+            delta = None
+            y, carries, _ = ops.selscan_fwd_dt(conv_out, Wdt, x_dbl[:R], A, Bm, Cm, D, z, dt_bias, True)
+        else:
+            delta = _mm_cm(Wdt, x_dbl[:R])                                  # (di, b*l)
+            y, carries, _ = ops.selscan_fwd(conv_out, _cm(delta, b, l), A, Bm, Cm, D, z, dt_bias, True)
         ctx.save_for_backward(xz, w2, conv_b, Wx, Wdt, dt_bias, A, D, conv_out, x_dbl, delta, carries)
         ctx.meta = (b, l, conv_w.shape, W_x.dtype, W_dt.dtype)
         ctx.wparams = (W_x, W_dt)  # the parameters themselves (native weight gradients accumulate into .grad)
@@ -271,11 +276,17 @@ class _Mamba1InnerFn(torch.autograd.Function):
         # per micro-step that reduction is a zero fill, two batch sums, casts and three small gradient adds
         d_s = (grad_accum.deferred(ctx.pkey, "selscan_small", (b * di * (N + 2),), xz.device, force=True)
                if ctx.pkey is not None else None)
-        du, ddelta, dA, dB, dC, dD, dz, ddt_bias = ops.selscan_bwd_into(
-            _cm(dy2.contiguous() if dy2.stride(-1) != 1 else dy2, b, l), conv_out, _cm(delta, b, l), A,
-            Bm, Cm, D, z, dt_bias, carries, True,
-            dxz3[:, di:], _cm(dx_dbl[R:R + N], b, l).unsqueeze(1), _cm(dx_dbl[R + N:], b, l).unsqueeze(1),
-            *(d_s or (None, 0)))
+        dyc = dy2.contiguous() if dy2.stride(-1) != 1 else dy2
+        outs = (dxz3[:, di:], _cm(dx_dbl[R:R + N], b, l).unsqueeze(1), _cm(dx_dbl[R + N:], b, l).unsqueeze(1),
+                *(d_s or (None, 0)))
+        if delta is None:  # fused dt_proj forward: the backward walk recomputes delta the same way
+            if dyc.data_ptr() % 16 or dyc.stride(0) % 8:
+                dyc = dyc.contiguous().clone()
+            du, ddelta, dA, dB, dC, dD, dz, ddt_bias = ops.selscan_bwd_dt_into(
+                _cm(dyc, b, l), conv_out, Wdt, x_dbl[:R], A, Bm, Cm, D, z, dt_bias, carries, True, *outs)
+        else:
+            du, ddelta, dA, dB, dC, dD, dz, ddt_bias = ops.selscan_bwd_into(
+                _cm(dyc, b, l), conv_out, _cm(delta, b, l), A, Bm, Cm, D, z, dt_bias, carries, True, *outs)
         nz = lambda t: t if t.numel() else None  # noqa: E731  (empty: deferred to the sync micro-step)
         dA, dD, ddt_bias = nz(dA), nz(dD), nz(ddt_bias)
         dd2 = _flat(ddelta)
@@ -293,6 +304,25 @@ class _Mamba1InnerFn(torch.autograd.Function):
         _, dw, db = ops.conv1d_cf_bwd(x, w2, conv_b, _cm(dco2, b, l), True, dxz3[:, :di])
         return (dxz, dw.reshape(wshape).to(w2.dtype), db.to(conv_b.dtype) if conv_b is not None else None,
                 dWx, dWdt, ddt_bias, dA, dD, None, None, None)
+
+
+def _dt_fused_ok(b, l, di, N, Wdt, x_dbl, conv_out, z) -> bool:
+    """dt_proj fused into the selective-scan walk (csrc/kernels/selective_scan.hip, DTF; selscan_dt_fusable mirrored
+    here): the wave-per-state-group kernels (bf16, d_state 16, 64-channel groups, b * di >= 32768, l % 16 == 0) and a
+    dt_rank the 4-step MFMA chain covers.  Opt-in (MAMBA_AMD_M1_DT_FUSED=1): it removes the delta GEMM (53 us per
+    280M layer) and the saved (b, di, l) delta (12 GB of activations per 64k-token micro-batch at Mamba-1 280M), but
+    the per-tile MFMA + extra barrier costs the forward walk 34 us and the backward walk 40 us, so the step is 0.5%
+    slower (profiles/r5/m1_dt_fused_ab.txt).  Worth it where activation memory, not time, is the limit."""
+    import os
+    R = Wdt.shape[1]
+    if os.environ.get("MAMBA_AMD_M1_DT_FUSED", "0") != "1":
+        return False
+    zok = z is None or (z.stride(0) % 8 == 0 and z.stride(1) % 8 == 0 and z.data_ptr() % 16 == 0)
+    return (conv_out.dtype == torch.bfloat16 and x_dbl.dtype == torch.bfloat16 and Wdt.dtype == torch.bfloat16
+            and Wdt.is_contiguous() and N == 16 and di % 64 == 0 and l % 16 == 0 and b * di >= 32768
+            and 0 < R <= 128 and R % 8 == 0 and x_dbl.stride(1) == 1 and x_dbl.stride(0) % 8 == 0
+            and x_dbl.data_ptr() % 16 == 0 and Wdt.data_ptr() % 16 == 0 and conv_out.stride(0) % 8 == 0
+            and conv_out.stride(1) % 8 == 0 and conv_out.data_ptr() % 16 == 0 and zok)
 
 
 def mamba1_inner_ref(xz3, conv_w, conv_b, W_x, W_dt, dt_bias, A, D):

@@ -1177,6 +1177,127 @@ def test_selective_scan_sequential_backward(cuda, monkeypatch, b, d, L, G, with_
             assert rel(a_, b_) < 1e-2, (nm, rel(a_, b_))
 
 
+@pytest.mark.parametrize("b,d,L,Rk,with_z", [(32, 1536, 256, 48, True), (32, 1024, 128, 64, False),
+                                              (24, 2048, 64, 96, True), (64, 512, 64, 16, True)])
+def test_selective_scan_fused_dt(cuda, b, d, L, Rk, with_z):
+    """dt_proj fused into the sequential scan walks (selscan_fwd_dt / selscan_bwd_dt_into, kernels/selective_scan.hip
+    DTF): delta_raw = W_dt x_dbl[:R] per 16-step tile on MFMA inside the kernels, in the Mamba-1 channel-major layout
+    (u, z as (d, b, l) memory; B / C / x as rows of one x_dbl).  Forward and every gradient vs the fp32 reference
+    with the fp32 delta, and vs the unfused kernels fed the bf16-rounded delta; dt_rank 16 exercises the zero-padded
+    K-step."""
+    torch.manual_seed(12)
+    n = 16
+    ops = torch.ops.mamba_amd
+    M = b * L
+    cm = lambda t2: t2.view(t2.shape[0], b, L).permute(1, 0, 2)  # noqa: E731  (rows, b*L) -> (b, rows, L)
+    u2 = torch.randn(d, M, device=cuda).to(torch.bfloat16)
+    z2 = torch.randn(d, M, device=cuda).to(torch.bfloat16) if with_z else None
+    x_dbl = (torch.randn(Rk + 2 * n, M, device=cuda)).to(torch.bfloat16)
+    W = (torch.randn(d, Rk, device=cuda) * Rk ** -0.5).to(torch.bfloat16)
+    A = -torch.rand(d, n, device=cuda) * 4 - 0.1
+    D = torch.randn(d, device=cuda)
+    db = torch.randn(d, device=cuda) * 0.3 - 1.0
+    u, z = cm(u2), (cm(z2) if with_z else None)
+    Bm, Cm = cm(x_dbl[Rk:Rk + n]).unsqueeze(1), cm(x_dbl[Rk + n:]).unsqueeze(1)
+    d32 = W.float() @ x_dbl[:Rk].float()                       # (d, b*L) fp32 delta_raw
+    y, carries, last = ops.selscan_fwd_dt(u, W, x_dbl[:Rk], A, Bm, Cm, D, z, db, True)
+    assert carries.shape[2] == L // 16
+    y_u, car_u, _ = ops.selscan_fwd(u, cm(d32.to(torch.bfloat16)), A, Bm, Cm, D, z, db, True)
+    # fp32 reference with autograd for the gradients
+    leaves = [t.detach().float().clone().requires_grad_(True) for t in (u, cm(d32), A, Bm, Cm, D, db)]
+    zr = z.float() if with_z else None
+    y_ref = R.selective_scan_ref(leaves[0], leaves[1], leaves[2], leaves[3], leaves[4], leaves[5], z=zr,
+                                 delta_bias=leaves[6], delta_softplus=True)
+    assert rel(y, y_ref) < 2e-2, rel(y, y_ref)
+    assert rel(y, y_u) < 2e-2, rel(y, y_u)
+    go = torch.randn_like(y_ref)
+    y_ref.backward(go)
+    gob = go.to(torch.bfloat16)
+    go2 = torch.empty(d, M, device=cuda, dtype=torch.bfloat16)
+    cm(go2).copy_(gob)
+
+    def bwd(fused):
+        dz2 = torch.empty(d, M, device=cuda, dtype=torch.bfloat16)
+        dx = torch.empty(2 * n, M, device=cuda, dtype=torch.bfloat16)
+        outs = (cm(dz2) if with_z else torch.empty(0, device=cuda, dtype=torch.bfloat16),
+                cm(dx[:n]).unsqueeze(1), cm(dx[n:]).unsqueeze(1))
+        if fused:
+            return ops.selscan_bwd_dt_into(cm(go2), u, W, x_dbl[:Rk], A, Bm, Cm, D, z, db, carries, True, *outs)
+        return ops.selscan_bwd_into(cm(go2), u, cm(d32.to(torch.bfloat16)), A, Bm, Cm, D, z, db, car_u, True, *outs)
+
+    gf, gu = bwd(True), bwd(False)
+    names = ["du", "ddelta", "dA", "dB", "dC", "dD", "dz", "dbias"]
+    refs = [leaves[0].grad, leaves[1].grad, leaves[2].grad, leaves[3].grad, leaves[4].grad, leaves[5].grad,
+            None, leaves[6].grad]
+    for nm, a_, b_, r_ in zip(names, gf, gu, refs):
+        if not a_.numel():
+            continue
+        assert torch.isfinite(a_.float()).all(), nm
+        assert rel(a_, b_) < 3e-2, (nm, rel(a_, b_))
+        if r_ is not None:
+            assert rel(a_, r_) < 3e-2, (nm, rel(a_, r_))
+    # determinism: the backward's recomputed delta is the forward's (same operands and instruction sequence)
+    gf2 = bwd(True)
+    for nm, a_, b_ in zip(names, gf, gf2):
+        if a_.numel():
+            assert torch.equal(a_, b_), nm
+
+
+def test_mamba1_fused_dt_model(cuda, monkeypatch):
+    """A Mamba-1 model at a shape that takes the fused dt_proj scan (b * d_inner >= 32768; opt-in
+    MAMBA_AMD_M1_DT_FUSED=1): loss and every parameter gradient vs the fp32 reference ops and vs the unfused path
+    (MAMBA_AMD_M1_DT_FUSED=0); a spy checks the fused op ran."""
+    from mamba_distributed_amd import LMHeadModel, MambaConfig
+    calls = []
+    ops = torch.ops.mamba_amd
+    orig = ops.selscan_fwd_dt
+
+    class Spy:
+        def __getattr__(self, k):
+            if k == "selscan_fwd_dt":
+                def f(*a):
+                    calls.append(1)
+                    return orig(*a)
+                return f
+            return getattr(ops, k)
+    from mamba_distributed_amd.ops import _ext
+    real = _ext.ops
+    monkeypatch.setattr(_ext, "ops", lambda: Spy())
+    torch.manual_seed(0)
+    cfg = MambaConfig(d_model=768, n_layer=2, vocab_size=4096, ssm_cfg={"layer": "Mamba1"})
+    m = LMHeadModel(cfg, device=cuda)
+    sharpen_logits(m)
+    x = torch.randint(0, 4096, (32, 256), device=cuda)
+    y = torch.randint(0, 4096, (32, 256), device=cuda)
+
+    def lossgrad(force_ref=False, fused=True):
+        os.environ["MAMBA_AMD_M1_DT_FUSED"] = "1" if fused else "0"
+        if force_ref:
+            os.environ["MAMBA_AMD_FORCE_REFERENCE"] = "1"
+        try:
+            m.zero_grad(set_to_none=True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                _, loss = m(x, y)
+            loss.backward()
+            return loss.item(), {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+        finally:
+            os.environ.pop("MAMBA_AMD_FORCE_REFERENCE", None)
+            os.environ.pop("MAMBA_AMD_M1_DT_FUSED", None)
+
+    ln, gn = lossgrad()
+    assert len(calls) == cfg.n_layer, calls
+    lu, gu = lossgrad(fused=False)
+    assert len(calls) == cfg.n_layer
+    monkeypatch.setattr(_ext, "ops", real)
+    lr, gr = lossgrad(force_ref=True)
+    check_loss(ln, lr, cfg.vocab_size)
+    assert abs(ln - lu) < 2e-3 * abs(lu), (ln, lu)
+    bad = {n: rel(gn[n], gr[n]) for n in gr if rel(gn[n], gr[n]) > 5e-2}
+    assert not bad, bad
+    bad = {n: rel(gn[n], gu[n]) for n in gu if rel(gn[n], gu[n]) > 3e-2}
+    assert not bad, bad
+
+
 @pytest.mark.parametrize("b,L,H,G,N,with_init", [(2, 200, 8, 1, 128, True), (1, 64, 4, 2, 64, False),
                                                  (3, 1030, 24, 1, 128, False)])
 def test_ssd_fp32_native_forward(cuda, b, L, H, G, N, with_init):
