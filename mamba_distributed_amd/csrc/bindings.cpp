@@ -1079,6 +1079,14 @@ Tensor colsum(Tensor part) {
   return out;
 }
 
+// batched late column sums (ops/grad_accum.py::flush_late): tab = uint8 (n, 80) LateCol rows
+void late_colsum(Tensor tab, int64_t n, int64_t nblk, int64_t ntile) {
+  TORCH_CHECK(tab.is_cuda() && tab.scalar_type() == at::kByte && tab.is_contiguous() && tab.numel() == n * 80,
+              "late_colsum: contiguous uint8 CUDA table of n 80-byte rows");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(tab.device());
+  HIPCHK(mamba_amd::launch_late_colsum(tab.data_ptr(), (int)n, (int)nblk, (int)ntile, cur_stream()));
+}
+
 // ---- native optimizer step (ops/optim.py): tab = uint8 OptSeg table, blk = int64 (nblk, 2) chunk table ----
 static void check_opt_tables(const Tensor& tab, const Tensor& blk) {
   TORCH_CHECK(tab.is_cuda() && tab.scalar_type() == at::kByte && tab.is_contiguous() && tab.numel() % 64 == 0,
@@ -1258,6 +1266,7 @@ TORCH_LIBRARY(mamba_amd, m) {
   m.def("gp_reduce(Tensor part, Tensor(a!) out, bool accumulate=False) -> ()");
   m.def("transpose_bf16(Tensor X) -> Tensor");
   m.def("colsum(Tensor(a!) part) -> Tensor");
+  m.def("late_colsum(Tensor tab, int n, int nblk, int ntile) -> ()");
   m.def("opt_grad_norm(Tensor tab, Tensor blk, float max_norm, float divisor) -> Tensor");
   m.def("opt_adamw(Tensor tab, Tensor blk, Tensor? gscale, float b1, float b2, float eps) -> ()");
   m.def("opt_chunk() -> int", &opt_chunk);
@@ -1282,6 +1291,7 @@ TORCH_LIBRARY_IMPL(mamba_amd, CUDA, m) {
   m.impl("gp_reduce", &gp_reduce);
   m.impl("transpose_bf16", &transpose_bf16);
   m.impl("colsum", &colsum);
+  m.impl("late_colsum", &late_colsum);
   m.impl("opt_grad_norm", &opt_grad_norm);
   m.impl("opt_adamw", &opt_adamw);
   m.impl("add_rmsnorm_bwd", &add_rmsnorm_bwd);

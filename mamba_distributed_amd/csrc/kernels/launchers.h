@@ -28,6 +28,8 @@ inline int split_k_count(int64_t tiles, int64_t P, int64_t Q, int64_t K, int64_t
 // optimizer step), and dw == nullptr skips the final column sum (deferred to the sync micro-step).
 // deterministic column sum of a (nrows, ncols) fp32 partial matrix (norm.hip)
 hipError_t launch_colsum(float* part, int nrows, int ncols, float* out, hipStream_t st);  // clobbers part
+// batched column sums into parameter gradients (kernels/norm.hip LateCol table rows, 80 bytes each)
+hipError_t launch_late_colsum(const void* tab, int n, int nblk, int ntile, hipStream_t st);
 
 // ---- norm.hip -------------------------------------------------------------------------------
 hipError_t launch_add_rmsnorm_fwd(const void* x, int xdt, int64_t sx, const void* res, int rdt, int64_t sr,

@@ -332,6 +332,98 @@ hipError_t launch_colsum(float* part, int nrows, int ncols, float* out, hipStrea
 }
 
 // ------------------------------------------------------------------------------------------
+// Batched late column sums (ops/grad_accum.py::late_colsum): at the sync micro-step every deferred parameter-gradient
+// partial block of the backward (norm weights, conv taps + bias, A_log / D / dt_bias) is reduced by ONE pair of
+// launches after the backward instead of two launches per block inside it -- at one micro-batch per optimizer step
+// (the 8-GPU per-rank regime) those ~4 small launch pairs per layer were 1.6% of the step.  The column sums go
+// straight into the parameters' .grad storage.  Host table row (ops/grad_accum.py _LATE_DTYPE, 64 bytes):
+struct LateCol {
+  float* part;               // (nrows, ncols) fp32 partial rows (stage 1 overwrites the first row of each split)
+  float* dst[3];             // destinations (see mode)
+  int nrows, ncols, R, RS;   // rows per split, splits
+  int G, mode, acc, pad0;    // mode 0: dst0[j]; 1: j = o G + i -> i < G - 1 ? dst0[o (G - 1) + i] : dst1[o]
+                             // (conv taps | bias); 2: j = o G + i -> dst[o][i] (A | D | bias); acc bit k: dst k +=
+  int blk0, tile0;           // first stage-1 block / stage-2 tile of this entry
+  int pad1, pad2;
+};
+static_assert(sizeof(LateCol) == 80, "late column-sum table row layout is shared with the host");
+
+__device__ __forceinline__ int late_find(const LateCol* __restrict__ t, int n, int key, bool by_tile) {
+  int lo = 0, hi = n - 1;  // last entry whose first index <= key
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if ((by_tile ? t[mid].tile0 : t[mid].blk0) <= key) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+// stage 1: block = (entry, column tile, split): the split's R rows of 64 columns, summed in a fixed order, written
+// over the split's first row
+__global__ __launch_bounds__(256) void late_colsum_split_k(const LateCol* __restrict__ tab, int n) {
+  __shared__ float red[4][65];
+  __shared__ int ent;
+  if (threadIdx.x == 0) ent = late_find(tab, n, blockIdx.x, false);
+  __syncthreads();
+  const LateCol e = tab[ent];
+  const int tiles = (e.ncols + 63) / 64, rel = blockIdx.x - e.blk0;
+  const int tile = rel % tiles, sp = rel / tiles;
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = tile * 64 + cl;
+  const int r0 = sp * e.R, r1 = min(r0 + e.R, e.nrows);
+  float s0 = 0.f, s1 = 0.f;
+  if (c < e.ncols) {
+    int r = r0 + rg;
+    for (; r + 4 < r1; r += 8) {
+      s0 += e.part[(int64_t)r * e.ncols + c];
+      s1 += e.part[(int64_t)(r + 4) * e.ncols + c];
+    }
+    if (r < r1) s0 += e.part[(int64_t)r * e.ncols + c];
+  }
+  red[rg][cl] = s0 + s1;
+  __syncthreads();
+  if (rg == 0 && c < e.ncols) e.part[(int64_t)r0 * e.ncols + c] = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
+}
+
+// stage 2: block = (entry, column tile): the RS split sums in order, then the destination mapping
+__global__ __launch_bounds__(256) void late_colsum_final_k(const LateCol* __restrict__ tab, int n) {
+  __shared__ float red[4][65];
+  __shared__ int ent;
+  if (threadIdx.x == 0) ent = late_find(tab, n, blockIdx.x, true);
+  __syncthreads();
+  const LateCol e = tab[ent];
+  const int tile = blockIdx.x - e.tile0;
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = tile * 64 + cl;
+  float s = 0.f;
+  if (c < e.ncols)
+    for (int k = rg; k < e.RS; k += 4) s += e.part[(int64_t)k * e.R * e.ncols + c];
+  red[rg][cl] = s;
+  __syncthreads();
+  if (rg != 0 || c >= e.ncols) return;
+  const float t = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
+  int k = 0;
+  int64_t off = c;
+  if (e.mode == 1) {
+    const int o = c / e.G, i = c % e.G;
+    if (i < e.G - 1) { k = 0; off = (int64_t)o * (e.G - 1) + i; } else { k = 1; off = o; }
+  } else if (e.mode == 2) {
+    k = c / e.G;
+    off = c % e.G;
+  }
+  float* d = e.dst[k];
+  if (d == nullptr) return;
+  d[off] = ((e.acc >> k) & 1) ? d[off] + t : t;
+}
+
+hipError_t launch_late_colsum(const void* tab, int n, int nblk, int ntile, hipStream_t st) {
+  if (n <= 0 || nblk <= 0 || ntile <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(late_colsum_split_k, dim3(nblk), dim3(256), 0, st, (const LateCol*)tab, n);
+  MAMBA_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(late_colsum_final_k, dim3(ntile), dim3(256), 0, st, (const LateCol*)tab, n);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
 // gated RMSNorm: y = RMSNorm_group(x * silu(z)) * w   (NBG = norm_before_gate=false)
 //                y = RMSNorm_group(x) * w * silu(z)    (NBG = true)
 template <int NCH, bool NBG>

@@ -66,6 +66,12 @@ def accumulation_scope(defer_reduce: bool = True):
             for ent in _bufs.values():  # buffers are kept (reused next step); their contents are dead
                 ent[2] = False
             join_side()
+            if _late:  # a loop that queued late column sums without flushing them (parallel/microbatch.py flushes)
+                if ok:
+                    flush_late()
+                else:
+                    _late.clear()
+            set_late(False)
             if ok and stuck:
                 raise RuntimeError(
                     f"grad_accum: deferred gradient partials ({sorted(set(stuck))}) were accumulated on no-sync "
@@ -199,6 +205,119 @@ def in_scope() -> bool:
 
 def direct() -> bool:
     return _direct and _scope_depth > 0
+
+
+# ---- late column sums: the sync micro-step's deferred partials reduced by one batched launch pair ----------------
+# On the sync micro-step each deferred partial block (norm weights, conv taps + bias, A_log / D / dt_bias) used to be
+# column-summed by its op -- two small launches per block, ~4 blocks per layer, 3.4 ms of a 209 ms step at one
+# micro-batch per optimizer step (profiles/r5/accum1_native_adamw_table.md).  With ``set_late(True)`` (the micro-batch
+# loop, parallel/microbatch.py, for the native reducer or a single process; never under torch DDP, whose hooks would
+# all-reduce the missing gradients) the ops instead leave the partials in their buffers, queue them here and return
+# no gradient; ``flush_late`` reduces every queued block with ONE pair of launches (csrc/kernels/norm.hip
+# late_colsum) straight into the parameters' .grad -- before the native reducer launches its held last bucket
+# (the small parameters, parallel/reducer.py) or, single process, before the micro-batch loop returns.
+_late_on = False
+_late: List[tuple] = []       # (part (rows, cols) fp32, mode, G, [destination params])
+_late_tab: Dict[int, tuple] = {}  # device index -> (key, device table, n, nblk, ntile)
+_LATE_ROWS = 64               # rows per stage-1 split
+
+try:
+    import numpy as _np
+    _LATE_DTYPE = _np.dtype([("part", "<u8"), ("d0", "<u8"), ("d1", "<u8"), ("d2", "<u8"), ("nrows", "<i4"),
+                             ("ncols", "<i4"), ("R", "<i4"), ("RS", "<i4"), ("G", "<i4"), ("mode", "<i4"),
+                             ("acc", "<i4"), ("pad0", "<i4"), ("blk0", "<i4"), ("tile0", "<i4"), ("pad1", "<i4"),
+                             ("pad2", "<i4")])
+    assert _LATE_DTYPE.itemsize == 80
+except ImportError:  # pragma: no cover
+    _np = None
+
+
+def set_late(enabled: bool) -> None:
+    global _late_on
+    _late_on = bool(enabled)
+
+
+def late_ok(*params) -> bool:
+    """The sync micro-step may queue ``params``' partials for ``flush_late`` (fp32 parameters whose .grad, if any, is
+    fp32 contiguous; MAMBA_AMD_LATE_REDUCE=0 turns it off)."""
+    import os
+    if not (_late_on and _scope_depth > 0 and not _direct and _np is not None):
+        return False
+    if os.environ.get("MAMBA_AMD_LATE_REDUCE", "1") == "0":
+        return False
+    for p in params:
+        if p is None:
+            continue
+        if not (isinstance(p, torch.Tensor) and p.is_leaf and p.requires_grad and p.dtype == torch.float32 and p.is_cuda):
+            return False
+        if p.grad is not None and (p.grad.dtype != torch.float32 or not p.grad.is_contiguous()):
+            return False
+    return True
+
+
+def late_colsum(part: torch.Tensor, mode: int, G: int, params) -> None:
+    """Queue the column sums of ``part`` (rows x cols after flattening the trailing dims) for ``flush_late``.
+    mode 0: params = [p], column j -> p.grad[j]; 1: [weight, bias], columns grouped by G = taps + 1 ([taps | bias]
+    per channel); 2: [p0, p1, p2], column o G + i -> p_o.grad[i] (None: skipped)."""
+    _late.append((part.reshape(part.shape[0], -1), int(mode), int(G), list(params)))
+
+
+def flush_late() -> None:
+    """Reduce every queued partial block into its parameters' .grad with one pair of launches (on the current
+    stream, which must be ordered after the backward that wrote the partials)."""
+    global _late
+    if not _late:
+        return
+    entries, _late = _late, []
+    from . import _ext
+    dev = entries[0][0].device
+    # destinations: add into an existing fp32 .grad, else store into fresh views of one flat buffer
+    need = []
+    seen = set()
+    for part, mode, G, ps in entries:
+        for p in ps:
+            if p is None:
+                continue
+            if id(p) in seen:
+                raise RuntimeError("grad_accum.flush_late: a parameter is the destination of two partial blocks")
+            seen.add(id(p))
+            if p.grad is None:
+                need.append(p)
+    if need:
+        flat = torch.empty(sum(p.numel() for p in need), device=dev, dtype=torch.float32)
+        o = 0
+        for p in need:
+            p.grad = flat[o:o + p.numel()].view_as(p)
+            o += p.numel()
+    fresh = {id(p) for p in need}
+    rows = []
+    key = []
+    blk = tile = 0
+    for part, mode, G, ps in entries:
+        nrows, ncols = part.shape
+        R = min(_LATE_ROWS, nrows)
+        RS = (nrows + R - 1) // R
+        tiles = (ncols + 63) // 64
+        d = [0, 0, 0]
+        acc = 0
+        for k, p in enumerate(ps):
+            if p is None:
+                continue
+            d[k] = p.grad.data_ptr()
+            if id(p) not in fresh:
+                acc |= 1 << k
+        rows.append((part.data_ptr(), d[0], d[1], d[2], nrows, ncols, R, RS, G, mode, acc, 0, blk, tile, 0, 0))
+        key.append((part.data_ptr(), d[0], d[1], d[2], nrows, ncols, G, mode, acc))
+        blk += tiles * RS
+        tile += tiles
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    key = tuple(key)
+    ent = _late_tab.get(idx)
+    if ent is None or ent[0] != key:
+        tab = _np.array(rows, dtype=_LATE_DTYPE)
+        t = torch.from_numpy(tab.view(_np.uint8).copy()).pin_memory().to(dev, non_blocking=True)
+        ent = _late_tab[idx] = (key, t, len(rows), blk, tile)
+    _ext.ops().late_colsum(ent[1], ent[2], ent[3], ent[4])
 
 
 # ---- bf16 weight images written by the native optimizer step (ops/optim.py) ----------------------------------

@@ -64,11 +64,17 @@ class _AddRMSNormFn(torch.autograd.Function):
         ops = _ext.ops()
         d = grad_accum.deferred(ctx.param, "rmsnorm", (ops.part_rows("add_rmsnorm", dy2.shape[0]), dy2.shape[1]),
                                 dy2.device) if ctx.needs_input_grad[1] else None
+        # sync micro-step: the weight-gradient partials go to the batched late column sum (grad_accum.flush_late)
+        late = d is not None and d[1] >= 3 and grad_accum.late_ok(ctx.param)
+        if late:
+            d = (d[0], d[1] - 2)
         dx, dres, dw = ops.add_rmsnorm_bwd(dy2, dr2, res_out, weight, rstd, ctx.x_dtype,
                                            res_dtype if res_dtype is not None else ctx.x_dtype,
                                            want_res and res_dtype != ctx.x_dtype, *(d or (None, 0)))
-        if dw.numel() == 0:  # deferred to the sync micro-step
+        if dw.numel() == 0:  # deferred to the sync micro-step / to the late column sum
             dw = None
+        if late:
+            grad_accum.late_colsum(d[0], 0, 0, [ctx.param])
         dx = dx.view(shape)
         dresidual = None
         if want_res:
@@ -121,10 +127,15 @@ class _GatedRMSNormFn(torch.autograd.Function):
         ops = _ext.ops()
         d = grad_accum.deferred(ctx.param, "gated_rmsnorm", (ops.part_rows("gated_rmsnorm", x2.shape[0]),
                                                              x2.shape[1]), x2.device)
+        late = d is not None and d[1] >= 3 and grad_accum.late_ok(ctx.param)
+        if late:
+            d = (d[0], d[1] - 2)
         dx, dz, dw = ops.gated_rmsnorm_bwd(_rows(dy), x2, z2, weight, rstd, ctx.group_size, ctx.nbg, None, None,
                                            *(d or (None, 0)))
         if dw.numel() == 0:
             dw = None
+        if late:
+            grad_accum.late_colsum(d[0], 0, 0, [ctx.param])
         return dx.view(ctx.shape), dz.view(ctx.shape), grad_accum.defer(ctx.param, dw), None, None, None
 
 

@@ -209,6 +209,12 @@ class _Mamba2InnerFn(torch.autograd.Function):
         # one tag for both conv kernels: their partial rows differ, so seq_idx appearing on only some micro-steps
         # of a step is refused by grad_accum.deferred instead of silently starting a second buffer
         d_c = grad_accum.deferred(pw, "conv_cl", (ops.part_rows(ck, b, l), conv_dim, w2.shape[1] + 1), dev)
+        # sync micro-step: leave the three partial blocks unreduced and queue them for the batched late column sum
+        # after the backward (ops/grad_accum.py::flush_late) instead of two launches each here
+        late = (d_n is not None and d_s is not None and d_c is not None and d_n[1] >= 3 and d_s[1] >= 3
+                and d_c[1] >= 3 and grad_accum.late_ok(pn, pA, pD, pdtb, pw, pb))
+        if late:
+            d_n, d_s, d_c = (d_n[0], d_n[1] - 2), (d_s[0], d_s[1] - 2), (d_c[0], d_c[1] - 2)
         # gated norm backward writes dz straight into its slice of d(zxbcdt)
         dy, _, dnorm_w = ops.gated_rmsnorm_bwd(dyn.reshape(b * l, di), y.view(b * l, di),
                                                z.flatten(0, 1), norm_w, rstd, di // ngroups, nbg,
@@ -236,6 +242,10 @@ class _Mamba2InnerFn(torch.autograd.Function):
         d = grad_accum.defer
         nz = lambda t: t if t.numel() else None  # noqa: E731  (empty = deferred to the sync micro-step)
         dw = nz(dw)
+        if late:
+            grad_accum.late_colsum(d_n[0], 0, 0, [pn])
+            grad_accum.late_colsum(d_s[0], 2, H, [pA, pD, pdtb])
+            grad_accum.late_colsum(d_c[0], 1, w2.shape[1] + 1, [pw, pb])
         if dz_full is not None:
             from .linear import register_zero_padded_grad
             register_zero_padded_grad(dz_full)

@@ -118,9 +118,13 @@ def run_micro_batches(model, next_batch: Callable, accum: int, compute_loss: Cal
             total = loss.detach().float() if total is None else total + loss.detach().float()
             if sync and reducer is not None:
                 reducer.arm()
+            if sync:
+                grad_accum.set_late(not _is_ddp(model))
             loss.backward()
         if reducer is not None:
             reducer.finish()
+        grad_accum.flush_late()
+        grad_accum.set_late(False)
         return total
     ddp = _is_ddp(model)
     main = torch.cuda.current_stream()
@@ -164,6 +168,10 @@ def run_micro_batches(model, next_batch: Callable, accum: int, compute_loss: Cal
         grad_accum.set_direct(k != accum - 1)
         if k == accum - 1 and reducer is not None:
             reducer.arm()
+        if k == accum - 1:
+            # the sync backward leaves its small parameter-gradient partials for ONE batched column sum after it
+            # (ops/grad_accum.py::flush_late; not under torch DDP, whose hooks would reduce the missing gradients)
+            grad_accum.set_late(not ddp)
         with torch.cuda.stream(streams[k]):
             losses[k].backward()
         if nxt < accum and not early:
@@ -173,6 +181,8 @@ def run_micro_batches(model, next_batch: Callable, accum: int, compute_loss: Cal
     main.wait_stream(other)
     if reducer is not None:
         reducer.finish()
+    grad_accum.flush_late()
+    grad_accum.set_late(False)
     total = losses[0].detach().float()
     for l in losses[1:]:
         total = total + l.detach().float()

@@ -28,6 +28,8 @@ import torch.distributed as dist
 
 
 class GradReducer:
+    SMALL_NUMEL = 1 << 17
+
     def __init__(self, module: torch.nn.Module, process_group=None, bucket_cap_mb: float = 100.0,
                  broadcast_params: bool = True, comm_dtype: str = "fp32"):
         self.group = process_group
@@ -39,15 +41,26 @@ class GradReducer:
         assert params, "no trainable parameters"
         dtypes = {p.dtype for p in params}
         assert dtypes == {torch.float32}, f"GradReducer keeps fp32 gradients for fp32 parameters, got {dtypes}"
-        order = list(reversed(params))
-        total = sum(p.numel() for p in order)
+        # the small parameters (norm weights, conv taps, A_log / D / dt_bias: < SMALL_NUMEL elements each) go last, in
+        # buckets of their own that are HELD until finish(): on the sync micro-step their gradients come from the
+        # batched late column sum after the backward (ops/grad_accum.py::flush_late), so their hooks fire before the
+        # gradients exist.  A few MB per model, all-reduced once at the end.
+        order = [p for p in reversed(params) if p.numel() >= self.SMALL_NUMEL]
+        small = [p for p in reversed(params) if p.numel() < self.SMALL_NUMEL]
+        total = sum(p.numel() for p in params)
         self.flat = torch.zeros(total, dtype=torch.float32, device=params[0].device)
         cap = max(1, int(bucket_cap_mb * 2**20 / 4))
         self.buckets: List[tuple] = []  # (start, end, n_params)
         self._bucket_of: Dict[int, int] = {}
         self._offset: Dict[int, int] = {}
         off, start, count = 0, 0, 0
-        for p in order:
+        self._held_from = None
+        for p in order + small:
+            if p is (small[0] if small else None) and count:
+                self.buckets.append((start, off, count))  # bucket boundary before the held small parameters
+                start, count = off, 0
+            if p is (small[0] if small else None):
+                self._held_from = len(self.buckets)
             self._offset[id(p)] = off
             self._bucket_of[id(p)] = len(self.buckets)
             off += p.numel()
@@ -57,6 +70,8 @@ class GradReducer:
                 start, count = off, 0
         if count:
             self.buckets.append((start, off, count))
+        if self._held_from is None:
+            self._held_from = len(self.buckets)
         self._params = params
         for p in params:
             self._attach(p)
@@ -106,7 +121,7 @@ class GradReducer:
         if not self._armed:
             return
         self._left[self._bucket_of[id(p)]] -= 1
-        while self._next < len(self.buckets) and self._left[self._next] == 0:
+        while self._next < self._held_from and self._left[self._next] == 0:
             s, e, _ = self.buckets[self._next]
             self._works.append(self._all_reduce(self.flat[s:e]))
             self._next += 1
@@ -142,7 +157,9 @@ class GradReducer:
         if not self._armed:
             return
         t0 = self._stamp()
-        while self._next < len(self.buckets):  # parameters that got no gradient this step
+        from ..ops import grad_accum
+        grad_accum.flush_late()  # the held small-parameter gradients (late column sums), on this stream
+        while self._next < len(self.buckets):  # held buckets; parameters that got no gradient this step
             s, e, _ = self.buckets[self._next]
             self._works.append(self._all_reduce(self.flat[s:e]))
             self._next += 1

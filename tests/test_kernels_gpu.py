@@ -1177,6 +1177,55 @@ def test_selective_scan_sequential_backward(cuda, monkeypatch, b, d, L, G, with_
             assert rel(a_, b_) < 1e-2, (nm, rel(a_, b_))
 
 
+@pytest.mark.parametrize("preset", [False, True])
+def test_late_colsum(cuda, preset):
+    """The batched late column sum (ops/grad_accum.py::flush_late, kernels/norm.hip late_colsum_*): the three
+    destination layouts (plain, conv taps | bias per channel, A | D | bias), stored into fresh .grad views or added
+    into existing gradients; against fp64 column sums, and bitwise repeatable."""
+    from mamba_distributed_amd.ops import grad_accum
+    g = torch.Generator(device=cuda).manual_seed(3)
+    P = lambda *s: torch.nn.Parameter(torch.zeros(*s, device=cuda))  # noqa: E731
+    pn, pA, pD, pb_, pw, pb = P(1536), P(24), P(24), P(24), P(1792, 1, 4), P(1792)
+    parts = [torch.randn(2048, 1536, device=cuda, generator=g), torch.randn(1024, 3, 24, device=cuda, generator=g),
+             torch.randn(300, 1792, 5, device=cuda, generator=g), torch.randn(7, 1536, device=cuda, generator=g)]
+    pn2 = P(1536)
+    sums = [t.double().sum(0) for t in parts]
+    base = {}
+    for p in (pn, pA, pD, pb_, pw, pb, pn2):
+        if preset:
+            p.grad = torch.randn(p.shape, device=cuda, generator=g)
+            base[id(p)] = p.grad.clone()
+
+    def run():
+        work = [t.clone() for t in parts]
+        with grad_accum.accumulation_scope():
+            grad_accum.set_late(True)
+            grad_accum.late_colsum(work[0], 0, 0, [pn])
+            grad_accum.late_colsum(work[1], 2, 24, [pA, pD, pb_])
+            grad_accum.late_colsum(work[2], 1, 5, [pw, pb])
+            grad_accum.late_colsum(work[3], 0, 0, [pn2])
+            grad_accum.flush_late()
+        torch.cuda.synchronize()
+        return [p.grad.clone() for p in (pn, pA, pD, pb_, pw, pb, pn2)]
+
+    got = run()
+    want = [sums[0], sums[1][0], sums[1][1], sums[1][2], sums[2][:, :4].reshape(1792, 1, 4), sums[2][:, 4], sums[3]]
+    for i, (a_, w_) in enumerate(zip(got, want)):
+        p = (pn, pA, pD, pb_, pw, pb, pn2)[i]
+        ref = w_ + (base[id(p)].double() if preset else 0)
+        assert a_.shape == p.shape
+        assert ((a_.double() - ref).abs().max() / (ref.abs().max() + 1e-9)).item() < 1e-5, i
+    if preset:
+        for p in (pn, pA, pD, pb_, pw, pb, pn2):
+            p.grad = base[id(p)].clone()
+    else:
+        for p in (pn, pA, pD, pb_, pw, pb, pn2):
+            p.grad = None
+    again = run()
+    for a_, b_ in zip(got, again):
+        assert torch.equal(a_, b_)
+
+
 @pytest.mark.parametrize("b,d,L,Rk,with_z", [(32, 1536, 256, 48, True), (32, 1024, 128, 64, False),
                                               (24, 2048, 64, 96, True), (64, 512, 64, 16, True)])
 def test_selective_scan_fused_dt(cuda, b, d, L, Rk, with_z):
