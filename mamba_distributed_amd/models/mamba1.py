@@ -164,6 +164,9 @@ def _wgrad_native(p, dY, X, dy_cm, x_cm):
           and dY.data_ptr() % 16 == 0 and X.data_ptr() % 16 == 0)
     if not ok:
         return False, None
+    if grad_accum.sync_accumulable(p):  # sync micro-step, gradient in place: add into it (ops/grad_accum.py)
+        _ext.ops().gemm_wgrad_cm(dY, X, p.grad, True, dy_cm, x_cm)
+        return True, None
     if (grad_accum.accumulable(p) and p.grad.dtype == torch.float32 and p.grad.is_contiguous()
             and _wgrad_inplace(dY.device)):
         side = grad_accum.side_stream(dY.device)

@@ -255,6 +255,20 @@ def late_ok(*params) -> bool:
     return True
 
 
+def sync_accumulable(param) -> bool:
+    """Sync micro-step (native reducer or single process: the same condition as the late column sums) and ``param``
+    already holds an fp32 contiguous gradient (the reducer's flat-buffer view, or earlier micro-steps' sum): a weight
+    gradient op may add its result into ``param.grad`` itself, on the current stream, and return none -- autograd's
+    AccumulateGrad would otherwise write the gradient and add it in a second pass (136 add kernels per step at one
+    micro-batch per step).  The parameter's AccumulateGrad still runs (with no gradient) and fires the reducer hook
+    after the add was queued.  MAMBA_AMD_SYNC_INPLACE=0 turns it off."""
+    import os
+    return (_late_on and _scope_depth > 0 and not _direct and isinstance(param, torch.nn.Parameter)
+            and param.requires_grad and param.grad is not None and param.grad.dtype == torch.float32
+            and param.grad.is_contiguous() and param.grad.is_cuda
+            and os.environ.get("MAMBA_AMD_SYNC_INPLACE", "1") != "0")
+
+
 def late_colsum(part: torch.Tensor, mode: int, G: int, params) -> None:
     """Queue the column sums of ``part`` (rows x cols after flattening the trailing dims) for ``flush_late``.
     mode 0: params = [p], column j -> p.grad[j]; 1: [weight, bias], columns grouped by G = taps + 1 ([taps | bias]

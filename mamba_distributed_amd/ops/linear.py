@@ -42,6 +42,16 @@ def _wgrad_native(p, dy2: torch.Tensor, x2: torch.Tensor, lb: int = 1):
     Q = x2.shape[1] if lb == 1 else x2.shape[0]
     S = ops.gp_splits(P, Q, T)
     d = grad_accum.deferred(p, "wgrad", (S, P, Q), dy2.device)
+    if grad_accum.sync_accumulable(p):
+        # sync micro-step with the gradient already in place (the reducer's flat-buffer view): the fixed-order slab
+        # sum adds straight into it instead of autograd writing dW and adding it in a second pass
+        if d is None:
+            buf = ops.gp_mm(dy2, x2, None, 1, lb, 1, S, 256)
+        else:
+            buf, mode = d
+            ops.gp_mm(dy2, x2, buf, 1, lb, 1 if mode in (1, 3) else 2, S, 256)
+        ops.gp_reduce(buf, p.grad, True)
+        return None
     if (d is None and lb == 1 and _wgrad_inplace(dy2.device) and grad_accum.accumulable(p) and p.grad.dtype == torch.float32
             and p.grad.is_contiguous()):
         # not deferred (wide models: auto_defer_reduce) on a no-sync micro-step: the split-K wgrad kernel adds
