@@ -132,8 +132,8 @@ def main():
     accum = a.global_batch_tokens // (a.B * a.T * world)
     from mamba_distributed_amd.utils.gemm_tuning import enable_tuned_gemms
     # the TunableOp table only matters when a library GEMM can run: the hipBLASLt A/B switches, or the reference ops
-    lib_gemms = (os.environ.get("MAMBA_AMD_PROJ_GEMM", "pk") != "pk" or os.environ.get("MAMBA_AMD_LMHEAD") == "lib"
-                 or a.reference_ops)
+    from mamba_distributed_amd.ops.linear import library_gemms_possible
+    lib_gemms = library_gemms_possible(cfg) or os.environ.get("MAMBA_AMD_LMHEAD") == "lib" or a.reference_ops
     tuned = False if (a.no_tuned_gemms or not lib_gemms) else enable_tuned_gemms()
     torch.manual_seed(1337)
     model = LMHeadModel(cfg, device=dev)

@@ -145,7 +145,7 @@ def _gp_xc_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
 def _pk_wins_xc(m: int, n: int, k: int) -> bool:
     """The projection-engine switch (MAMBA_AMD_PROJ_GEMM, ops/linear.py::_pk_wins) for the XC . XC input gradient."""
     from ..ops.linear import _pk_wins
-    return _pk_wins(m, n, k, "dgrad")
+    return _pk_wins(m, n, k, "dgrad_xc")
 
 
 def _wgrad_native(p, dY, X, dy_cm, x_cm):

@@ -124,24 +124,50 @@ def _wgrad_inplace(dev) -> bool:
 
 
 def _proj_engine() -> str:
-    """Forward / input-gradient projection GEMM: "pk" (default: the persistent native engine, gemm_pk_k, for
-    every shape it takes), "auto" (pk only for the short-K shapes where it measured faster than hipBLASLt), "lib"
-    (hipBLASLt, A/B only), or a comma list of roles on pk: fwd / dgrad, each optionally suffixed _short
-    (K <= 1024) or _long (K > 1024), e.g. "fwd_short,dgrad".  MAMBA_AMD_PROJ_GEMM selects."""
+    """Forward / input-gradient projection GEMM: "route" (default: the persistent native engine, gemm_pk_k, for every
+    product except the long-K ones of wide models -- see _pk_wins), "pk" (native for every shape it takes), "auto"
+    (pk only for the short-K shapes), "lib" (hipBLASLt, A/B only), or a comma list of roles on pk: fwd / dgrad, each
+    optionally suffixed _short (K <= 1024) or _long (K > 1024), e.g. "fwd_short,dgrad".  MAMBA_AMD_PROJ_GEMM selects."""
     import os
-    return os.environ.get("MAMBA_AMD_PROJ_GEMM", "pk")
+    return os.environ.get("MAMBA_AMD_PROJ_GEMM", "route")
+
+
+def _route_lib(m: int, n_out: int, k: int, role: str) -> bool:
+    """The default routing's library products: the Mamba-2 projection forward / input-gradient GEMMs with a long
+    contraction (K > 1024) AND a wide output (n_out >= 2048, i.e. d_model >= 2048).  Measured whole-step, interleaved
+    (profiles/r5/proj_engine_routing.txt): Mamba-2 1.4B +2.2% and 2.8B @ 8192 +1.0% on hipBLASLt with the tuned
+    solution table, while at d_model 768 (280M: out_proj fwd K = 1536, in_proj dgrad K = 3392 with 768-wide outputs)
+    the native engine ties it and the Mamba-1 channel-major products lose 0.4% on the library."""
+    return role in ("fwd", "dgrad") and k > 1024 and n_out >= 2048 and m >= 2048
+
+
+def library_gemms_possible(cfg) -> bool:
+    """Whether this model's training step can run a library (hipBLASLt) GEMM under the current switches -- the
+    callers load the tuned solution table only then."""
+    import os
+    e = _proj_engine()
+    if e == "pk":
+        return False
+    if e == "route":
+        layer = (getattr(cfg, "ssm_cfg", None) or {}).get("layer", "Mamba1")
+        return layer == "Mamba2" and getattr(cfg, "d_model", 0) >= 2048
+    return True
 
 
 def _pk_wins(m: int, n_out: int, k: int, role: str = "fwd") -> bool:
-    """Engine choice for an (m, n_out, k) product of one role ("fwd" / "dgrad").  Isolated timings at the 280M
-    shapes (profiles/r3/pk*_vs_hipblaslt.log, pk5_inproj_padded_width.log): pk wins at K = 768 with moderate
-    outputs (padded in_proj fwd 316 vs 334 us, out_proj dgrad 135 vs 132 us at 64k tokens) and loses at K >= 1536
-    and on the 50k-wide lm_head, which stay on hipBLASLt under the default "auto"."""
+    """Engine choice for an (m, n_out, k) product of one role ("fwd" / "dgrad"; the Mamba-1 channel-major products
+    pass "fwd_cm" / "dgrad_xc", which the default routing keeps native).  Isolated timings at the 280M shapes
+    (profiles/r3/pk*_vs_hipblaslt.log, pk5_inproj_padded_width.log): pk wins at K = 768 with moderate outputs (padded
+    in_proj fwd 316 vs 334 us, out_proj dgrad 135 vs 132 us at 64k tokens) and loses at K >= 1536; whole-step, the
+    wide models gain from the library on those (_route_lib)."""
     e = _proj_engine()
     if e == "lib":
         return False
     if e == "pk":
         return True
+    if e == "route":
+        return not _route_lib(m, n_out, k, role)
+    role = {"fwd_cm": "fwd", "dgrad_xc": "dgrad"}.get(role, role)
     if e == "auto":
         return k <= 1024 and m * n_out <= (1 << 28)
     if m * n_out > (1 << 28):  # never the lm_head
@@ -170,7 +196,7 @@ def mm_nt(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
           and a.stride(-1) == 1 and b.stride(-1) == 1 and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0
           and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0 and a.shape[1] > 192 and a.shape[1] % 8 == 0
           and b.shape[0] % 8 == 0 and a.shape[0] * b.shape[0] >= (1 << 23)
-          and _pk_wins(a.shape[0], b.shape[0], a.shape[1]))
+          and _pk_wins(a.shape[0], b.shape[0], a.shape[1], "fwd_cm"))
     return _pk_mm(a, b) if ok else torch.mm(a, b.t())
 
 
