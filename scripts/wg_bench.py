@@ -52,6 +52,7 @@ def m1_cases(T=65536, d=768, di=1536, R=48, N=16):
         ("m1_out_fwd XC.KC bf16", y2, w_out, 1, 0, 0, 1, 256, 2.0 * T * di * d),
         ("m1_out_wgrad XC.KC slabs", dout, y2, 1, 0, 1, 0, 256, 2.0 * T * di * d),
         ("m1_in_wgrad KC.XC slabs", dxz, h2, 0, 1, 1, 0, 256, 2.0 * T * d * 2 * di),
+        ("m1_in_wgrad^T XC.KC slabs (768 x 3072)", h2, dxz, 1, 0, 1, 0, 256, 2.0 * T * d * 2 * di),
         ("m1_x_wgrad KC.KC slabs", dxdbl, co2, 0, 0, 1, 0, 256, 2.0 * T * di * (R + 2 * N)),
         ("m1_x_wgrad KC.KC slabs 128-row", dxdbl, co2, 0, 0, 1, 0, 128, 2.0 * T * di * (R + 2 * N)),
         ("m1_dt_wgrad KC.KC slabs (1536 x 48)", dd2, dxdbl[:R], 0, 0, 1, 0, 256, 2.0 * T * di * R),
