@@ -19,8 +19,11 @@ projection gradients.  Inside an ``accumulation_scope`` on the no-sync micro-ste
     whole step's gradient.  ``accumulation_scope(defer_reduce=...)`` picks this per model
     (parallel/microbatch.py::auto_defer_reduce); MAMBA_AMD_DEFER_REDUCE=0 / 1 forces it off / on.
 
-The last micro-step (the one that triggers DDP's bucketed all-reduce) and anything outside a scope
-use the normal autograd path, so DDP's gradient hooks fire exactly as usual.  The scope also caches
+The last micro-step (the one that triggers the bucketed all-reduce) and anything outside a scope use the normal
+autograd path, so torch DDP's gradient hooks fire exactly as usual.  Under the native reducer or in a single process
+(``set_late``, parallel/microbatch.py) the sync micro-step additionally (a) adds the projection weight gradients into
+the existing flat-buffer .grad instead of returning them (``sync_accumulable``) and (b) leaves the small parameter-
+gradient partials for one batched column sum after the backward (``late_colsum`` / ``flush_late``).  The scope also caches
 bf16 copies of the projection weights: weights cannot change between the micro-steps of one
 optimizer step, and the fused AdamW update does not bump tensor versions, so the cache is tied to
 the scope rather than to version counters.
