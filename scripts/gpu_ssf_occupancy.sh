@@ -1,3 +1,6 @@
+#!/bin/bash
+# (experiment record: MAMBA_AMD_SSF_LDS_PAD was a temporary launcher switch -- dynamic LDS padding of selscan_fwd_sg_k --
+#  removed after the measurement, profiles/r5/selscan_fwd_whole_rounds_rejected.txt)
 cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp
 mkdir -p gpurun_out/ssf
 for r in 1 2; do
