@@ -35,11 +35,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--B", type=int, default=64)
     ap.add_argument("--L", type=int, default=1024)
+    ap.add_argument("--H", type=int, default=24, help="heads (24: Mamba-2 280M, 80: 2.8B)")
     a = ap.parse_args()
     assert _ext.load(), _ext.error()
     ops = torch.ops.mamba_amd
     dev = "cuda"
-    B, L, H, P, N, G = a.B, a.L, 24, 64, 128, 1
+    B, L, H, P, N, G = a.B, a.L, a.H, 64, 128, 1
     di = H * P
     conv_dim = di + 2 * G * N
     torch.manual_seed(0)
