@@ -42,8 +42,11 @@ template <typename T> __device__ __forceinline__ void st4(T* p, const float (&o)
 template <> __device__ __forceinline__ void st4<float>(float* p, const float (&o)[4]) {
   *reinterpret_cast<float4*>(p) = make_float4(o[0], o[1], o[2], o[3]);
 }
+// two floats -> two RNE bf16 in one dword (one v_cvt_pk_bf16_f32; NaN stays NaN)
+typedef __bf16 mamba_bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float mamba_f32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ unsigned pack2(float a, float b) {
-  return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((mamba_f32x2_t){a, b}, mamba_bf16x2_t));
 }
 template <> __device__ __forceinline__ void st4<bf16_t>(bf16_t* p, const float (&o)[4]) {
   *reinterpret_cast<uint2*>(p) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));

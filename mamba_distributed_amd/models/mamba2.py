@@ -7,8 +7,8 @@ Parameter names, shapes and init follow upstream ``mamba_ssm/modules/mamba2.py::
                                              native persistent dgrad (K = padded width), native split-K wgrad
     y      = mamba2_inner_fn(zxbcdt, ...)    HIP: conv1d(xBC)+SiLU -> SSD -> gated RMSNorm
     out    = out_proj(y)                     native persistent fwd and dgrad, native split-K wgrad
-(projection routing: ops/linear.py; hipBLASLt only for the long-K fwd / dgrad products of d_model >= 2048 models,
-where it measured faster, and under the MAMBA_AMD_PROJ_GEMM=lib A/B switch)
+(projection routing: ops/linear.py; the native engines for every model, hipBLASLt only under the
+MAMBA_AMD_PROJ_GEMM A/B switches)
 
 The conv, SSD and norm kernels read their operands straight out of the strided zxbcdt buffer
 and the backward writes d(zxbcdt) as one buffer in the same padded layout (ops/ssd.py).

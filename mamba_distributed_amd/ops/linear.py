@@ -3,8 +3,8 @@
 Forward and input-gradient GEMMs run on the persistent engine (``gp_pk``: one workgroup per CU walks the
 output tiles; the next tile's operands stream into LDS while the previous tile's bf16 epilogue drains as
 whole-row stores), the input gradient as dY . (W^T)^T against a transposed weight cached per optimizer step,
-for every training-size shape (``_pk_wins``; hipBLASLt only for tiny token counts and as an A/B switch).  The
-weight
+for every training-size shape of every model (``_pk_wins``; torch.mm only below the engine's minimum token count,
+hipBLASLt only under the MAMBA_AMD_PROJ_GEMM A/B switch).  The weight
 gradient dW = dY^T X reduces over all B*T tokens into a small output (3352 x 768 for in_proj), where the
 library leaves most CUs idle: the native engine (csrc/kernels/gemm_pipe.hip, ``gp_mm`` with both operands
 token-major) splits the tokens into S K-slices written as fp32 slabs.  Inside an accumulation scope the
@@ -124,49 +124,31 @@ def _wgrad_inplace(dev) -> bool:
 
 
 def _proj_engine() -> str:
-    """Forward / input-gradient projection GEMM: "route" (default: the persistent native engine, gemm_pk_k, for every
-    product except the long-K ones of wide models -- see _pk_wins), "pk" (native for every shape it takes), "auto"
-    (pk only for the short-K shapes), "lib" (hipBLASLt, A/B only), or a comma list of roles on pk: fwd / dgrad, each
-    optionally suffixed _short (K <= 1024) or _long (K > 1024), e.g. "fwd_short,dgrad".  MAMBA_AMD_PROJ_GEMM selects."""
+    """Forward / input-gradient projection GEMM engine: "pk" (default: the persistent native engine, gemm_pk_k, for
+    every product), "auto" (pk only for the short-K shapes, K <= 1024), "lib" (hipBLASLt), or a comma list of roles on
+    pk: fwd / dgrad, each optionally suffixed _short (K <= 1024) or _long (K > 1024), e.g. "fwd_short,dgrad".
+    Everything but "pk" is an A/B switch (MAMBA_AMD_PROJ_GEMM).  hipBLASLt measured 2.2% / 1.0% faster whole-step at
+    the 1.4B / 2.8B long-K shapes (profiles/r5/proj_engine_routing.txt); the native engine stays the default there
+    (profiles/r6/pp_ring_gemm_rejected.txt has the round-6 attempt at closing that gap)."""
     import os
-    return os.environ.get("MAMBA_AMD_PROJ_GEMM", "route")
-
-
-def _route_lib(m: int, n_out: int, k: int, role: str) -> bool:
-    """The default routing's library products: the Mamba-2 projection forward / input-gradient GEMMs with a long
-    contraction (K > 1024) AND a wide output (n_out >= 2048, i.e. d_model >= 2048).  Measured whole-step, interleaved
-    (profiles/r5/proj_engine_routing.txt): Mamba-2 1.4B +2.2% and 2.8B @ 8192 +1.0% on hipBLASLt with the tuned
-    solution table, while at d_model 768 (280M: out_proj fwd K = 1536, in_proj dgrad K = 3392 with 768-wide outputs)
-    the native engine ties it and the Mamba-1 channel-major products lose 0.4% on the library."""
-    return role in ("fwd", "dgrad") and k > 1024 and n_out >= 2048 and m >= 2048
+    return os.environ.get("MAMBA_AMD_PROJ_GEMM", "pk")
 
 
 def library_gemms_possible(cfg) -> bool:
-    """Whether this model's training step can run a library (hipBLASLt) GEMM under the current switches -- the
-    callers load the tuned solution table only then."""
-    import os
-    e = _proj_engine()
-    if e == "pk":
-        return False
-    if e == "route":
-        layer = (getattr(cfg, "ssm_cfg", None) or {}).get("layer", "Mamba1")
-        return layer == "Mamba2" and getattr(cfg, "d_model", 0) >= 2048
-    return True
+    """Whether a training step can run a library (hipBLASLt) projection GEMM under the current switches (only the
+    A/B switches route there); the callers load the tuned solution table only then."""
+    return _proj_engine() != "pk"
 
 
 def _pk_wins(m: int, n_out: int, k: int, role: str = "fwd") -> bool:
     """Engine choice for an (m, n_out, k) product of one role ("fwd" / "dgrad"; the Mamba-1 channel-major products
-    pass "fwd_cm" / "dgrad_xc", which the default routing keeps native).  Isolated timings at the 280M shapes
-    (profiles/r3/pk*_vs_hipblaslt.log, pk5_inproj_padded_width.log): pk wins at K = 768 with moderate outputs (padded
-    in_proj fwd 316 vs 334 us, out_proj dgrad 135 vs 132 us at 64k tokens) and loses at K >= 1536; whole-step, the
-    wide models gain from the library on those (_route_lib)."""
+    pass "fwd_cm" / "dgrad_xc").  The default ("pk") takes the native engine for every training-size product; the
+    other settings are the A/B switches described in _proj_engine."""
     e = _proj_engine()
     if e == "lib":
         return False
     if e == "pk":
         return True
-    if e == "route":
-        return not _route_lib(m, n_out, k, role)
     role = {"fwd_cm": "fwd", "dgrad_xc": "dgrad"}.get(role, role)
     if e == "auto":
         return k <= 1024 and m * n_out <= (1 << 28)

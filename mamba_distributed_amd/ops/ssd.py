@@ -124,8 +124,8 @@ def mamba_chunk_scan_combined(x, dt, A, B, C, chunk_size=256, D=None, z=None, dt
 
 
 # ----------------------------------------------------------------------------------------
-# Fused Mamba-2 inner path: conv1d(xBC)+SiLU -> SSD -> gated RMSNorm   (out_proj stays outside,
-# on hipBLASLt, so autocast handles it)
+# Fused Mamba-2 inner path: conv1d(xBC)+SiLU -> SSD -> gated RMSNorm   (out_proj stays outside, on the
+# native persistent GEMM of ops/linear.py)
 # ----------------------------------------------------------------------------------------
 class _Mamba2InnerFn(torch.autograd.Function):
     @staticmethod

@@ -77,7 +77,8 @@ class TrainArgs:
     metrics_jsonl: Optional[str] = None
     sample_prompt: str = "Hello, I'm a language model,"
     device_type: str = "auto"
-    tuned_gemms: bool = True             # replay the shipped gfx950 GEMM solution table
+    tuned_gemms: bool = True             # replay the shipped gfx950 hipBLASLt solution table (only consulted when a
+                                         # library GEMM can run: the MAMBA_AMD_PROJ_GEMM / MAMBA_AMD_LMHEAD A/B switches)
     fp32_matmul_precision: str = "highest"  # reference train.py uses "high" (A100 TF32); gfx950 has no
                                             # xf32 and the tuned GEMM table needs "highest" (utils/gemm_tuning)
     tp: int = 1                          # tensor parallel degree (Mamba-2 heads; parallel/tensor_parallel.py)
@@ -130,7 +131,8 @@ class Trainer:
             self.val_loader = DataLoaderLite(a.B, a.T, data_rank, world, "val", self.master, a.data_root)
         if self.device_type == "cuda":
             torch.set_float32_matmul_precision(a.fp32_matmul_precision)
-            if a.tuned_gemms:
+            from .ops.linear import library_gemms_possible
+            if a.tuned_gemms and (library_gemms_possible(self.config) or os.environ.get("MAMBA_AMD_LMHEAD") == "lib"):
                 from .utils.gemm_tuning import enable_tuned_gemms
                 enable_tuned_gemms()
         self.raw_model = LMHeadModel(self.config, device=self.device)

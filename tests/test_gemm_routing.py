@@ -1,5 +1,5 @@
-"""Default projection-GEMM routing (ops/linear.py::_pk_wins "route"): native persistent engine everywhere except the
-long-K products of wide Mamba-2 models, which go to hipBLASLt (measured, profiles/r5/proj_engine_routing.txt)."""
+"""Default projection-GEMM routing (ops/linear.py::_pk_wins): the native persistent engine for every forward /
+input-gradient product of every BASELINE config; hipBLASLt only under the MAMBA_AMD_PROJ_GEMM A/B switches."""
 import pytest
 
 from mamba_distributed_amd import preset
@@ -11,7 +11,7 @@ def _default_engine(monkeypatch):
     monkeypatch.delenv("MAMBA_AMD_PROJ_GEMM", raising=False)
 
 
-def test_route_keeps_headline_shapes_native():
+def test_default_keeps_headline_shapes_native():
     T = 65536
     # Mamba-2 280M: in_proj fwd (padded), out_proj fwd, in_proj dgrad, out_proj dgrad
     assert linear._pk_wins(T, 3392, 768, "fwd")
@@ -20,25 +20,26 @@ def test_route_keeps_headline_shapes_native():
     assert linear._pk_wins(T, 1536, 768, "dgrad")
 
 
-def test_route_sends_wide_long_k_to_library():
+def test_default_keeps_wide_long_k_native():
     T = 32768
-    # Mamba-2 1.4B: every projection product has K > 1024 and a >= 2048-wide output
-    assert not linear._pk_wins(T, 8512, 2048, "fwd")
-    assert not linear._pk_wins(T, 2048, 4096, "fwd")
-    assert not linear._pk_wins(T, 2048, 8512, "dgrad")
-    assert not linear._pk_wins(T, 4096, 2048, "dgrad")
-    # the Mamba-1 channel-major products stay native at any width
+    # Mamba-2 1.4B and 2.8B: every projection product has K > 1024 and a >= 2048-wide output (round 5 sent these to
+    # hipBLASLt; round 6 keeps them on the hand-written engine)
+    for n, k, role in ((8512, 2048, "fwd"), (2048, 4096, "fwd"), (2048, 8512, "dgrad"), (4096, 2048, "dgrad"),
+                       (10624, 2560, "fwd"), (2560, 5120, "fwd"), (2560, 10624, "dgrad"), (5120, 2560, "dgrad")):
+        assert linear._pk_wins(T, n, k, role), (n, k, role)
+    # the Mamba-1 channel-major products
     assert linear._pk_wins(8192, T, 2048, "fwd_cm")
     assert linear._pk_wins(T, 2048, 8192, "dgrad_xc")
 
 
-def test_library_table_only_where_a_library_gemm_can_run(monkeypatch):
-    assert not linear.library_gemms_possible(preset("mamba2-280m"))
-    assert not linear.library_gemms_possible(preset("mamba1-280m"))
+def test_library_table_only_under_the_ab_switches(monkeypatch):
+    for name in ("mamba2-280m", "mamba1-280m", "mamba2-1.4b", "mamba2-2.8b", "mamba1-370m"):
+        assert not linear.library_gemms_possible(preset(name)), name
+    monkeypatch.setenv("MAMBA_AMD_PROJ_GEMM", "auto")
     assert linear.library_gemms_possible(preset("mamba2-1.4b"))
-    assert linear.library_gemms_possible(preset("mamba2-2.8b"))
-    monkeypatch.setenv("MAMBA_AMD_PROJ_GEMM", "pk")
-    assert not linear.library_gemms_possible(preset("mamba2-1.4b"))
-    assert linear._pk_wins(32768, 8512, 2048, "fwd")
+    assert not linear._pk_wins(32768, 8512, 2048, "fwd")  # auto: K > 1024 -> library
+    assert not linear._pk_wins(32768, 2048, 4096, "fwd")
+    monkeypatch.setenv("MAMBA_AMD_PROJ_GEMM", "lib")
+    assert not linear._pk_wins(65536, 3392, 768, "fwd")
     monkeypatch.setenv("MAMBA_AMD_PROJ_GEMM", "fwd_short,dgrad")
     assert linear._pk_wins(65536, 768, 3072, "dgrad_xc")  # role lists see the Mamba-1 roles as fwd / dgrad

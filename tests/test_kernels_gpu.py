@@ -174,8 +174,9 @@ def test_cross_entropy(cuda):
 @pytest.mark.parametrize("row_chunk", [None, 2048])
 def test_fused_lm_head_ce_native(cuda, row_chunk, engine, monkeypatch):
     """The row-chunked lm_head + CE at the 280M head shape (d 768, V 50304) against fp32 math: loss, dh and dW
-    (row_chunk 2048: three chunks, the last one 404 rows, dW accumulated across them); engine "native": all three
-    products on the native MFMA engines, "lib": the default (hipBLASLt, fp32-output dW accumulation)."""
+    (row_chunk 2048: three chunks, the last one 404 rows, dW accumulated across them); engine "native" (the
+    default): all three products on the native MFMA engines, "lib": the MAMBA_AMD_LMHEAD=lib A/B switch (hipBLASLt,
+    fp32-output dW accumulation)."""
     import importlib
     monkeypatch.setenv("MAMBA_AMD_LMHEAD", engine)
     ce = importlib.import_module("mamba_distributed_amd.ops.cross_entropy")
