@@ -439,6 +439,51 @@ def test_model_native_vs_reference_headline_width(cuda, monkeypatch, layer, engi
     assert not bad, bad
 
 
+@pytest.mark.parametrize("d_model", [2048, 2560])
+def test_model_native_wide_vs_reference(cuda, monkeypatch, d_model):
+    """The 1.4B / 2.8B layer widths (d_model 2048 / 2560: in_proj 8512 / 10576 -> padded 10624 wide, out_proj
+    K = 4096 / 5120) through 2 Mamba-2 layers on the DEFAULT routing: every projection forward and input gradient on
+    the hand-written persistent engine (a spy counts them: the wide long-K products that round 5 routed to hipBLASLt
+    included), loss and every parameter gradient vs the fp32 reference ops."""
+    monkeypatch.delenv("MAMBA_AMD_PROJ_GEMM", raising=False)
+    from mamba_distributed_amd import LMHeadModel, MambaConfig
+    from mamba_distributed_amd.ops import linear as lin
+    calls = []
+    orig = lin._pk_mm
+
+    def spy(a2, w):
+        calls.append((a2.shape[0], w.shape[0], a2.shape[1]))
+        return orig(a2, w)
+    monkeypatch.setattr(lin, "_pk_mm", spy)
+    torch.manual_seed(0)
+    cfg = MambaConfig(d_model=d_model, n_layer=2, vocab_size=4096, ssm_cfg={"layer": "Mamba2"})
+    m = LMHeadModel(cfg, device=cuda)
+    sharpen_logits(m)
+    x = torch.randint(0, 4096, (4, 1024), device=cuda)
+    y = torch.randint(0, 4096, (4, 1024), device=cuda)
+
+    def lossgrad(force_ref):
+        if force_ref:
+            os.environ["MAMBA_AMD_FORCE_REFERENCE"] = "1"
+        try:
+            m.zero_grad(set_to_none=True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                _, loss = m(x, y)
+            loss.backward()
+            return loss.item(), {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+        finally:
+            os.environ.pop("MAMBA_AMD_FORCE_REFERENCE", None)
+
+    ln, gn = lossgrad(False)
+    # per layer: in_proj fwd + dgrad, out_proj fwd + dgrad, all with K > 1024 or a >= 2048-wide output
+    long_k = [c for c in calls if c[2] > 1024]
+    assert len(calls) >= 4 * cfg.n_layer and len(long_k) >= 2 * cfg.n_layer, calls
+    lr, gr = lossgrad(True)
+    check_loss(ln, lr, cfg.vocab_size)
+    bad = {n: rel(gn[n], gr[n]) for n in gr if rel(gn[n], gr[n]) > 5e-2}
+    assert not bad, bad
+
+
 @pytest.mark.parametrize("layer", ["Mamba1", "Mamba2"])
 def test_bench_path_vs_reference(cuda, monkeypatch, layer):
     """The exact bench.py / trainer step path against the fp32 reference ops: fused lm_head + cross-entropy
