@@ -141,6 +141,8 @@ def main():
         model.set_activation_checkpointing(a.activation_checkpointing)
     dmodel = ddp_mod.wrap_data_parallel(model, info, a.dp_impl, a.bucket_cap_mb, a.grad_comm_dtype)
     opt = model.configure_optimizers(0.1, 6e-4, "cuda" if dev.startswith("cuda") else "cpu", False)
+    # the reducer leaves the gradients summed for the native AdamW, which divides (parallel/ddp.py)
+    ddp_mod.configure_grad_average(dmodel, opt)
     loader = SyntheticTokens(a.B, a.T, cfg.vocab_size, info.rank, world, device=dev)
     fused = not a.no_fused_ce
     overlap = resolve_overlap("off" if a.no_overlap else a.overlap, cfg, a.B * a.T)

@@ -81,7 +81,10 @@ __global__ __launch_bounds__(1024) void clip_scale_k(const float* __restrict__ p
   }
   if (threadIdx.x == 0) {
     const float norm = (float)(sqrt(red[0]) / (double)divisor);
-    const float coef = max_norm > 0.f ? fminf(1.f, max_norm / (norm + 1e-6f)) : 1.f;
+    // torch.nn.utils.clip_grad_norm_: clamp(max_norm / (norm + 1e-6), max=1) -- a NaN norm gives a NaN coefficient
+    // (poisoning every parameter, as torch does; fminf would return 1 and drop it)
+    const float c = max_norm / (norm + 1e-6f);
+    const float coef = max_norm > 0.f ? (c > 1.f ? 1.f : c) : 1.f;
     out[0] = norm;
     out[1] = coef / divisor;
   }

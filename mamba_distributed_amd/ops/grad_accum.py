@@ -31,7 +31,7 @@ the scope rather than to version counters.
 from __future__ import annotations
 
 import contextlib
-from typing import Dict, List, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import torch
 
@@ -240,6 +240,16 @@ def set_late(enabled: bool) -> None:
     _late_on = bool(enabled)
 
 
+_held: Optional[set] = None  # ids of the native reducer's held parameters (parallel/reducer.py::held_param), if any
+
+
+def register_held(params) -> None:
+    """The native reducer's held parameters: with a reducer alive, only these may take the late path (a late
+    gradient of any other parameter would be all-reduced from its hook before flush_late wrote it)."""
+    global _held
+    _held = {id(p) for p in params}
+
+
 def late_ok(*params) -> bool:
     """The sync micro-step may queue ``params``' partials for ``flush_late`` (fp32 parameters whose .grad, if any, is
     fp32 contiguous; MAMBA_AMD_LATE_REDUCE=0 turns it off)."""
@@ -248,12 +258,17 @@ def late_ok(*params) -> bool:
         return False
     if os.environ.get("MAMBA_AMD_LATE_REDUCE", "1") == "0":
         return False
+    from ..parallel.reducer import held_param
     for p in params:
         if p is None:
             continue
         if not (isinstance(p, torch.Tensor) and p.is_leaf and p.requires_grad and p.dtype == torch.float32 and p.is_cuda):
             return False
         if p.grad is not None and (p.grad.dtype != torch.float32 or not p.grad.is_contiguous()):
+            return False
+        # only parameters the reducer holds until finish() (small non-matrix ones): a late gradient of a parameter
+        # whose bucket launches from the backward's hooks would be all-reduced before flush_late writes it
+        if not held_param(p) or (_held is not None and id(p) not in _held):
             return False
     return True
 

@@ -9,7 +9,8 @@ What it folds, per optimizer step:
     clip coefficient on the device (``clip_and_step``); the update multiplies each gradient by it as it reads it,
     so there is no separate scale pass over the gradients;
   * the data-parallel average: with the native reducer (parallel/reducer.py) the reducer can leave the summed
-    gradients unscaled and the 1/world factor rides on the same coefficient (``fold_average``);
+    gradients unscaled and the 1/world factor rides on the same coefficient (``clip_and_step(grad_divisor=...)``,
+    passed explicitly per call from the reducer's state);
   * the bf16 weight images: the projection GEMMs of the next step read bf16 copies of the weights (plain casts, and
     the zero-padded in_proj rows of ops/linear.py).  The update pass writes them from the updated fp32 value it
     already holds (ops/grad_accum.py image_demand / provide_image), instead of a cast / zero-fill / copy per
@@ -56,7 +57,6 @@ class NativeAdamW(torch.optim.Optimizer):
         self._flat: Dict[torch.device, tuple] = {}  # device -> (m, v, {id(p): offset})
         self._imgs: Dict[tuple, torch.Tensor] = {}   # (id(p), kind) -> persistent bf16 image buffer
         self._blk_cache: Dict[tuple, torch.Tensor] = {}
-        self.fold_average = 1.0  # gradients arrive summed over this many ranks (the reducer skipped its 1/world)
 
     # ---- state -------------------------------------------------------------------------------------------------
     def _params(self) -> List[torch.Tensor]:
@@ -187,10 +187,11 @@ class NativeAdamW(torch.optim.Optimizer):
 
     # ---- step --------------------------------------------------------------------------------------------------
     @torch.no_grad()
-    def clip_and_step(self, max_norm: float) -> torch.Tensor:
-        """clip_grad_norm_(params, max_norm) followed by step(), as one norm pass + one update pass.  Returns the
-        total gradient norm (of the averaged gradients when the reducer's average is folded)."""
-        return self._run(max_norm)
+    def clip_and_step(self, max_norm: float, grad_divisor: float = 1.0) -> torch.Tensor:
+        """clip_grad_norm_(params, max_norm) followed by step(), as one norm pass + one update pass, on the gradients
+        DIVIDED by ``grad_divisor`` (the native reducer's deferred 1/world average: parallel/ddp.py::clip_and_step
+        passes reducer.grad_divisor).  Returns the total norm of the divided gradients."""
+        return self._run(max_norm, float(grad_divisor))
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -198,17 +199,16 @@ class NativeAdamW(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        self._run(None)
+        self._run(None, 1.0)
         return loss
 
-    def _run(self, max_norm: Optional[float]):
+    def _run(self, max_norm: Optional[float], grad_divisor: float):
         ops = _ext.ops()
         norm = None
         for dev, (tab, blk, regs, ranges, keep) in self._tables().items():
             gscale = None
-            if max_norm is not None or self.fold_average != 1.0:
-                gscale = ops.opt_grad_norm(tab, blk, float(max_norm) if max_norm is not None else 0.0,
-                                           float(self.fold_average))
+            if max_norm is not None or grad_divisor != 1.0:
+                gscale = ops.opt_grad_norm(tab, blk, float(max_norm) if max_norm is not None else 0.0, grad_divisor)
                 norm = gscale[0]
             for gi, group in enumerate(self.param_groups):
                 r = ranges.get(gi)

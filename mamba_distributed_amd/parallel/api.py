@@ -110,7 +110,9 @@ def sync_tp_grads(model, groups: Optional[ParallelGroups] = None) -> None:
 @torch.no_grad()
 def grad_norm(model) -> torch.Tensor:
     """Global L2 norm of the gradients of a (possibly TP-sharded) model: sharded params are summed
-    over TP, replicated rows / params counted once."""
+    over TP, replicated rows / params counted once (of the data-parallel AVERAGE: a deferred 1/world is applied)."""
+    from .ddp import averaged_grads
+    averaged_grads(model)
     m = getattr(model, "module", model)
     ctx = _ctx(model)
     tp = ctx.tp if ctx is not None else 1
@@ -138,6 +140,8 @@ def grad_norm(model) -> torch.Tensor:
 @torch.no_grad()
 def clip_grad_norm_(model, max_norm: float, groups: Optional[ParallelGroups] = None) -> torch.Tensor:
     """TP-aware ``torch.nn.utils.clip_grad_norm_`` (identical to it when tp == 1)."""
+    from .ddp import averaged_grads
+    averaged_grads(model)  # a deferred data-parallel 1/world average (parallel/reducer.py) is applied first
     ctx = _ctx(model)
     if ctx is None or ctx.tp == 1:
         m = getattr(model, "module", model)

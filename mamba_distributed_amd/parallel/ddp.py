@@ -96,13 +96,37 @@ def set_grad_sync(model, enabled: bool):
         r.arm()
 
 
+def configure_grad_average(model, optimizer) -> bool:
+    """Once, before the first optimizer step: with the native reducer, fp32 collectives and the native AdamW as the
+    gradient consumer, the reducer leaves the all-reduced gradients SUMMED (``reducer.grad_divisor = world``) and
+    ``clip_and_step`` hands that divisor to the optimizer, which folds it into its clip coefficient.  Every step takes
+    the same path.  Returns whether the average is deferred.  Any other consumer (a torch optimizer, the TP clip,
+    ``averaged_grads``) divides first (``materialize_average``)."""
+    from ..ops.optim import NativeAdamW
+    r = _reducer(model)
+    if r is None:
+        return False
+    r.defer_average = isinstance(optimizer, NativeAdamW) and r.world > 1 and r.comm_dtype is None
+    return r.defer_average
+
+
+def averaged_grads(model) -> None:
+    """Make every ``.grad`` hold the data-parallel AVERAGE (a deferred 1/world is applied now): call before reading
+    gradients outside clip_and_step (logging a norm, a custom optimizer, hooks)."""
+    r = _reducer(model)
+    if r is not None:
+        r.materialize_average()
+
+
 def clip_grad_norm_(model, max_norm: float) -> torch.Tensor:
     """``torch.nn.utils.clip_grad_norm_`` (reference train.py:222).  Under the native reducer every
     gradient is a view into one flat fp32 buffer, so the global 2-norm and the rescale are one
-    reduction and one scale kernel over that buffer instead of per-tensor foreach launches."""
+    reduction and one scale kernel over that buffer instead of per-tensor foreach launches (a deferred
+    1/world average is applied first)."""
     r = _reducer(model)
     if r is None:
         return torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm)
+    r.materialize_average()
     total = torch.linalg.vector_norm(r.flat, 2.0)
     r.flat.mul_(torch.clamp(max_norm / (total + 1e-6), max=1.0))
     return total
@@ -111,21 +135,16 @@ def clip_grad_norm_(model, max_norm: float) -> torch.Tensor:
 def clip_and_step(model, optimizer, max_norm: float) -> torch.Tensor:
     """``clip_grad_norm_(model, max_norm)`` then ``optimizer.step()`` (reference train.py:222, :227).  With the
     native AdamW (ops/optim.py) the two are one norm pass and one update pass with the clip coefficient folded into
-    the update's gradient read; under the native reducer the 1/world average rides on the same coefficient from the
-    second step on (the reducer stops scaling its flat buffer: one full pass over it less per step)."""
+    the update's gradient read; a deferred 1/world average (configure_grad_average) rides on the same coefficient,
+    passed explicitly from the reducer's ``grad_divisor`` on every step.  The returned norm is always the norm of
+    the AVERAGED gradients."""
     from ..ops.optim import NativeAdamW
     if not isinstance(optimizer, NativeAdamW):
-        norm = clip_grad_norm_(model, max_norm)
+        norm = clip_grad_norm_(model, max_norm)  # materialises a deferred average first
         optimizer.step()
         return norm
     r = _reducer(model)
-    norm = optimizer.clip_and_step(max_norm)
-    if r is not None and r.world > 1 and r.comm_dtype is None:
-        # the first step's gradients were averaged by the reducer; from the next step on it leaves them summed
-        # and the optimizer divides (so nothing else may read .grad between finish() and this call)
-        r.average_in_finish = False
-        optimizer.fold_average = float(r.world)
-    return norm
+    return optimizer.clip_and_step(max_norm, grad_divisor=r.grad_divisor if r is not None else 1.0)
 
 
 def finish_grad_sync(model) -> None:

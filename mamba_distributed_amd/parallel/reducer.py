@@ -27,6 +27,14 @@ import torch
 import torch.distributed as dist
 
 
+def held_param(p: torch.Tensor) -> bool:
+    """The parameters whose gradients the sync micro-step may produce AFTER the backward, in the batched late column
+    sum (ops/grad_accum.py::flush_late): the small non-matrix ones -- norm weights, conv taps / bias, A_log / D /
+    dt_bias.  Their buckets are held until finish(); every other parameter's bucket launches from the backward's
+    hooks (small 2-D weights such as Mamba-1's x_proj / dt_proj included, so they keep overlapping the backward)."""
+    return p.numel() < GradReducer.SMALL_NUMEL and p.dim() != 2
+
+
 class GradReducer:
     SMALL_NUMEL = 1 << 17
 
@@ -41,12 +49,12 @@ class GradReducer:
         assert params, "no trainable parameters"
         dtypes = {p.dtype for p in params}
         assert dtypes == {torch.float32}, f"GradReducer keeps fp32 gradients for fp32 parameters, got {dtypes}"
-        # the small parameters (norm weights, conv taps, A_log / D / dt_bias: < SMALL_NUMEL elements each) go last, in
-        # buckets of their own that are HELD until finish(): on the sync micro-step their gradients come from the
-        # batched late column sum after the backward (ops/grad_accum.py::flush_late), so their hooks fire before the
-        # gradients exist.  A few MB per model, all-reduced once at the end.
-        order = [p for p in reversed(params) if p.numel() >= self.SMALL_NUMEL]
-        small = [p for p in reversed(params) if p.numel() < self.SMALL_NUMEL]
+        # the held parameters (held_param: norm weights, conv taps, A_log / D / dt_bias) go last, in buckets of their
+        # own that are HELD until finish(): on the sync micro-step their gradients come from the batched late column
+        # sum after the backward (ops/grad_accum.py::flush_late), so their hooks fire before the gradients exist.  A
+        # few MB per model, all-reduced once at the end.  grad_accum.late_ok refuses any other parameter.
+        order = [p for p in reversed(params) if not held_param(p)]
+        small = [p for p in reversed(params) if held_param(p)]
         total = sum(p.numel() for p in params)
         self.flat = torch.zeros(total, dtype=torch.float32, device=params[0].device)
         cap = max(1, int(bucket_cap_mb * 2**20 / 4))
@@ -73,13 +81,20 @@ class GradReducer:
         if self._held_from is None:
             self._held_from = len(self.buckets)
         self._params = params
+        from ..ops import grad_accum
+        grad_accum.register_held([p for p in params if held_param(p)])
         for p in params:
             self._attach(p)
         self._hooks = [p.register_post_accumulate_grad_hook(self._hook) for p in params]
         self._armed = False
-        # finish() divides the summed gradients by the world size; parallel/ddp.py::clip_and_step turns this off when
-        # the native optimizer folds the 1/world factor into its update
-        self.average_in_finish = True
+        # The 1/world average.  finish() multiplies the summed gradients by 1/world unless ``defer_average`` is set
+        # (parallel/ddp.py::configure_grad_average, once, before the first step, when the consumer is the native
+        # AdamW: it folds the factor into its clip coefficient, one full pass over the buffer less per step).
+        # ``grad_divisor`` is the explicit state of .grad: the gradients in the flat buffer are the data-parallel
+        # average times grad_divisor (1.0, or world after a deferred finish) until the next zero_grad.  Consumers go
+        # through parallel/ddp.py (clip_grad_norm_ / clip_and_step / averaged_grads), which divide or materialise.
+        self.defer_average = False
+        self.grad_divisor = 1.0
         self._main = None  # the stream that called arm() (the caller's / main micro-batch stream)
         # exposed all-reduce time per sync step: stream time from the end of the last backward
         # (finish() entry, in stream order) to the averaged gradients being ready (finish() exit)
@@ -108,6 +123,13 @@ class GradReducer:
             if p.grad is None or p.grad.data_ptr() != base + 4 * self._offset[id(p)]:
                 self._attach(p)
         self.flat.zero_()
+        self.grad_divisor = 1.0
+
+    def materialize_average(self) -> None:
+        """Make .grad hold the averaged gradients (divide a deferred 1/world now)."""
+        if self.grad_divisor != 1.0:
+            self.flat.mul_(1.0 / self.grad_divisor)
+            self.grad_divisor = 1.0
 
     def arm(self) -> None:
         """Call right before the sync micro-step's backward: its gradient hooks launch the buckets."""
@@ -168,8 +190,12 @@ class GradReducer:
                 w[0].wait()
                 if w[1] is not None:
                     w[1].copy_(w[2])
-        if self.world > 1 and self.comm_dtype is None and self.average_in_finish:
-            self.flat.mul_(1.0 / self.world)
+        if self.world > 1 and self.comm_dtype is None:
+            if self.defer_average:
+                self.grad_divisor = float(self.world)
+            else:
+                self.flat.mul_(1.0 / self.world)
+                self.grad_divisor = 1.0
         if t0 is not None:
             self._exposed.append((t0, self._stamp()))
         self._armed = False

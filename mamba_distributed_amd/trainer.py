@@ -159,6 +159,8 @@ class Trainer:
             self.model = ddp_mod.wrap_data_parallel(self.raw_model, self.info, a.dp_impl, a.bucket_cap_mb,
                                                     a.grad_comm_dtype)
         self.optimizer = self.raw_model.configure_optimizers(a.weight_decay, a.max_lr, self.device_type, self.master)
+        if not self.parallel:  # TP / CP: sync_tp_grads and the TP clip read .grad (the average stays in finish())
+            ddp_mod.configure_grad_average(self.model, self.optimizer)
         if ck is not None:
             self._resume_rest(ck)
         if self.master and self.start_step == 0:

@@ -35,8 +35,11 @@ def main():
     ap.add_argument("--impl", default="native", choices=["native", "ddp"])
     ap.add_argument("--optim", action="store_true",
                     help="also step the optimizer (configure_optimizers -> the native AdamW on the GPU) through "
-                         "parallel/ddp.py::clip_and_step for 3 steps and compare parameters with a single process "
-                         "on torch's AdamW (the reducer's 1/world average is folded into the update from step 2)")
+                         "parallel/ddp.py::clip_and_step for 4 steps and compare parameters with a single process "
+                         "on torch's AdamW: the reducer leaves the gradients summed and the optimizer divides on every "
+                         "step (configure_grad_average); step 2 also logs the gradient norm through "
+                         "parallel/api.py::grad_norm first; steps 3-4 continue on a torch AdamW loaded from the native "
+                         "optimizer's state_dict")
     a = ap.parse_args()
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
@@ -99,10 +102,20 @@ def run_optim(a, rank, world, ref, model, data, loss_fn):
     opt_ref = torch.optim.AdamW([{"params": [p for p in ref.parameters() if p.dim() >= 2], "weight_decay": 0.1},
                                  {"params": [p for p in ref.parameters() if p.dim() < 2], "weight_decay": 0.0}],
                                 lr=3e-3, betas=(0.9, 0.95), eps=1e-8)
+    from mamba_distributed_amd.parallel.api import grad_norm
     dm = wrap_reducer(model, None, a.bucket_mb, comm_dtype=a.comm_dtype)
     opt = model.configure_optimizers(0.1, 3e-3, "cuda", False)
     assert isinstance(opt, NativeAdamW) or os.environ.get("MAMBA_AMD_NATIVE_ADAMW") == "0", type(opt)
-    for rep in range(3):
+    deferred = ddp_mod.configure_grad_average(dm, opt)
+    assert deferred == (isinstance(opt, NativeAdamW) and a.comm_dtype == "fp32"), deferred
+    for rep in range(4):
+        if rep == 2:
+            # mid-run switch to torch's AdamW through the state_dict (the reducer keeps deferring: clip_and_step's
+            # torch path materialises the average before reading .grad)
+            topt = torch.optim.AdamW([{k: v for k, v in g_.items() if k != "params"} | {"params": g_["params"]}
+                                      for g_ in opt.param_groups])
+            topt.load_state_dict(opt.state_dict())
+            opt = topt
         ref.zero_grad(set_to_none=True)
         it = iter(data)
         with grad_accum.accumulation_scope():
@@ -113,6 +126,12 @@ def run_optim(a, rank, world, ref, model, data, loss_fn):
         mine = iter(data[rank::world])
         with grad_accum.accumulation_scope():
             run_micro_batches(dm, lambda: next(mine), a.accum, loss_fn(dm, a.accum), overlap=True)
+        logged = None
+        if rep == 1:
+            assert dm.reducer.grad_divisor == (world if deferred else 1.0), dm.reducer.grad_divisor
+            logged = grad_norm(dm)  # a reader outside clip_and_step: the average is materialised first
+            assert dm.reducer.grad_divisor == 1.0
+            assert abs(logged.item() - nr.item()) < 2e-3 * nr.item(), (rep, logged.item(), nr.item())
         nd = ddp_mod.clip_and_step(dm, opt, 1.0)
         torch.cuda.synchronize()
         assert abs(nd.item() - nr.item()) < 2e-3 * nr.item(), (rep, nd.item(), nr.item())
@@ -127,7 +146,8 @@ def run_optim(a, rank, world, ref, model, data, loss_fn):
             if rep == 0:
                 assert d.abs().max().item() < 1e-5, (rep, k, d.abs().max().item())
         assert worst < 3e-3 and frac < 1e-2, (rep, worst, frac)
-        print(f"rank {rank} step {rep}: optim folded_average={getattr(opt, 'fold_average', None)} grad_norm {nd.item():.4f} vs "
+        print(f"rank {rank} step {rep}: optim={type(opt).__name__} deferred_average={deferred} "
+              f"logged_norm={None if logged is None else round(logged.item(), 4)} grad_norm {nd.item():.4f} vs "
               f"{nr.item():.4f} rel_param_diff={worst:.2e} frac_off={frac:.1e}", flush=True)
     dist.destroy_process_group()
     print(f"rank {rank} OK", flush=True)

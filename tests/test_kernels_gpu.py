@@ -940,7 +940,8 @@ def test_microbatch_overlap_is_bitwise_identical(cuda, layer):
     # the 8-GPU per-rank regime (accum 2: forward 0 on the second stream) and the degenerate accum 1
     ("Mamba2", "fp32", 2, "native"), ("Mamba2", "fp32", 1, "native"), ("Mamba1", "fp32", 2, "native"),
     ("Mamba2", "fp32", 2, "ddp"), ("Mamba2", "fp32", 1, "ddp"),
-    # three optimizer steps through clip_and_step: the native AdamW with the reducer's average folded in
+    # four optimizer steps through clip_and_step: the native AdamW dividing the deferred average, a logged norm, then
+    # a torch AdamW loaded from its state_dict
     ("Mamba2", "fp32", 1, "optim"), ("Mamba1", "fp32", 2, "optim")])
 def test_native_reducer_two_ranks_one_gpu(cuda, layer, comm, accum, impl):
     """parallel/reducer.py (and torch DDP) on real HIP streams: two gloo ranks on cuda:0, overlapped

@@ -57,20 +57,41 @@ def test_native_adamw_matches_torch(clip):
         assert float(sa["step"]) == float(sb["step"]) == 5.0
 
 
+def test_native_adamw_nan_gradient_poisons_like_torch():
+    """A NaN gradient element makes the total norm NaN; torch's clip_grad_norm_ then multiplies EVERY gradient by a
+    NaN coefficient (clamp propagates it), so every parameter turns NaN after the step.  The native clip coefficient
+    must propagate it the same way (a loss-spike / NaN detector relies on it), not clamp NaN to 1."""
+    from mamba_distributed_amd.ops.optim import NativeAdamW
+    pn, pr = _params(), _params()
+    on = NativeAdamW(_groups(pn), lr=6e-4, betas=(0.9, 0.95), eps=1e-8)
+    orf = torch.optim.AdamW(_groups(pr), lr=6e-4, betas=(0.9, 0.95), eps=1e-8)
+    _grads(pn, 0)
+    _grads(pr, 0)
+    pn[0].grad[3, 5] = float("nan")
+    pr[0].grad[3, 5] = float("nan")
+    nn_ = on.clip_and_step(1.0)
+    nr = torch.nn.utils.clip_grad_norm_(pr, 1.0)
+    orf.step()
+    assert math.isnan(nn_.item()) and math.isnan(nr.item())
+    for a, b in zip(pn, pr):
+        assert torch.isnan(b).all()
+        assert torch.isnan(a).all(), (a.shape, torch.isnan(a).float().mean().item())
+
+
 def test_native_adamw_fold_average():
-    """Gradients summed over `world` ranks with fold_average = world update exactly like averaged gradients."""
+    """Gradients summed over `world` ranks, stepped with grad_divisor = world, update exactly like averaged gradients
+    (the divisor is an explicit per-call argument: the native reducer's grad_divisor, parallel/ddp.py)."""
     from mamba_distributed_amd.ops.optim import NativeAdamW
     pa, pb = _params(3), _params(3)
     oa = NativeAdamW(_groups(pa), lr=1e-3, betas=(0.9, 0.95))
     ob = NativeAdamW(_groups(pb), lr=1e-3, betas=(0.9, 0.95))
-    ob.fold_average = 8.0
     for step in range(3):
         _grads(pa, step)
         _grads(pb, step)
         for p in pb:
             p.grad.mul_(8.0)
         na = oa.clip_and_step(1.0)
-        nb = ob.clip_and_step(1.0)
+        nb = ob.clip_and_step(1.0, grad_divisor=8.0)
         assert abs(na.item() - nb.item()) <= 1e-5 * na.item()
     for a, b in zip(pa, pb):
         assert torch.allclose(a, b, rtol=1e-6, atol=1e-7)
