@@ -246,8 +246,10 @@ __global__ __launch_bounds__(256) void ssd_fused_fwd_k(SSDArgs a, unsigned long 
       pb.t[i].load(bg + (int64_t)c * Q * a.sBl + 64 * i, a.sBl, valid);
       pc.t[i].load(cg + (int64_t)c * Q * a.sCl + 64 * i, a.sCl, valid);
     }
-    pcum = cumbh[c * Q + (threadIdx.x & 63)];
-    pdt = dtbh[c * Q + (threadIdx.x & 63)];
+    if (w == 0) {  // only the staging wave uses them (a wave-uniform branch: no load in the other three)
+      pcum = cumbh[c * Q + l];
+      pdt = dtbh[c * Q + l];
+    }
   };
   // Y rows of one chunk, staged in Os by the wave that owns them (no block barrier needed)
   auto store_y_rows = [&](int cc) {
