@@ -1,4 +1,4 @@
-"""parallel/reducer.py bucket layout: the small parameters (norm weights, conv taps, A_log / D / dt_bias) are laid
+"""parallel/reducer.py bucket layout: the small non-matrix parameters (norm weights, conv taps, A_log / D / dt_bias) are laid
 out last in buckets of their own, which the per-parameter hooks never launch -- finish() does, after the batched
 late column sums wrote their gradients (ops/grad_accum.py::flush_late).  Single-rank gloo on the CPU."""
 import socket
@@ -8,7 +8,7 @@ import torch
 import torch.distributed as dist
 
 from mamba_distributed_amd import LMHeadModel, MambaConfig
-from mamba_distributed_amd.parallel.reducer import GradReducer
+from mamba_distributed_amd.parallel.reducer import GradReducer, held_param
 
 
 @pytest.fixture
@@ -28,8 +28,8 @@ def test_small_parameters_last_and_held(gloo_world1, layer):
     m = LMHeadModel(MambaConfig(d_model=256, n_layer=2, vocab_size=1024, ssm_cfg={"layer": layer}))
     r = GradReducer(m, bucket_cap_mb=0.5)
     params = [p for p in m.parameters() if p.requires_grad]
-    small = [p for p in params if p.numel() < r.SMALL_NUMEL]
-    big = [p for p in params if p.numel() >= r.SMALL_NUMEL]
+    small = [p for p in params if held_param(p)]  # small non-matrix parameters (Mamba-1's 2-D x_proj is not held)
+    big = [p for p in params if not held_param(p)]
     assert small and big
     assert max(r._offset[id(p)] for p in big) < min(r._offset[id(p)] for p in small)
     held = r._held_from
