@@ -421,12 +421,25 @@ void ssd_common(mamba_amd::SSDArgs& a, const Tensor& x, const Tensor& dt, const 
               Bm.stride(2) % 8 == 0 && Cm.stride(2) % 8 == 0, "B/C rows must be 16-B aligned");
   a.nc = (a.L + 63) / 64; a.Lp = a.nc * 64;
   a.HG = pick_hg(a.B, a.nc, a.H, a.G); a.nhg = a.H / a.HG;
+  a.nseg = mamba_amd::ssd_pick_segments(a.B, a.H, a.nc);
+  a.cps = (a.nc + a.nseg - 1) / a.nseg;
+  a.nseg = (a.nc + a.cps - 1) / a.cps;  // no empty segment
   a.x = (const mamba_amd::bf16_t*)x.data_ptr(); a.sxb = x.stride(0); a.sxl = x.stride(1); a.sxh = x.stride(2);
   a.dt = dt.data_ptr(); a.dt_dtype = dcode(dt.scalar_type());
   a.sdtb = dt.stride(0); a.sdtl = dt.stride(1); a.sdth = dt.stride(2);
   a.Bm = (const mamba_amd::bf16_t*)Bm.data_ptr(); a.sBb = Bm.stride(0); a.sBl = Bm.stride(1); a.sBg = Bm.stride(2);
   a.Cm = (const mamba_amd::bf16_t*)Cm.data_ptr(); a.sCb = Cm.stride(0); a.sCl = Cm.stride(1); a.sCg = Cm.stride(2);
   a.softplus = softplus; a.dt_min = (float)dt_min; a.dt_max = (float)dt_max;
+}
+
+// the segment-parallel walks' workspace: (b, h, nseg - 1) fp32 states and their decays (none for one segment)
+Tensor ssd_seg_workspace(mamba_amd::SSDArgs& a, const Tensor& like) {
+  if (a.nseg < 2) return Tensor();
+  const int64_t n = (int64_t)a.B * a.H * (a.nseg - 1);
+  auto ws = at::empty({n * 64 * a.N + n}, like.options().dtype(at::kFloat));
+  a.seg = ws.data_ptr<float>();
+  a.segd = a.seg + n * 64 * a.N;
+  return ws;
 }
 
 // fp32 sequential SSD forward (evaluation in fp32): x (b,l,h,64), dt (b,l,h), B/C (b,l,g,n) fp32
@@ -498,6 +511,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> ssd_fwd(Tensor x, Tensor dt, 
   a.dtp = dtp.data_ptr<float>(); a.cum = cum.data_ptr<float>();
   a.states = (mamba_amd::bf16_t*)states.data_ptr(); a.final_state = final_.data_ptr<float>();
   a.y = (mamba_amd::bf16_t*)y.data_ptr(); a.syb = y.stride(0); a.syl = y.stride(1); a.syh = y.stride(2);
+  Tensor seg_ws = ssd_seg_workspace(a, x);
   HIPCHK(mamba_amd::launch_ssd_fwd(a, cur_stream()));
   return {y, cum, dtp, states, final_};
 }
@@ -567,6 +581,7 @@ std::vector<Tensor> ssd_bwd(Tensor dy, Tensor x, Tensor dt, Tensor A, Tensor Bm,
   a.psl = 3 * a.H;
   a.part_dA = part_small.data_ptr<float>(); a.part_dD = a.part_dA + a.H; a.part_dbias = a.part_dA + 2 * a.H;
   a.a_log = A_is_log;
+  Tensor seg_ws = ssd_seg_workspace(a, x);
   HIPCHK(mamba_amd::launch_ssd_bwd(a, cur_stream()));
   if (!pm.reduce) return {dx, ddt, at::empty({0}, fo), dB, dC, at::empty({0}, fo), at::empty({0}, fo), dinit};
   auto sums = at::empty({3, a.H}, fo);  // deterministic column sums over the (b, chunk) rows
@@ -1052,6 +1067,15 @@ void ssd_stamps(optional<Tensor> buf) {
   }
 }
 
+// segment-parallel SSD walks: n >= 0 sets the process override (0 = automatic, kernels/ssd.hip), n < 0 leaves it;
+// returns the segment count a (B, H, nc) walk gets
+int64_t ssd_segments(int64_t n, int64_t B, int64_t H, int64_t nc) {
+  if (n >= 0) mamba_amd::set_ssd_segments((int)n);
+  const int s = mamba_amd::ssd_pick_segments((int)B, (int)H, (int)nc);
+  const int cps = ((int)nc + s - 1) / s;
+  return ((int)nc + cps - 1) / cps;
+}
+
 // split-K GEMM engine workgroup shape (8 or 4 waves); w <= 0 only reads it
 int64_t gp_waves(int64_t w) {
   if (w > 0) mamba_amd::set_gemm_pipe_waves((int)w);
@@ -1261,6 +1285,7 @@ TORCH_LIBRARY(mamba_amd, m) {
   m.def("gp_waves(int w=0) -> int", &gp_waves);
   m.def("gp_wg_nb(int nb=-1) -> int", &gp_wg_nb);
   m.def("ssd_stamps(Tensor? buf) -> ()", &ssd_stamps);
+  m.def("ssd_segments(int n, int B, int H, int nc) -> int", &ssd_segments);
   m.def("gp_splits(int M, int N, int K) -> int", &gp_splits);
   m.def("part_rows(str kind, int a, int b=0) -> int", &part_rows);
   m.def("gp_reduce(Tensor part, Tensor(a!) out, bool accumulate=False) -> ()");

@@ -40,7 +40,18 @@ struct SSDArgs {
   float* part_db;         // (b, nc, nhg, 64, N)
   float* part_dc;         // (b, nc, nhg, 64, N)
   float* part_dA; float* part_dD; float* part_dbias;  // (b, nc, h)
+  // segment-parallel state walks (small b * H): the chunks split into nseg segments of cps chunks; the forward's
+  // and the reverse walk's workgroups run one (h, b, segment) each from a carried-in state that a state-only pass
+  // per segment plus a (b, h) combine produced.  nseg = 1, cps = nc: one walk per (h, b) over every chunk.
+  int nseg, cps;
+  float* seg;             // (b, h, nseg - 1, p, n) fp32: per-segment local states, then the carried-in states
+  float* segd;            // (b, h, nseg - 1): the summed log-decay of each segment
 };
+
+// segments for a state walk over nc chunks at B * H (h, b) pairs: 1 unless a split fills the CUs better
+// (set_ssd_segments(n > 0) forces n, clamped to nc; 0 = automatic)
+int ssd_pick_segments(int B, int H, int nc);
+void set_ssd_segments(int n);
 
 // fp32 sequential SSD forward (evaluation in fp32, e.g. the reference's HellaSwag protocol); P = 64,
 // N = 64 / 128, no varlen.  Outputs y (b, l, h, p) and optionally the final state (b, h, p, n).

@@ -19,6 +19,7 @@
 //                   stay in registers across the heads of the group (no per-head HBM round trip).
 //   ssd_dbc_bwd     WG per (chunk, group, b): dC = sum dC_off + dCB B ; dB = sum dB_off + dCB^T C.
 // No float atomics on global memory: every cross-workgroup sum goes through fixed-order partials.
+#include <algorithm>
 #include <cstdlib>
 
 #include "mfma.h"
@@ -215,10 +216,15 @@ __global__ __launch_bounds__(256) void ssd_fused_fwd_k(SSDArgs a, unsigned long 
   __shared__ __attribute__((aligned(16))) bf16_t Xs[Q * LD64];
   __shared__ __attribute__((aligned(16))) bf16_t Os[Q * LDY];
   __shared__ __attribute__((aligned(16))) float cumr[Q], dtr[Q], wjr[Q];  // wjr = e^{cl-cum_j} dt_j
-  const int h = blockIdx.x, b = blockIdx.y;
+  const int h = blockIdx.x, b = blockIdx.y, sg = blockIdx.z;  // segment sg: chunks [c0, c1)
+  const int c0 = sg * a.cps, c1 = min(a.nc, c0 + a.cps);
   const int g = h / (a.H / a.G);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;  // wave-uniform: scalar branches
   const int li = l & 15, lg = l >> 4;
+  const int64_t bh = (int64_t)b * a.H + h;
+  // the state entering the segment: initial_states for the first, the combined carry (ssd_seg_combine_k) after
+  const float* ini = sg == 0 ? (a.init ? a.init + bh * P * N : nullptr)
+                             : a.seg + (bh * (a.nseg - 1) + sg - 1) * P * N;
   const float* cumbh = a.cum + ((int64_t)b * a.H + h) * a.Lp;
   const float* dtbh = a.dtp + ((int64_t)b * a.H + h) * a.Lp;
   const bf16_t* xg = a.x + (int64_t)b * a.sxb + (int64_t)h * a.sxh;
@@ -229,10 +235,9 @@ __global__ __launch_bounds__(256) void ssd_fused_fwd_k(SSDArgs a, unsigned long 
 #pragma unroll
   for (int nt = 0; nt < NTS; ++nt) {
     st[nt] = zero4();
-    if (a.init) {
+    if (ini) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        st[nt][r] = a.init[(((int64_t)b * a.H + h) * P + 16 * w + 4 * lg + r) * N + 16 * nt + li];
+      for (int r = 0; r < 4; ++r) st[nt][r] = ini[(16 * w + 4 * lg + r) * N + 16 * nt + li];
     }
   }
   Tile64<256> px;
@@ -260,9 +265,9 @@ __global__ __launch_bounds__(256) void ssd_fused_fwd_k(SSDArgs a, unsigned long 
       *reinterpret_cast<uint4*>(yg + 8) = *reinterpret_cast<const uint4*>(Os + row * LDY + col + 8);
     }
   };
-  prefetch(0);
+  prefetch(c0);
   SSD_STAMP_INIT
-  for (int c = 0; c < a.nc; ++c) {
+  for (int c = c0; c < c1; ++c) {
     __syncthreads();  // chunk c-1 is fully consumed
     SSD_STAMP(0)
     px.store(Xs, LD64);
@@ -281,18 +286,18 @@ __global__ __launch_bounds__(256) void ssd_fused_fwd_k(SSDArgs a, unsigned long 
     // ---- global stores BEFORE the prefetch loads: vmcnt counts stores too and completes in order,
     // so the wait for chunk c+1's operands at the next loop top must not also wait for stores issued
     // at the end of this chunk.  Y rows of chunk c-1 (staged in Os by this same wave), then S_c.
-    if (c > 0) store_y_rows(c - 1);
+    if (c > c0) store_y_rows(c - 1);
     {
-      bf16_t* sg = a.states + ((((int64_t)b * a.nc + c) * a.H + h) * P) * N;
+      bf16_t* sgp = a.states + ((((int64_t)b * a.nc + c) * a.H + h) * P) * N;
 #pragma unroll
       for (int q = 0; q < N / 64; ++q) {
         const int row = 16 * w + (l >> 2), col = 64 * q + 16 * (l & 3);
-        *reinterpret_cast<uint4*>(sg + (int64_t)row * N + col) = *reinterpret_cast<const uint4*>(Ss + row * LDN + col);
-        *reinterpret_cast<uint4*>(sg + (int64_t)row * N + col + 8) =
+        *reinterpret_cast<uint4*>(sgp + (int64_t)row * N + col) = *reinterpret_cast<const uint4*>(Ss + row * LDN + col);
+        *reinterpret_cast<uint4*>(sgp + (int64_t)row * N + col + 8) =
             *reinterpret_cast<const uint4*>(Ss + row * LDN + col + 8);
       }
     }
-    if (c + 1 < a.nc) prefetch(c + 1);
+    if (c + 1 < c1) prefetch(c + 1);
     SSD_STAMP(3)
     const float cl = cumr[Q - 1];
     // ---- Y_off = e^{cum_i} C_i . S_c^T   (rows i of tile w, 4 p-tiles)
@@ -372,8 +377,8 @@ __global__ __launch_bounds__(256) void ssd_fused_fwd_k(SSDArgs a, unsigned long 
     SSD_STAMP(7)
   }
   SSD_STAMP_FLUSH(blockIdx.y * gridDim.x + blockIdx.x)
-  store_y_rows(a.nc - 1);
-  if (a.final_state) {
+  store_y_rows(c1 - 1);
+  if (a.final_state && sg == a.nseg - 1) {
 #pragma unroll
     for (int nt = 0; nt < NTS; ++nt)
 #pragma unroll
@@ -394,21 +399,26 @@ __global__ __launch_bounds__(256) void ssd_dstate_bwd_k(SSDArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t Cs[Q * LDN];
   __shared__ __attribute__((aligned(16))) bf16_t Os[P * LDO];
   __shared__ float er[Q];
-  const int h = blockIdx.x, b = blockIdx.y;
+  const int h = blockIdx.x, b = blockIdx.y, sg = blockIdx.z;  // segment sg: chunks [c0, c1), walked from c1 - 1
+  const int c0 = sg * a.cps, c1 = min(a.nc, c0 + a.cps);
   const int g = h / (a.H / a.G);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;  // wave-uniform: scalar branches
+  const int64_t bh = (int64_t)b * a.H + h;
   const float* cumbh = a.cum + ((int64_t)b * a.H + h) * a.Lp;
   const bf16_t* yg = a.dy + (int64_t)b * a.sdyb + (int64_t)h * a.sdyh;
   const bf16_t* cg = a.Cm + (int64_t)b * a.sCb + (int64_t)g * a.sCg;
+  // the gradient entering the segment from the right: dfinal for the last, the combined carry before
+  const float* ini = sg == a.nseg - 1 ? (a.dfinal ? a.dfinal + bh * P * N : nullptr)
+                                      : a.seg + (bh * (a.nseg - 1) + sg) * P * N;
   f32x4 acc[NTS];
 #pragma unroll
   for (int nt = 0; nt < NTS; ++nt) {
     acc[nt] = zero4();
-    if (a.dfinal) {
+    if (ini) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int p = 16 * w + 4 * (l >> 4) + r, n = 16 * nt + (l & 15);
-        acc[nt][r] = a.dfinal[(((int64_t)b * a.H + h) * P + p) * N + n];
+        acc[nt][r] = ini[p * N + n];
       }
     }
   }
@@ -423,8 +433,8 @@ __global__ __launch_bounds__(256) void ssd_dstate_bwd_k(SSDArgs a) {
     for (int i = 0; i < N / 64; ++i) pcs.t[i].load(cg + (int64_t)c * Q * a.sCl + 64 * i, a.sCl, valid);
     pe = cumbh[c * Q + (threadIdx.x & 63)];  // exp at use: no ALU on a value still in flight
   };
-  prefetch(a.nc - 1);
-  for (int c = a.nc - 1; c >= 0; --c) {
+  prefetch(c1 - 1);
+  for (int c = c1 - 1; c >= c0; --c) {
 #pragma unroll
     for (int nt = 0; nt < NTS; ++nt) acc_to_lds_pk(Os, LDO, 16 * w, 16 * nt, acc[nt]);
     if (threadIdx.x < Q) er[threadIdx.x] = __expf(pe);
@@ -435,7 +445,7 @@ __global__ __launch_bounds__(256) void ssd_dstate_bwd_k(SSDArgs a) {
     py.store(Ys, LD64, er);
     pcs.store(Cs, LDN);
     store_tile<P, N>(a.dstates + ((((int64_t)b * a.nc + c) * a.H + h) * P) * N, N, Os, LDO, P);
-    if (c > 0) prefetch(c - 1);
+    if (c > c0) prefetch(c - 1);
     __syncthreads();
 #pragma unroll
     for (int nt = 0; nt < NTS; ++nt) acc[nt] *= decay;
@@ -446,7 +456,7 @@ __global__ __launch_bounds__(256) void ssd_dstate_bwd_k(SSDArgs a) {
       for (int nt = 0; nt < NTS; ++nt) acc[nt] = mfma16(A, frag_tr(Cs, LDN, 32 * ks, 16 * nt), acc[nt]);
     }
   }
-  if (a.dinit) {
+  if (a.dinit && sg == 0) {
 #pragma unroll
     for (int nt = 0; nt < NTS; ++nt)
 #pragma unroll
@@ -454,6 +464,171 @@ __global__ __launch_bounds__(256) void ssd_dstate_bwd_k(SSDArgs a) {
         const int p = 16 * w + 4 * (l >> 4) + r, n = 16 * nt + (l & 15);
         a.dinit[(((int64_t)b * a.H + h) * P + p) * N + n] = acc[nt][r];
       }
+  }
+}
+
+// ============================== segment-parallel state walks (small b * H) ====================
+// At 2.8B / T = 8192 (b = 4, H = 80) the forward and reverse walks are 320 workgroups of 128 chunks on 256 CUs that
+// hold two of them each: the kernel time is one workgroup's serial walk.  With nseg segments of cps chunks:
+//   ssd_seg_state_k    (h, b, segment < nseg - 1): the segment's state contribution from a zero state,
+//                      S = e^{cl} S + (X o w)^T B per chunk (no y, no C, no per-chunk stores), and its summed
+//                      log-decay D = sum cl;
+//   ssd_seg_combine_k  (h, b): S_in(s + 1) = e^{D_s} S_in(s) + L_s carried through the segments (fp32, in place);
+//   ssd_fused_fwd_k    (h, b, segment): the full walk over the segment's chunks from S_in(segment).
+// The backward mirrors it: ssd_seg_dstate_k walks segments 1 .. nseg - 1 in reverse from zero, the combine carries
+// right to left, and ssd_dstate_bwd_k walks every segment from its carried-in gradient.  Exact in real arithmetic:
+// both recurrences are linear in the carried state and a segment's decay is the scalar e^{D} (A is per head).
+template <int N>
+__global__ __launch_bounds__(256) void ssd_seg_state_k(SSDArgs a) {
+  constexpr int LDN = N + 16, NTS = N / 16;
+  __shared__ __attribute__((aligned(16))) bf16_t Bs[Q * LDN];
+  __shared__ __attribute__((aligned(16))) bf16_t Xs[Q * LD64];
+  __shared__ __attribute__((aligned(16))) float wjr[Q];
+  const int h = blockIdx.x, b = blockIdx.y, sg = blockIdx.z;
+  const int c0 = sg * a.cps, c1 = min(a.nc, c0 + a.cps);
+  const int g = h / (a.H / a.G);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
+  const int li = l & 15, lg = l >> 4;
+  const int64_t bh = (int64_t)b * a.H + h;
+  const float* cumbh = a.cum + bh * a.Lp;
+  const float* dtbh = a.dtp + bh * a.Lp;
+  const bf16_t* xg = a.x + (int64_t)b * a.sxb + (int64_t)h * a.sxh;
+  const bf16_t* bg = a.Bm + (int64_t)b * a.sBb + (int64_t)g * a.sBg;
+  f32x4 st[NTS];
+#pragma unroll
+  for (int nt = 0; nt < NTS; ++nt) st[nt] = zero4();
+  Tile64<256> px;
+  TileState<256, N> pb;
+  float pcum = 0.f, pdt = 0.f;
+  auto prefetch = [&](int c) {
+    const int valid = min(Q, a.L - c * Q);
+    px.load(xg + (int64_t)c * Q * a.sxl, a.sxl, valid);
+#pragma unroll
+    for (int i = 0; i < N / 64; ++i) pb.t[i].load(bg + (int64_t)c * Q * a.sBl + 64 * i, a.sBl, valid);
+    pcum = cumbh[c * Q + l];
+    pdt = dtbh[c * Q + l];
+  };
+  float dsum = 0.f;
+  prefetch(c0);
+  for (int c = c0; c < c1; ++c) {
+    __syncthreads();  // chunk c-1 is consumed
+    px.store(Xs, LD64);
+    pb.store(Bs, LDN);
+    const float cl = __shfl(pcum, Q - 1, 64);
+    if (w == 0) wjr[l] = __expf(cl - pcum) * pdt;
+    __syncthreads();
+    if (c + 1 < c1) prefetch(c + 1);
+    dsum += cl;
+    const float decay = __expf(cl);
+#pragma unroll
+    for (int nt = 0; nt < NTS; ++nt) st[nt] *= decay;
+#pragma unroll
+    for (int ks = 0; ks < Q / 32; ++ks) {
+      bf16x8 A = frag_tr(Xs, LD64, 32 * ks, 16 * w);
+      const float4 w0 = *reinterpret_cast<const float4*>(&wjr[32 * ks + 8 * lg]);
+      const float4 w1 = *reinterpret_cast<const float4*>(&wjr[32 * ks + 8 * lg + 4]);
+      const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) A[jj] = (__bf16)((float)A[jj] * wv[jj]);
+#pragma unroll
+      for (int nt = 0; nt < NTS; ++nt) st[nt] = mfma16(A, frag_tr(Bs, LDN, 32 * ks, 16 * nt), st[nt]);
+    }
+  }
+  float* out = a.seg + (bh * (a.nseg - 1) + sg) * P * N;
+#pragma unroll
+  for (int nt = 0; nt < NTS; ++nt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) out[(16 * w + 4 * lg + r) * N + 16 * nt + li] = st[nt][r];
+  if (threadIdx.x == 0) a.segd[bh * (a.nseg - 1) + sg] = dsum;
+}
+
+// reverse walk of segment blockIdx.z + 1 from a zero gradient: dS = e^{cl} dS + (e^{cum} dY)^T C per chunk
+template <int N>
+__global__ __launch_bounds__(256) void ssd_seg_dstate_k(SSDArgs a) {
+  constexpr int LDN = N + 16, NTS = N / 16;
+  __shared__ __attribute__((aligned(16))) bf16_t Ys[Q * LD64];
+  __shared__ __attribute__((aligned(16))) bf16_t Cs[Q * LDN];
+  __shared__ float er[Q];
+  const int h = blockIdx.x, b = blockIdx.y, sg = blockIdx.z + 1;
+  const int c0 = sg * a.cps, c1 = min(a.nc, c0 + a.cps);
+  const int g = h / (a.H / a.G);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
+  const int64_t bh = (int64_t)b * a.H + h;
+  const float* cumbh = a.cum + bh * a.Lp;
+  const bf16_t* yg = a.dy + (int64_t)b * a.sdyb + (int64_t)h * a.sdyh;
+  const bf16_t* cg = a.Cm + (int64_t)b * a.sCb + (int64_t)g * a.sCg;
+  f32x4 acc[NTS];
+#pragma unroll
+  for (int nt = 0; nt < NTS; ++nt) acc[nt] = zero4();
+  Tile64<256> py;
+  TileState<256, N> pcs;
+  float pe = 0.f, pl = 0.f;
+  auto prefetch = [&](int c) {
+    pl = cumbh[c * Q + Q - 1];
+    const int valid = min(Q, a.L - c * Q);
+    py.load(yg + (int64_t)c * Q * a.sdyl, a.sdyl, valid);
+#pragma unroll
+    for (int i = 0; i < N / 64; ++i) pcs.t[i].load(cg + (int64_t)c * Q * a.sCl + 64 * i, a.sCl, valid);
+    pe = cumbh[c * Q + l];
+  };
+  float dsum = 0.f;
+  prefetch(c1 - 1);
+  for (int c = c1 - 1; c >= c0; --c) {
+    __syncthreads();  // chunk c+1 is consumed (Ys, Cs and er)
+    if (threadIdx.x < Q) er[threadIdx.x] = __expf(pe);
+    const float cl = pl;
+    __syncthreads();
+    py.store(Ys, LD64, er);
+    pcs.store(Cs, LDN);
+    if (c > c0) prefetch(c - 1);
+    __syncthreads();
+    dsum += cl;
+    const float decay = __expf(cl);
+#pragma unroll
+    for (int nt = 0; nt < NTS; ++nt) acc[nt] *= decay;
+#pragma unroll
+    for (int ks = 0; ks < Q / 32; ++ks) {
+      const bf16x8 A = frag_tr(Ys, LD64, 32 * ks, 16 * w);
+#pragma unroll
+      for (int nt = 0; nt < NTS; ++nt) acc[nt] = mfma16(A, frag_tr(Cs, LDN, 32 * ks, 16 * nt), acc[nt]);
+    }
+  }
+  float* out = a.seg + (bh * (a.nseg - 1) + sg - 1) * P * N;
+#pragma unroll
+  for (int nt = 0; nt < NTS; ++nt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) out[(16 * w + 4 * (l >> 4) + r) * N + 16 * nt + (l & 15)] = acc[nt][r];
+  if (threadIdx.x == 0) a.segd[bh * (a.nseg - 1) + sg - 1] = dsum;
+}
+
+// (h, b): carry the segment states through the segments in place.  fwd: slot s holds L_s (segment s's local state,
+// decay D_s) and becomes S_in(s + 1), starting from initial_states; bwd: slot s holds segment s + 1's local gradient
+// (decay D_{s+1}) and becomes the gradient entering segment s from the right, starting from dfinal.
+constexpr int SEG_MAX = 16;
+__global__ __launch_bounds__(256) void ssd_seg_combine_k(SSDArgs a, int fwd) {
+  const int h = blockIdx.x, b = blockIdx.y;
+  const int64_t bh = (int64_t)b * a.H + h;
+  const int ns = a.nseg - 1, PN = P * a.N;
+  float* base = a.seg + bh * ns * PN;
+  const float* dec = a.segd + bh * ns;
+  const float* first = fwd ? a.init : a.dfinal;
+  float d[SEG_MAX];
+#pragma unroll
+  for (int k = 0; k < SEG_MAX; ++k) d[k] = k < ns ? __expf(dec[fwd ? k : ns - 1 - k]) : 0.f;
+  for (int e = 4 * threadIdx.x; e < PN; e += 4 * 256) {
+    float4 v[SEG_MAX];
+#pragma unroll
+    for (int k = 0; k < SEG_MAX; ++k)
+      if (k < ns) v[k] = *reinterpret_cast<const float4*>(base + (int64_t)(fwd ? k : ns - 1 - k) * PN + e);
+    float4 cy = first ? *reinterpret_cast<const float4*>(first + bh * PN + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int k = 0; k < SEG_MAX; ++k) {
+      if (k < ns) {
+        cy = make_float4(fmaf(d[k], cy.x, v[k].x), fmaf(d[k], cy.y, v[k].y), fmaf(d[k], cy.z, v[k].z),
+                         fmaf(d[k], cy.w, v[k].w));
+        *reinterpret_cast<float4*>(base + (int64_t)(fwd ? k : ns - 1 - k) * PN + e) = cy;
+      }
+    }
   }
 }
 
@@ -1004,9 +1179,58 @@ hipError_t launch_ssd_fwd_f32(const SSDF32Args& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+static int g_ssd_nseg = -1;  // < 0: read MAMBA_AMD_SSD_SEG once; 0: automatic; n: forced
+void set_ssd_segments(int n) { g_ssd_nseg = n < 0 ? 0 : n; }
+
+int ssd_pick_segments(int B, int H, int nc) {
+  if (g_ssd_nseg < 0) {
+    const char* e = getenv("MAMBA_AMD_SSD_SEG");
+    g_ssd_nseg = e ? std::max(0, atoi(e)) : 0;
+  }
+  if (g_ssd_nseg > 0) return std::max(1, std::min({g_ssd_nseg, nc, SEG_MAX}));
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        ncu <= 0)
+      ncu = 256;
+  }
+  // Measured on MI355X (profiles/r6/ssd_segments.txt): with b * H >= the CU count every CU already runs a walk and
+  // splitting does not pay (2.8B at T = 8192, b * H = 320: forward -6% at 4 segments, reverse walk +2%, worse beyond);
+  // with fewer walks than CUs the chip idles and segments pay almost linearly (batch-1 prefill of 32k tokens at
+  // H = 24: forward 1552 -> 237 us, backward 1056 -> 406 us at 16 segments).  So: segments only below one walk per
+  // CU, as many as keep b * H * segments within two workgroups per CU and >= 4 chunks per segment.
+  const int64_t bh = (int64_t)B * H;
+  if (bh >= ncu) return 1;
+  int best = 1;
+  for (int s = 2; s <= SEG_MAX; ++s) {
+    const int cps = (nc + s - 1) / s, se = (nc + cps - 1) / cps;
+    if (cps < 4 || bh * se > 2LL * ncu) break;
+    best = se;
+  }
+  return best;
+}
+
+static hipError_t launch_seg_pass(const SSDArgs& a, bool fwd, hipStream_t st) {
+  if (a.nseg < 2) return hipSuccess;
+  if (a.nseg > SEG_MAX || !a.seg || !a.segd || (int64_t)(a.nseg - 1) * a.cps >= a.nc) return hipErrorInvalidValue;
+  const dim3 grid(a.H, a.B, a.nseg - 1);
+  if (fwd) N_SWITCH(a.N, hipLaunchKernelGGL(ssd_seg_state_k<NN>, grid, dim3(256), 0, st, a));
+  else N_SWITCH(a.N, hipLaunchKernelGGL(ssd_seg_dstate_k<NN>, grid, dim3(256), 0, st, a));
+  MAMBA_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(ssd_seg_combine_k, dim3(a.H, a.B), dim3(256), 0, st, a, fwd ? 1 : 0);
+  return hipGetLastError();
+}
+
 hipError_t launch_ssd_fwd(const SSDArgs& a, hipStream_t st) {
+  if (a.nseg < 1 || a.cps < 1 || (int64_t)a.nseg * a.cps < a.nc) return hipErrorInvalidValue;
   hipLaunchKernelGGL(ssd_cumsum_k, dim3((unsigned)((int64_t)a.B * a.nc)), dim3(256), 0, st, a);
   MAMBA_HIP_CHECK(hipGetLastError());
+  MAMBA_HIP_CHECK(launch_seg_pass(a, true, st));
+  if (a.nseg > 1) {
+    N_SWITCH(a.N, hipLaunchKernelGGL(ssd_fused_fwd_k<NN>, dim3(a.H, a.B, a.nseg), dim3(256), 0, st, a, nullptr));
+    return hipGetLastError();
+  }
   if (g_ssd_stamps && a.N == 128 && (int64_t)a.H * a.B * 8 <= g_ssd_stamps_n) {
     hipLaunchKernelGGL((ssd_fused_fwd_k<128, true>), dim3(a.H, a.B), dim3(256), 0, st, a, g_ssd_stamps,
                        g_ssd_stamp_wave & 3);
@@ -1017,7 +1241,9 @@ hipError_t launch_ssd_fwd(const SSDArgs& a, hipStream_t st) {
 }
 
 hipError_t launch_ssd_bwd(const SSDArgs& a, hipStream_t st) {
-  N_SWITCH(a.N, hipLaunchKernelGGL(ssd_dstate_bwd_k<NN>, dim3(a.H, a.B), dim3(256), 0, st, a));
+  if (a.nseg < 1 || a.cps < 1 || (int64_t)a.nseg * a.cps < a.nc) return hipErrorInvalidValue;
+  MAMBA_HIP_CHECK(launch_seg_pass(a, false, st));
+  N_SWITCH(a.N, hipLaunchKernelGGL(ssd_dstate_bwd_k<NN>, dim3(a.H, a.B, a.nseg), dim3(256), 0, st, a));
   MAMBA_HIP_CHECK(hipGetLastError());
   if (a.fuse_dbc && a.HG != a.H / a.G) return hipErrorInvalidValue;  // the fused finish needs the whole group
   if (g_ssd_stamps && a.N == 128 && ((int64_t)a.H * a.B + (int64_t)a.nc * a.nhg * a.B) * 8 <= g_ssd_stamps_n) {

@@ -299,6 +299,59 @@ def test_ssd_initial_and_final_states(cuda):
         assert rel(a, b_) < 3e-2
 
 
+@pytest.mark.parametrize("b,L,H,S", [(1, 8192, 8, 1), (1, 8192, 8, 2), (1, 8192, 8, 4),  # the 2.8B sequence length
+                                     (2, 1000, 8, 3), (2, 1000, 8, 16)])   # partial segments / chunk, 16 x 1 chunk
+def test_ssd_segment_parallel(cuda, b, L, H, S):
+    """Segment-parallel state walks (kernels/ssd.hip ssd_seg_state_k / ssd_seg_dstate_k / ssd_seg_combine_k): the
+    forward and reverse walks split into S segments from carried-in states, forced through the ssd_segments
+    override; y, the final state and every gradient (incl. initial_states and through the final state) against the
+    fp32 reference, and against the one-segment walk."""
+    from mamba_distributed_amd.ops import _ext
+    from mamba_distributed_amd.ops.ssd import mamba_chunk_scan_combined
+    ops = _ext.ops()
+    nc = (L + 63) // 64
+    x, dt, A, Bm, Cm, D, dt_bias = _ssd_inputs(cuda, b, L, H, 1, 128, seed=17)
+    # slow decay (a dt ~ -0.002 .. -0.008 per step): the carried-in state of a segment is far from negligible, so a
+    # wrong combine shows (with _ssd_inputs' A the state forgets within a chunk)
+    A = -(torch.rand(H, generator=torch.Generator(device=cuda).manual_seed(3), device=cuda) * 0.02 + 0.005)
+    init = torch.randn(b, H, 64, 128, device=cuda) * 0.2
+
+    def f(x, dt, Bm, Cm, init):
+        y, fin = mamba_chunk_scan_combined(x, dt, A, Bm, Cm, 64, D=D, dt_bias=dt_bias, dt_softplus=True,
+                                           initial_states=init, return_final_states=True)
+        return y.float().mean(-1) + fin.sum((-1, -2))[:, None, :].float() * 1e-2
+
+    try:
+        got = int(ops.ssd_segments(S, b, H, nc))
+        assert got == min(S, nc), got
+        on, orf, gn, gr = run_both(f, f, [x, dt, Bm, Cm, init])
+        ops.ssd_segments(1, b, H, nc)
+        xs = [leaf(t) for t in (x, dt, Bm, Cm, init)]
+        o1 = f(*xs)
+        o1.backward(torch.randn(o1.shape, generator=torch.Generator(device=cuda).manual_seed(0), device=cuda))
+    finally:
+        ops.ssd_segments(0, 1, 1, 1)
+    assert rel(on, orf) < 2e-2, rel(on, orf)
+    assert rel(on, o1) < 5e-3, rel(on, o1)
+    for nm, a, b_, c in zip(["x", "dt", "B", "C", "init"], gn, gr, [t.grad for t in xs]):
+        assert rel(a, b_) < 3e-2, (nm, rel(a, b_))
+        assert rel(a, c) < 1e-2, (nm, rel(a, c))
+
+
+def test_ssd_segments_auto_pick(cuda):
+    """The automatic segment count: one walk per (h, b) whenever b * H fills the CUs (every BASELINE training shape),
+    a split below that (batch-1 / small-batch long prefill)."""
+    from mamba_distributed_amd.ops import _ext
+    ops = _ext.ops()
+    ops.ssd_segments(0, 1, 1, 1)
+    assert ops.ssd_segments(-1, 64, 24, 16) == 1      # 280M, micro-batch 64 x 1024
+    assert ops.ssd_segments(-1, 32, 48, 16) == 1      # 1.4B, micro-batch 32 x 1024
+    assert ops.ssd_segments(-1, 4, 80, 128) == 1      # 2.8B, micro-batch 4 x 8192: 320 walks, splitting measured no gain
+    assert ops.ssd_segments(-1, 1, 24, 512) == 16     # batch-1 prefill of 32k tokens: 24 walks on 256 CUs
+    assert ops.ssd_segments(-1, 1, 8, 128) == 16
+    assert ops.ssd_segments(-1, 2, 80, 128) == 3      # <= 2 workgroups per CU
+
+
 def test_ssd_deterministic(cuda):
     from mamba_distributed_amd.ops.ssd import mamba_chunk_scan_combined
     x, dt, A, Bm, Cm, D, dt_bias = _ssd_inputs(cuda, 2, 256, 8, 1, 128, seed=7)
