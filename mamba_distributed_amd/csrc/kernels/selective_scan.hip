@@ -1203,8 +1203,13 @@ __global__ __launch_bounds__(256) void selscan_bwd_sg_k(SelScanArgs a) {
   constexpr int N = 16, T = SGB_T, TH = SGB_T / 2;
   constexpr bool DTF = KS > 0;
   // per step and channel: dt, dt u, dout silu(z) (adjoint) and u, softplus', dout silu'(z) (finish)
-  __shared__ float dlS[T][65], duS[T][65], dyS[T][65], uS[T][65], sdS[T][65], gzS[T][65];
-  __shared__ __attribute__((aligned(16))) float sS[4][3][T][65];  // per wave: sum_n lam B, A lam a h, C h
+  // Rows of 64 channels, column c of step row t stored at c ^ sw(t): the step loops read / write a whole row (a
+  // permutation: conflict-free), the staging and finish passes touch (t = 8 hf + 2 sp + e, c = tid / 4), whose 32-lane
+  // groups then hit 32 distinct banks (a 65-float pitch put 2-3 lanes on a bank there, and a conflict-free pitch of 68
+  // would not fit two workgroups per CU)
+  __shared__ float dlS[T][64], duS[T][64], dyS[T][64], uS[T][64], sdS[T][64], gzS[T][64];
+  __shared__ __attribute__((aligned(16))) float sS[4][3][T][64];  // per wave: sum_n lam B, A lam a h, C h
+  auto sw = [](int t, int c) { return c ^ (8 * ((t >> 1) & 3)); };
   bf16_t* const xS = reinterpret_cast<bf16_t*>(&sS[0][0][0][0]);  // DTF: x_dbl tile [32 ceil(R / 32)][16]
   __shared__ __attribute__((aligned(16))) float BCs[4][T][8];  // per wave and step: B of its 4 states, C
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -1301,13 +1306,13 @@ __global__ __launch_bounds__(256) void selscan_bwd_sg_k(SelScanArgs a) {
         if (!DTF) {
           const float v = upk(nr[hf]) + sbias;
           const float dl = a.softplus ? softplus_fast(v) : v;
-          dlS[tl][sr] = dl;
-          duS[tl][sr] = dl * u;
-          sdS[tl][sr] = a.softplus ? sigmoid_fast(v) : 1.f;
+          dlS[tl][sw(tl, sr)] = dl;
+          duS[tl][sw(tl, sr)] = dl * u;
+          sdS[tl][sw(tl, sr)] = a.softplus ? sigmoid_fast(v) : 1.f;
         }
-        dyS[tl][sr] = zb ? go * (zz * sg) : go;
-        uS[tl][sr] = u;
-        gzS[tl][sr] = zb ? go * sg * (1.f + zz * (1.f - sg)) : 0.f;
+        dyS[tl][sw(tl, sr)] = zb ? go * (zz * sg) : go;
+        uS[tl][sw(tl, sr)] = u;
+        gzS[tl][sw(tl, sr)] = zb ? go * sg * (1.f + zz * (1.f - sg)) : 0.f;
       }
     }
     if (DTF && threadIdx.x < 2 * 32 * KS)
@@ -1327,9 +1332,9 @@ __global__ __launch_bounds__(256) void selscan_bwd_sg_k(SelScanArgs a) {
         const int ch = 16 * w + 4 * g16 + r4;
         const float v = acc[r4] + bias4[r4];
         const float dl = a.softplus ? softplus_fast(v) : v;
-        dlS[li][ch] = dl;
-        duS[li][ch] = dl * uS[li][ch];
-        sdS[li][ch] = a.softplus ? sigmoid_fast(v) : 1.f;
+        dlS[li][sw(li, ch)] = dl;
+        duS[li][sw(li, ch)] = dl * uS[li][sw(li, ch)];
+        sdS[li][sw(li, ch)] = a.softplus ? sigmoid_fast(v) : 1.f;
       }
       __syncthreads();  // every wave's channels of the tile are in dlS / duS / sdS
     }
@@ -1349,7 +1354,7 @@ __global__ __launch_bounds__(256) void selscan_bwd_sg_k(SelScanArgs a) {
       ss_f2 h[2] = {hst[0], hst[1]};
 #pragma unroll
       for (int t = 0; t < T; ++t) {
-        const float dl = dlS[t][lane], du = duS[t][lane];
+        const float dl = dlS[t][sw(t, lane)], du = duS[t][sw(t, lane)];
         ss_f2 Bv[2];
         ldB(t, Bv);
 #pragma unroll
@@ -1371,7 +1376,7 @@ __global__ __launch_bounds__(256) void selscan_bwd_sg_k(SelScanArgs a) {
 #pragma unroll
       for (int k = 1; k >= 0; --k) {
         const int t = t2 + k;
-        const float dl = dlS[t][lane], du = duS[t][lane], dy = dyS[t][lane];
+        const float dl = dlS[t][sw(t, lane)], du = duS[t][sw(t, lane)], dy = dyS[t][sw(t, lane)];
         ss_f2 s1 = ss_f2{0.f, 0.f}, s2 = s1, yy = s1;
         ss_f2 Bv[2], Cv[2];
         ldB(t, Bv);
@@ -1393,9 +1398,9 @@ __global__ __launch_bounds__(256) void selscan_bwd_sg_k(SelScanArgs a) {
           dA[p] = __builtin_elementwise_fma(t1, ss_f2{dl, dl}, dA[p]);
           x[p] = av * lam;
         }
-        sS[w][0][t][lane] = s1.x + s1.y;
-        sS[w][1][t][lane] = s2.x + s2.y;
-        sS[w][2][t][lane] = yy.x + yy.y;
+        sS[w][0][t][sw(t, lane)] = s1.x + s1.y;
+        sS[w][1][t][sw(t, lane)] = s2.x + s2.y;
+        sS[w][2][t][sw(t, lane)] = yy.x + yy.y;
       }
       float rb, rc;
       lane_sum8x2(cB, cC, rb, rc);
@@ -1412,13 +1417,14 @@ __global__ __launch_bounds__(256) void selscan_bwd_sg_k(SelScanArgs a) {
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         const int tl = TH * hf + 2 * sp + e;
-        const float S1 = (sS[0][0][tl][sr] + sS[1][0][tl][sr]) + (sS[2][0][tl][sr] + sS[3][0][tl][sr]);
-        const float S2 = (sS[0][1][tl][sr] + sS[1][1][tl][sr]) + (sS[2][1][tl][sr] + sS[3][1][tl][sr]);
-        const float Y = (sS[0][2][tl][sr] + sS[1][2][tl][sr]) + (sS[2][2][tl][sr] + sS[3][2][tl][sr]);
-        const float dl = dlS[tl][sr], dy = dyS[tl][sr], u = uS[tl][sr];
+        const int cs = sw(tl, sr);
+        const float S1 = (sS[0][0][tl][cs] + sS[1][0][tl][cs]) + (sS[2][0][tl][cs] + sS[3][0][tl][cs]);
+        const float S2 = (sS[0][1][tl][cs] + sS[1][1][tl][cs]) + (sS[2][1][tl][cs] + sS[3][1][tl][cs]);
+        const float Y = (sS[0][2][tl][cs] + sS[1][2][tl][cs]) + (sS[2][2][tl][cs] + sS[3][2][tl][cs]);
+        const float dl = dlS[tl][cs], dy = dyS[tl][cs], u = uS[tl][cs];
         o_du[e] = fmaf(dl, S1, sD * dy);
-        o_dd[e] = fmaf(u, S1, S2) * sdS[tl][sr];
-        o_dz[e] = gzS[tl][sr] * fmaf(sD, u, Y);
+        o_dd[e] = fmaf(u, S1, S2) * sdS[tl][cs];
+        o_dz[e] = gzS[tl][cs] * fmaf(sD, u, Y);
         dDp = fmaf(dy, u, dDp);
         dbp += o_dd[e];
       }
