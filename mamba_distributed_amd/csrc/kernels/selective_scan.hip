@@ -1287,10 +1287,15 @@ __global__ __launch_bounds__(256) void selscan_bwd_sg_k(SelScanArgs a) {
   ss_f2 x[2] = {ss_f2{0.f, 0.f}, ss_f2{0.f, 0.f}};  // adjoint carried into the step after the tile
   ss_f2 dA[2] = {ss_f2{0.f, 0.f}, ss_f2{0.f, 0.f}};
   float dDp = 0.f, dbp = 0.f;
-  // this lane's dB / dC totals (lane_sum8): state 4 w + ((lane >> 3) & 3), step t2 + (lane >> 5)
+  // this lane's dB / dC totals (lane_sum8x2): state 4 w + ((lane >> 3) & 3), step t2 + (lane >> 5)
+  // stored through buffer descriptors over the wave's 4 state rows: the lane part of the offset is one VGPR for the
+  // whole walk, the tile's step in an SGPR and the step pair's in the immediate (64-bit lane addresses were
+  // recomputed at every step pair)
   float* pdB = a.part_dB + (((int64_t)b * ndg + dg) * N + 4 * w) * a.L;
   float* pdC = a.part_dC + (((int64_t)b * ndg + dg) * N + 4 * w) * a.L;
-  const int opd = ((lane >> 3) & 3) * a.L + (lane >> 5);
+  const __amdgpu_buffer_rsrc_t rdB = __builtin_amdgcn_make_buffer_rsrc(pdB, (short)0, 16 * a.L, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rdC = __builtin_amdgcn_make_buffer_rsrc(pdC, (short)0, 16 * a.L, 0x00020000);
+  const int opd = 4 * (((lane >> 3) & 3) * a.L + (lane >> 5));
   fetch(ntile - 1);
   for (int tile = ntile - 1; tile >= 0; --tile) {
     const int t0 = tile * T;
@@ -1405,8 +1410,8 @@ __global__ __launch_bounds__(256) void selscan_bwd_sg_k(SelScanArgs a) {
       float rb, rc;
       lane_sum8x2(cB, cC, rb, rc);
       if ((lane & 7) == 0) {
-        pdB[t0 + t2 + opd] = rb;
-        pdC[t0 + t2 + opd] = rc;
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, rb), rdB, opd + 4 * t2, 4 * t0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, rc), rdC, opd + 4 * t2, 4 * t0, 0);
       }
     }
     __syncthreads();  // the 4 waves' sums over states of the tile are in LDS
