@@ -1147,6 +1147,9 @@ __global__ __launch_bounds__(256) void selscan_bwd_fast_k(SelScanArgs a) {
 // Per lane and step: 2 x (pk_mul, 2 exp, pk_mul, pk_fma) replay + 2 x (pk_mul, 2 exp, 11 pk ops) adjoint.
 // Deterministic: every partial has one writer and every sum a fixed order.
 constexpr int SGB_T = kSelScanCarrySG;  // backward tile = forward carry granularity
+#ifndef SGB_NAV
+#define SGB_NAV 16  // steps per tile whose exp(dt A) the replay keeps for the adjoint (all: 256 VGPRs, no spill; 8: -1.6%, 12: -2.8%, 16: -4..6% kernel time)
+#endif
 static_assert(SGB_T == SG_T, "the forward writes a carry at every one of its tiles");
 
 // v_permlane32_swap / v_permlane16_swap (inline asm: the clang builtins of this ROCm return the first
@@ -1354,7 +1357,11 @@ __global__ __launch_bounds__(256) void selscan_bwd_sg_k(SelScanArgs a) {
       o[1] = ss_f2{q.z, q.w};
     };
     // replay the tile from its saved state, keeping h_t of every step
+    // exp(dt A) of the last NAV steps is kept for the adjoint, which starts there (short-lived registers around the
+    // replay -> adjoint turn); the earlier steps' are recomputed
+    constexpr int NAV = SGB_NAV, TAV = T - NAV;
     ss_f2 hs[T][2];
+    ss_f2 avs[NAV > 0 ? NAV : 1][2];
     {
       ss_f2 h[2] = {hst[0], hst[1]};
 #pragma unroll
@@ -1368,6 +1375,7 @@ __global__ __launch_bounds__(256) void selscan_bwd_sg_k(SelScanArgs a) {
           const ss_f2 av = ss_f2{__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
           h[p] = __builtin_elementwise_fma(av, h[p], Bv[p] * du);
           hs[t][p] = h[p];
+          if (t >= TAV) avs[t >= TAV ? t - TAV : 0][p] = av;
         }
       }
     }
@@ -1388,8 +1396,13 @@ __global__ __launch_bounds__(256) void selscan_bwd_sg_k(SelScanArgs a) {
         ldC(t, Cv);
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
-          const ss_f2 e = A2[p] * dl;
-          const ss_f2 av = ss_f2{__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
+          ss_f2 av;
+          if (t >= TAV) {
+            av = avs[t >= TAV ? t - TAV : 0][p];
+          } else {
+            const ss_f2 e = A2[p] * dl;
+            av = ss_f2{__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
+          }
           const ss_f2 Bp = Bv[p], Cp = Cv[p];
           const ss_f2 lam = __builtin_elementwise_fma(Cp, ss_f2{dy, dy}, x[p]);
           const ss_f2 hp = t > 0 ? hs[t > 0 ? t - 1 : 0][p] : hst[p];
