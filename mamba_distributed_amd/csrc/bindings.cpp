@@ -1088,6 +1088,13 @@ int64_t gp_wg_nb(int64_t nb) {
   return mamba_amd::gemm_wg_nb();
 }
 
+// staged-ring KC operand images: 0 = 32-deep, 1 = paired 64-deep for wide KC operands, 2 = paired for every KC
+// operand; v < 0 only reads it
+int64_t gp_wg_kcpair(int64_t v) {
+  if (v >= 0) mamba_amd::set_gemm_wg_kcpair((int)v);
+  return mamba_amd::gemm_wg_kcpair();
+}
+
 int64_t wgrad_splits(int64_t M, int64_t P, int64_t Q) { return mamba_amd::gemm_wgrad_splits((int)M, (int)P, (int)Q); }
 int64_t gp_splits(int64_t M, int64_t N, int64_t K) { return mamba_amd::gemm_pipe_splits((int)M, (int)N, (int)K); }
 
@@ -1284,6 +1291,7 @@ TORCH_LIBRARY(mamba_amd, m) {
   m.def("gp_pk(Tensor A, Tensor B, Tensor(a!)? out=None, int la=0, int lb=0, int mode=0, Tensor? rowscale=None) -> Tensor");
   m.def("gp_waves(int w=0) -> int", &gp_waves);
   m.def("gp_wg_nb(int nb=-1) -> int", &gp_wg_nb);
+  m.def("gp_wg_kcpair(int v=-1) -> int", &gp_wg_kcpair);
   m.def("ssd_stamps(Tensor? buf) -> ()", &ssd_stamps);
   m.def("ssd_segments(int n, int B, int H, int nc) -> int", &ssd_segments);
   m.def("gp_splits(int M, int N, int K) -> int", &gp_splits);

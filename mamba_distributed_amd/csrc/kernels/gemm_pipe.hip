@@ -580,6 +580,296 @@ __global__ __launch_bounds__(512) void gemm_wg_k(GemmPipeArgs a) {
   }
 }
 
+// ---- staged-ring engine with PAIRED KC images (gemm_wg_kp_k) ----------------------------------------------------
+// gemm_wg_k for products with a KC operand: such an operand's 32-deep stage is a [rows][32 k] image of 64-B rows,
+// DMA'd as half cache lines (4 lanes per row), and the same product runs 1.2-1.5x slower than its XC form
+// (profiles/r6/wg_kc_pairs.txt).  Here a KC operand's stages 2j and 2j+1 share one [rows][64 k] image of 128-B
+// rows (gemm_pipe_k's KC layout: chunk c of row r at c ^ (r & 7)), filled by ONE DMA of whole row segments at the
+// odd stage that frees it; XC operands keep their per-stage images.  Everything else is gemm_wg_k.
+template <int LA, int LB, int EPI, int MI>
+__global__ __launch_bounds__(512) void gemm_wg_kp_k(GemmPipeArgs a) {
+  constexpr int NB = 4;
+  constexpr int NT = 512, WN = 4, NJ = 4, MH = MI / 2;
+  constexpr int BM = 32 * MI, BN = 256, BK = 32;
+  constexpr int SA = BM * BK * 2, SB = BN * BK * 2, SS = SA + SB;  // bytes per operand image / slot
+  constexpr int GA = BM / 128, GB = BN / 128, G = GA + GB;          // DMA instructions per thread per stage
+  constexpr int RA = LA ? 2 : 1, RB = LB ? 2 : 1;                   // LDS read instructions per fragment
+  constexpr bool PA = LA == 0, PB = LB == 0;  // paired (KC) operands
+  constexpr int GX = (PA ? 0 : GA) + (PB ? 0 : GB);  // per-stage DMA instructions
+  constexpr int GP = (PA ? GA : 0) + (PB ? GB : 0);  // per-stage share of the pair DMAs (2 GP at odd stages)
+  static_assert(GP > 0, "a KC operand");
+  static_assert(NB >= 3 && NB * SS <= 163840, "LDS");
+  __shared__ __attribute__((aligned(1024))) char smem[NB * SS];
+  // LDS map: [A images: NB x SA][B images: NB x SB]; a paired operand's stage positions 2q, 2q+1 share the
+  // 2 S-byte image q
+  auto offA = [](int p) -> unsigned { return PA ? (p >> 1) * 2 * SA : p * SA; };
+  auto offB = [](int p) -> unsigned { return NB * SA + (PB ? (p >> 1) * 2 * SB : p * SB); };
+
+  const int tn = (a.N + BN - 1) / BN, tm = (a.M + BM - 1) / BM;
+  const int nwg = tm * tn * a.splits;
+  const int t = xcd_remap(blockIdx.x, nwg);
+  const int split = t / (tm * tn), tile = t % (tm * tn);
+  const int m0 = (tile / tn) * BM, n0 = (tile % tn) * BN;
+  const int kbeg = split * a.kslice, kend = min(a.K, kbeg + a.kslice);
+  const int KT = (kend - kbeg + BK - 1) / BK;  // stages
+  const int KTF = (kend - kbeg) / BK;          // full stages
+  const int mvalid = min(BM, a.M - m0), nvalid = min(BN, a.N - n0);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, tid = threadIdx.x;
+  const int wr = w / WN, wc = w % WN;
+  const int am0 = wr * (BM / 2), bn0 = wc * (BN / WN);
+
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, (short)0, (int)a.nbA, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)a.B, (short)0, (int)a.nbB, 0x00020000);
+  // per-thread DMA byte offsets of stage 0 (32-bit, host-checked) and the per-stage step
+  // XC: instruction ii = half ii of [32 k][R]: k-row tid >> 4, chunk (tid & 15) swizzled on the source (rule 21)
+  // KC: instruction ii = rows 128 ii .. +127 of [R][32 k]: row (ii 512 + tid) >> 2, 16-B chunk (tid & 3) ^ kc32_swz
+  // KC pair: instruction ii = rows 64 ii .. +63 of [R][64 k]: row (ii 512 + tid) >> 3, chunk (tid & 7) ^ (row & 7)
+  auto off0 = [&](int L, bool pr, int ii, int base, int valid, int64_t ld) -> unsigned {
+    if (L == 1) {
+      const int kr = tid >> 4, sx = tid & 15;
+      return (unsigned)((((int64_t)kbeg + kr) * ld + base + min(ii * 128 + 8 * (sx ^ (2 * xc_swz(kr))), valid - 8)) * 2);
+    }
+    if (pr) {
+      const int r = (ii * NT + tid) >> 3, c = (tid & 7) ^ (r & 7);
+      return (unsigned)((((int64_t)base + r) * ld + kbeg + 8 * c) * 2);
+    }
+    const int r = (ii * NT + tid) >> 2, c = (tid & 3) ^ kc32_swz(r);
+    return (unsigned)((((int64_t)base + r) * ld + kbeg + 8 * c) * 2);
+  };
+  constexpr int NDA = PA ? 2 * GA : GA, NDB = PB ? 2 * GB : GB;
+  unsigned offAd[NDA], offBd[NDB];
+#pragma unroll
+  for (int ii = 0; ii < NDA; ++ii) offAd[ii] = off0(LA, PA, ii, m0, mvalid, a.lda);
+#pragma unroll
+  for (int ii = 0; ii < NDB; ++ii) offBd[ii] = off0(LB, PB, ii, n0, nvalid, a.ldb);
+  const unsigned stepA = LA ? (unsigned)(BK * a.lda * 2) : BK * 2u, stepB = LB ? (unsigned)(BK * a.ldb * 2) : BK * 2u;
+  // this thread's k offset inside a KC stage (all ii) / inside a KC stage pair
+  const int kchunk = 8 * ((tid & 7) ^ ((tid >> 3) & 7));
+  const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // per-stage DMA of the unpaired (XC) operands of stage s into position p
+  auto dma = [&](int s_, int p) {
+    const unsigned s = (unsigned)__builtin_amdgcn_readfirstlane(s_);
+    const unsigned ua = __builtin_amdgcn_readfirstlane(s * stepA), ub = __builtin_amdgcn_readfirstlane(s * stepB);
+    char* const bufA = smem + offA(p);
+    char* const bufB = smem + offB(p);
+    if constexpr (!PA) {
+#pragma unroll
+      for (int ii = 0; ii < GA; ++ii) {
+        const unsigned v = offAd[ii] + ua;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(bufA + ii * 8192 + wu * 1024), 16, v, 0, 0, 0);
+      }
+    }
+    if constexpr (!PB) {
+#pragma unroll
+      for (int ii = 0; ii < GB; ++ii) {
+        const unsigned v = offBd[ii] + ub;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(bufB + ii * 8192 + wu * 1024), 16, v, 0, 0, 0);
+      }
+    }
+  };
+  // the paired operands' stages s0 (even), s0 + 1 into the pair image at position p (p even); `chk`: k-chunks past
+  // kend get an out-of-range offset (zeros)
+  auto dma_pair = [&](int s0_, int p, bool chk) {
+    {
+      const unsigned s0 = (unsigned)__builtin_amdgcn_readfirstlane(s0_);
+      const unsigned ua = __builtin_amdgcn_readfirstlane(s0 * stepA), ub = __builtin_amdgcn_readfirstlane(s0 * stepB);
+      const bool dead = chk && kbeg + (int)s0 * BK + kchunk >= kend;
+      if constexpr (PA) {
+        char* const buf = smem + offA(p);
+#pragma unroll
+        for (int ii = 0; ii < 2 * GA; ++ii) {
+          const unsigned v = dead ? 0xFFFFFFF0u : offAd[ii] + ua;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(buf + ii * 8192 + wu * 1024), 16, v, 0, 0, 0);
+        }
+      }
+      if constexpr (PB) {
+        char* const buf = smem + offB(p);
+#pragma unroll
+        for (int ii = 0; ii < 2 * GB; ++ii) {
+          const unsigned v = dead ? 0xFFFFFFF0u : offBd[ii] + ub;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(buf + ii * 8192 + wu * 1024), 16, v, 0, 0, 0);
+        }
+      }
+    }
+  };
+
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = zero4();
+  bf16x8 alo[MH], ahi[MH], b0[NJ], b1[NJ];
+  // Fragment reads as in gemm_wg_k; a paired operand has one LDS address per k half (row blocks are immediates).
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  constexpr int NOA = LA ? MI : (PA ? 2 : 1), NOB = LB ? NJ : (PB ? 2 : 1);
+  unsigned oa[NOA], ob[NOB];
+#pragma unroll
+  for (int i = 0; i < NOA; ++i)
+    oa[i] = LA ? lds0 + ((am0 + 16 * i) >> 7) * (32 * 256) + lane_xc(am0 + 16 * i) : lds0 + am0 * 128 + lane_kc(i);
+#pragma unroll
+  for (int j = 0; j < NOB; ++j)
+    ob[j] = LB ? lds0 + ((bn0 + 16 * j) >> 7) * (32 * 256) + lane_xc(bn0 + 16 * j) : lds0 + bn0 * 128 + lane_kc(j);
+  auto rd_xc = [&](bf16x8& d, unsigned addr) {
+    u32x2 x, y;
+    asm volatile("ds_read_b64_tr_b16 %0, %2\n\tds_read_b64_tr_b16 %1, %2 offset:1024" : "=&v"(x), "=&v"(y) : "v"(addr));
+    d = __builtin_bit_cast(bf16x8, __builtin_shufflevector(x, y, 0, 1, 2, 3));
+  };
+  auto rd_kc = [&](bf16x8& d, unsigned addr, auto off) {
+    u32x4 x;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(x) : "v"(addr), "n"(decltype(off)::value));
+    d = __builtin_bit_cast(bf16x8, x);
+  };
+  // a stage position's image offsets (A / B) and k half (paired images)
+  struct Pos { unsigned sa, sb; int ks; };
+  auto pos = [&](int p) -> Pos { return Pos{offA(p), offB(p) - NB * SA, p & 1}; };
+  // fragment i of A (16 rows) / j of B (16 columns) of the stage at position q
+  auto fa = [&](bf16x8& d, auto I, const Pos& q) {
+    constexpr int i = decltype(I)::value;
+    if constexpr (LA) rd_xc(d, oa[i] + q.sa);
+    else rd_kc(d, (q.ks ? oa[1] : oa[0]) + q.sa, std::integral_constant<int, 2048 * i>{});
+  };
+  constexpr unsigned bbase = NB * SA;  // the B images' region
+  auto fb = [&](bf16x8& d, auto J, const Pos& q) {
+    constexpr int j = decltype(J)::value;
+    if constexpr (LB) rd_xc(d, ob[j] + bbase + q.sb);
+    else rd_kc(d, (q.ks ? ob[1] : ob[0]) + bbase + q.sb, std::integral_constant<int, 2048 * j>{});
+  };
+  auto lgkm = [](auto n) {  // fenced on both sides: no MFMA may cross it either way
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(decltype(n)::value) : "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto mm_lo = [&](bf16x8 (&bf)[NJ]) {
+#pragma unroll
+    for (int i = 0; i < MH; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = mfma16(bf[j], alo[i], acc[i][j]);
+  };
+  // compile-time loops over fragment indices (the asm immediates and register arrays need constants)
+  auto rd_ahi = [&](const Pos& q) {
+    [&]<int... I>(std::integer_sequence<int, I...>) {
+      (fa(ahi[I], std::integral_constant<int, MH + I>{}, q), ...);
+    }(std::make_integer_sequence<int, MH>{});
+  };
+  auto rd_lo = [&](const Pos& q, bf16x8 (&bn)[NJ]) {
+    [&]<int... I>(std::integer_sequence<int, I...>) {
+      (fa(alo[I], std::integral_constant<int, I>{}, q), ...);
+    }(std::make_integer_sequence<int, MH>{});
+    [&]<int... J>(std::integer_sequence<int, J...>) {
+      (fb(bn[J], std::integral_constant<int, J>{}, q), ...);
+    }(std::make_integer_sequence<int, NJ>{});
+  };
+  // mm_hi (ahi x bc) with the next stage's alo / bn reads spread between its MFMAs: one fragment per MFMA
+  auto mm_hi_rd = [&](bf16x8 (&bc)[NJ], bf16x8 (&bn)[NJ], const Pos& q, bool rd) {
+    [&]<int... Q>(std::integer_sequence<int, Q...>) {
+      ([&] {
+        constexpr int qq = Q, i = qq / NJ, j = qq % NJ;
+        if (rd) {
+          if constexpr (qq < MH) fa(alo[qq], std::integral_constant<int, qq>{}, q);
+          else if constexpr (qq < MH + NJ) fb(bn[qq - MH], std::integral_constant<int, qq - MH>{}, q);
+        }
+        acc[MH + i][j] = mfma16(bc[j], ahi[i], acc[MH + i][j]);
+        __builtin_amdgcn_sched_barrier(0);
+      }(), ...);
+    }(std::make_integer_sequence<int, MH * NJ>{});
+  };
+  // stage s from position pc (which then receives the XC operands of stage s+NB; at odd s the pair image of
+  // positions pc-1, pc receives the paired operands of stages s+3, s+4); position pn holds stage s+1.  `steady`: stages s+1 .. s+NB exist and are full
+  // (counted vmcnt wait, unchecked DMA).  Reads in flight on entry: alo / bc of stage s.
+  auto stage = [&](int s, int pc, int pn, bf16x8 (&bc)[NJ], bf16x8 (&bn)[NJ], bool steady) {
+    const Pos qc = pos(pc), qn = pos(pn);
+    rd_ahi(qc);
+    lgkm(std::integral_constant<int, MH * RA>{});  // alo / bc have landed (LDS returns in order)
+    mm_lo(bc);
+    lgkm(std::integral_constant<int, 0>{});  // ahi has landed: this wave is done reading stage s
+    const bool more = steady || s + 1 < KT;
+    if (more) {
+      // stage s+1 has landed; younger DMAs stay in flight (issue order per stage: the unpaired stage s+4, then at
+      // odd stages the pair s+3, s+4): even s waits for the pair issued at s-3 (2 GX + 2 GP younger), odd s for
+      // the pair issued at s-2 (GX younger); s and pc have the same parity
+      if (steady) {
+        if (pc & 1) vm_wait<GX>();
+        else vm_wait<2 * GX + 2 * GP>();
+      } else {
+        vm_wait<0>();
+      }
+      __builtin_amdgcn_s_barrier();  // ... for every wave; every wave is done reading stage s
+      __builtin_amdgcn_sched_barrier(0);
+      if (steady) {
+        dma(s + NB, pc);
+        if (pc & 1) dma_pair(s + 3, pc - 1, false);
+      } else {
+        if (s + NB < KT) dma(s + NB, pc);
+        if ((pc & 1) && s + 3 < KT) dma_pair(s + 3, pc - 1, true);
+      }
+    }
+    mm_hi_rd(bc, bn, qn, more);
+  };
+
+  if (KT > 0) {
+    // the steady issue order from stage -4 on: unpaired 0, 1, pair (0, 1), unpaired 2, 3, pair (2, 3)
+#pragma unroll
+    for (int s = 0; s < NB; ++s) {
+      if (s < KT) dma(s, s);
+      if ((s & 1) && s - 1 < KT) dma_pair(s - 1, s - 1, true);
+    }
+    if (KT >= NB) vm_wait<2 * GX + 2 * GP>();  // stage 0 landed
+    else vm_wait<0>();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    rd_lo(pos(0), b0);
+  }
+  // steady loop: U = lcm(NB, 2) stages per iteration
+  constexpr int U = NB % 2 ? 2 * NB : NB;
+  int s = 0;
+#pragma unroll 1
+  for (; s + U + NB <= KTF; s += U) {  // stages s+1 .. s+U-1+NB exist and are full
+#pragma unroll
+    for (int u = 0; u < U; u += 2) {
+      stage(s + u, u % NB, (u + 1) % NB, b0, b1, true);
+      stage(s + u + 1, (u + 1) % NB, (u + 2) % NB, b1, b0, true);
+    }
+  }
+  // tail (a multiple of U stages done: stage s is at position 0): every wait vmcnt(0)
+  int p0 = 0;
+  auto adv = [](int p) { return p + 1 == NB ? 0 : p + 1; };
+#pragma unroll 1
+  for (; s < KT; s += 2) {
+    const int p1 = adv(p0), p2 = adv(p1);
+    stage(s, p0, p1, b0, b1, false);
+    if (s + 1 < KT) stage(s + 1, p1, p2, b1, b0, false);
+    p0 = p2;
+  }
+  vm_wait<0>();
+  lgkm(std::integral_constant<int, 0>{});
+
+  // epilogue: lane holds C[m][n .. n+3], m = m0 + am0 + 16 i + (l & 15), n = n0 + bn0 + 16 j + 4 (l >> 4)
+  const int mr = l & 15, nc = 4 * (l >> 4);
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int mm = am0 + 16 * i + mr;
+    if (mm >= mvalid) continue;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int nn = bn0 + 16 * j + nc;
+      if (nn >= nvalid) continue;
+      const int64_t off = (int64_t)(m0 + mm) * a.ldc + n0 + nn;
+      if constexpr (EPI == 0) {
+        bf16_t* c = reinterpret_cast<bf16_t*>(a.C) + off;
+        *reinterpret_cast<uint2*>(c) = make_uint2(pack2(acc[i][j][0], acc[i][j][1]), pack2(acc[i][j][2], acc[i][j][3]));
+      } else {
+        float* c = reinterpret_cast<float*>(a.C) + (int64_t)split * a.split_stride + off;
+        float4 v = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+        if constexpr (EPI == 2) {
+          const float4 o = *reinterpret_cast<const float4*>(c);
+          v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+        }
+        *reinterpret_cast<float4*>(c) = v;
+      }
+    }
+  }
+}
+
 // ---- persistent engine --------------------------------------------------------------------------------------
 // The same K-loop as gemm_pipe_k (256 x 256 or 128 x 256 tiles, 8 waves, 64-deep K-tiles in two LDS buffers),
 // but ONE workgroup per CU walks output tiles, and the K-tile stream runs across tile boundaries: the last two
@@ -871,6 +1161,19 @@ int gemm_wg_nb() {
 }
 void set_gemm_wg_nb(int nb) { g_wg_nb = (nb == 4 || nb == 5) ? nb : 0; }
 
+// paired 64-deep KC images (gemm_wg_kp_k): 0 never, 1 for wide KC operands (default), 2 for every KC operand;
+// MAMBA_AMD_WG_KCPAIR sets the process default, set_gemm_wg_kcpair overrides it
+static int g_wg_kcpair = -1;
+int gemm_wg_kcpair() {
+  if (g_wg_kcpair < 0) {
+    const char* e = getenv("MAMBA_AMD_WG_KCPAIR");
+    const int v = e ? atoi(e) : 1;
+    g_wg_kcpair = (v >= 0 && v <= 2) ? v : 1;
+  }
+  return g_wg_kcpair;
+}
+void set_gemm_wg_kcpair(int v) { g_wg_kcpair = (v >= 0 && v <= 2) ? v : 1; }
+
 bool gemm_pipe_supported(int la, int lb, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc) {
   if (M <= 0 || N <= 0 || K <= 0) return false;
   if (lda % 8 || ldb % 8 || ldc % 4 || N % 4) return false;
@@ -919,11 +1222,24 @@ hipError_t launch_gemm_pipe(int la, int lb, const void* A, int64_t lda, const vo
     a.nbA = (unsigned)((la ? (int64_t)(K - 1) * lda + M : (int64_t)(M - 1) * lda + K) * 2);
     a.nbB = (unsigned)((lb ? (int64_t)(K - 1) * ldb + N : (int64_t)(N - 1) * ldb + K) * 2);
     const int mi = bm == 128 ? 4 : 8;
-#define WG_L(LA_, LB_, E_, MI_) hipLaunchKernelGGL((gemm_wg_k<LA_, LB_, E_, 4, MI_>), dim3(nwg), dim3(512), 0, st, a)
+    // KC operands in paired 64-deep images (whole 128-B rows per DMA) when the KC operand is a wide streaming one:
+    // measured (profiles/r6/wg_kc_pairs.txt) 1.27x on the Mamba-1 in_proj weight gradient (3072 KC rows, either
+    // side), but slower when the KC operand is narrow or short-K (out_proj wgrad with 1536 KC rows +4%, the
+    // out_proj forward's 768-row weight +22%, the 48 / 80-row x_proj / dt_proj products +25-60%): the pair
+    // halves the prefetch distance of every even stage.  MAMBA_AMD_WG_KCPAIR: 0 off, 1 this rule, 2 every KC.
+    const int kpm = gemm_wg_kcpair();
+    const bool kp = kpm == 2 ? (la == 0 || lb == 0) : kpm == 1 && ((la == 0 && M >= 3072) || (lb == 0 && N >= 3072));
+#define WG_L(LA_, LB_, E_, MI_)                                                                          \
+  if constexpr (LA_ == 0 || LB_ == 0) {                                                                  \
+    if (kp) hipLaunchKernelGGL((gemm_wg_kp_k<LA_, LB_, E_, MI_>), dim3(nwg), dim3(512), 0, st, a);       \
+    else hipLaunchKernelGGL((gemm_wg_k<LA_, LB_, E_, 4, MI_>), dim3(nwg), dim3(512), 0, st, a);          \
+  } else {                                                                                                \
+    hipLaunchKernelGGL((gemm_wg_k<LA_, LB_, E_, 4, MI_>), dim3(nwg), dim3(512), 0, st, a);               \
+  }
 #define WG_M(LA_, LB_, MI_)                                     \
-  if (epi == 0) WG_L(LA_, LB_, 0, MI_);                         \
-  else if (epi == 1) WG_L(LA_, LB_, 1, MI_);                    \
-  else WG_L(LA_, LB_, 2, MI_);
+  if (epi == 0) { WG_L(LA_, LB_, 0, MI_) }                      \
+  else if (epi == 1) { WG_L(LA_, LB_, 1, MI_) }                 \
+  else { WG_L(LA_, LB_, 2, MI_) }
 #define WG_E(LA_, LB_)                                          \
   if (mi == 4) { WG_M(LA_, LB_, 4) }                            \
   else { WG_M(LA_, LB_, 8) }

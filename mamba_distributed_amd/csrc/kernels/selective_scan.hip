@@ -1422,6 +1422,8 @@ __global__ __launch_bounds__(256) void selscan_bwd_sg_k(SelScanArgs a) {
       }
       float rb, rc;
       lane_sum8x2(cB, cC, rb, rc);
+      asm volatile("" : "+v"(rb), "+v"(rc));  // finish the sums here: sunk into the branch, their last DPP add
+                                             // no longer folds (v_mov 0 + v_mov_dpp + v_add instead of v_add_dpp)
       if ((lane & 7) == 0) {
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, rb), rdB, opd + 4 * t2, 4 * t0, 0);
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, rc), rdC, opd + 4 * t2, 4 * t0, 0);

@@ -53,11 +53,44 @@ def m1_cases(T=65536, d=768, di=1536, R=48, N=16):
         ("m1_out_wgrad XC.KC slabs", dout, y2, 1, 0, 1, 0, 256, 2.0 * T * di * d),
         ("m1_in_wgrad KC.XC slabs", dxz, h2, 0, 1, 1, 0, 256, 2.0 * T * d * 2 * di),
         ("m1_in_wgrad^T XC.KC slabs (768 x 3072)", h2, dxz, 1, 0, 1, 0, 256, 2.0 * T * d * 2 * di),
+        ("m1_in_wgrad XC.XC slabs (dxz token-major copy)", dxz.t().contiguous(), h2, 1, 1, 1, 0, 256,
+         2.0 * T * d * 2 * di),
+        ("m1_out_wgrad XC.XC slabs (y2 token-major copy)", dout, y2.t().contiguous(), 1, 1, 1, 0, 256,
+         2.0 * T * di * d),
+        ("m1_out_fwd KC.KC bf16 (y2 token-major copy)", y2.t().contiguous(), w_out, 0, 0, 0, 1, 256, 2.0 * T * di * d),
         ("m1_x_wgrad KC.KC slabs", dxdbl, co2, 0, 0, 1, 0, 256, 2.0 * T * di * (R + 2 * N)),
         ("m1_x_wgrad KC.KC slabs 128-row", dxdbl, co2, 0, 0, 1, 0, 128, 2.0 * T * di * (R + 2 * N)),
         ("m1_dt_wgrad KC.KC slabs (1536 x 48)", dd2, dxdbl[:R], 0, 0, 1, 0, 256, 2.0 * T * di * R),
         ("m1_dt_wgrad^T KC.KC slabs 128-row (48 x 1536)", dxdbl[:R], dd2, 0, 0, 1, 0, 128, 2.0 * T * di * R),
     ]
+
+
+def run_m1_kp(a, ops, kps):
+    """The Mamba-1 cases on the staged-ring engine with the KC operand images paired (kp 1, gemm_wg_kp_k) or not."""
+    for name, A, B, la, lb, mode, S, bm, fl in m1_cases():
+        if la == 1 and lb == 1 or (la == 0 and lb == 0 and mode == 0):
+            continue
+        M = A.shape[0] if la == 0 else A.shape[1]
+        N = B.shape[0] if lb == 0 else B.shape[1]
+        K = A.shape[1] if la == 0 else A.shape[0]
+        if S == 0:
+            S = ops.gp_splits(M, N, K)
+        out = torch.empty(S, M, N, device="cuda") if mode else torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        res = {kp: [] for kp in kps}
+        outs = {}
+        for _ in range(a.rounds):
+            for kp in kps:
+                ops.gp_wg_kcpair(kp)  # 0 off, 1 default rule, 2 every KC operand
+                res[kp].append(timeit(lambda: ops.gp_mm(A, B, out, la, lb, mode, S, bm), a.reps))
+                outs[kp] = out.clone()
+        ops.gp_wg_kcpair(1)
+        r = {"case": name, "M": M, "N": N, "K": K, "splits": S}
+        for kp in kps:
+            t = min(res[kp])
+            r[f"kp{kp}_us"] = round(t, 1)
+            r[f"kp{kp}_tflops"] = round(fl / t / 1e6, 1)
+            r[f"kp{kp}_equal_kp{kps[0]}"] = bool(torch.equal(outs[kp], outs[kps[0]]))
+        print(json.dumps(r), flush=True)
 
 
 def run_m1(a, ops, nbs):
@@ -92,10 +125,14 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--nb", default="0,4")
     ap.add_argument("--m1", action="store_true", help="the Mamba-1 layer's gp_mm products instead")
+    ap.add_argument("--kp", default="", help="with --m1: compare KC image modes (0 off, 1 default rule, 2 all), e.g. 0,2")
     a = ap.parse_args()
     assert _ext.load(), _ext.error()
     ops = _ext.ops()
     nbs = [int(v) for v in a.nb.split(",")]
+    if a.m1 and a.kp:
+        run_m1_kp(a, ops, [int(v) for v in a.kp.split(",")])
+        return
     if a.m1:
         run_m1(a, ops, nbs)
         return

@@ -278,3 +278,56 @@ def test_gp_wg_engine_default_path(cuda):
     out = torch.zeros(dp, d, device=cuda)
     ops.gp_reduce(part, out, False)
     assert _rel(out, _ref(A, B, 1, 1)) < 1e-5
+
+
+@pytest.mark.parametrize("la,lb,mode", [(0, 1, 0), (0, 1, 1), (1, 0, 0), (1, 0, 2), (0, 0, 1), (0, 0, 2)])
+@pytest.mark.parametrize("M,N,K,S,bm", [(256, 256, 32, 1, 256), (264, 136, 96, 1, 256), (520, 776, 200, 1, 256),
+                                        (256, 512, 128, 1, 256), (768, 520, 1544, 3, 256), (3072, 768, 4160, 7, 256),
+                                        (80, 1536, 2056, 4, 128), (128, 264, 288, 1, 128)])
+def test_gp_wg_kc_pairs(cuda, la, lb, mode, M, N, K, S, bm):
+    """gemm_wg_kp_k (paired 64-deep KC images, csrc/kernels/gemm_pipe.hip) against the 32-deep gemm_wg_k: the same
+    fragments in the same MFMA order, so bitwise equal outputs -- over 1..4 stages (prologue only), odd stage counts,
+    partial last stages, K splits, both tile heights and every epilogue -- and both against the fp32 reference."""
+    ops = _ops()
+    if la == 1 and M % 8 or lb == 1 and N % 8:
+        pytest.skip("XC operands need 8-aligned rows")
+    g = torch.Generator(device=cuda).manual_seed(M + 3 * N + 7 * K + la)
+    A, B = _mk(M, K, la, cuda, g), _mk(N, K, lb, cuda, g)
+    ref = _ref(A, B, la, lb)
+    outs = {}
+    old = ops.gp_wg_kcpair(-1)
+    try:
+        for kp in (0, 1):  # 1: forced on every KC operand (mode 2)
+            assert ops.gp_wg_kcpair(2 * kp) == 2 * kp
+            if mode == 2:
+                acc = torch.full((M, N), 0.25, device=cuda)
+                ops.gp_mm(A, B, acc, la, lb, 2, 1, bm)
+                outs[kp] = acc
+            elif mode == 1:
+                outs[kp] = ops.gp_mm(A, B, None, la, lb, 1, S, bm)
+            else:
+                outs[kp] = ops.gp_mm(A, B, None, la, lb, 0, 1, bm)
+    finally:
+        ops.gp_wg_kcpair(old)
+    assert torch.equal(outs[0], outs[1])
+    got = outs[1].sum(0) if mode == 1 else outs[1]
+    want = ref + 0.25 if mode == 2 else ref
+    assert _rel(got, want) < (8e-3 if mode == 0 else 1e-5), _rel(got, want)
+
+
+def test_gp_wg_kc_pairs_default_rule(cuda):
+    """The default rule pairs a KC operand of >= 3072 rows (the Mamba-1 in_proj weight gradient, either side) and
+    nothing narrower; either way the result is bitwise the unpaired engine's."""
+    ops = _ops()
+    g = torch.Generator(device=cuda).manual_seed(5)
+    A, B = _mk(3072, 4096, 0, cuda, g), _mk(768, 4096, 1, cuda, g)
+    old = ops.gp_wg_kcpair(-1)
+    try:
+        ops.gp_wg_kcpair(1)
+        p1 = ops.gp_mm(A, B, None, 0, 1, 1, 2, 256)
+        ops.gp_wg_kcpair(0)
+        p0 = ops.gp_mm(A, B, None, 0, 1, 1, 2, 256)
+    finally:
+        ops.gp_wg_kcpair(old)
+    assert torch.equal(p0, p1)
+    assert _rel(p1.sum(0), _ref(A, B, 0, 1)) < 1e-5
