@@ -67,7 +67,40 @@ __device__ __forceinline__ float act_bwd(float a, float g, bool silu) {
   return g * s * (1.f + a * (1.f - s));
 }
 
+// 8 consecutive elements of a VEC row (wholly inside or wholly past L) as raw 16-B pieces, unpacked at use:
+// half the registers of the fp32 form for bf16 while the load is in flight
+template <typename T> struct Raw8 {
+  static constexpr int NV = sizeof(T) / 2;
+  uint4 v[NV];
+  __device__ __forceinline__ void load(const T* p) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = reinterpret_cast<const uint4*>(p)[i];
+  }
+  __device__ __forceinline__ void unpack(float (&o)[8], bool valid) const {
+    if constexpr (sizeof(T) == 2) {
+      const uint32_t u[4] = {v[0].x, v[0].y, v[0].z, v[0].w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        o[2 * i] = __uint_as_float(u[i] << 16);
+        o[2 * i + 1] = __uint_as_float(u[i] & 0xffff0000u);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        o[4 * i] = __uint_as_float(v[i].x); o[4 * i + 1] = __uint_as_float(v[i].y);
+        o[4 * i + 2] = __uint_as_float(v[i].z); o[4 * i + 3] = __uint_as_float(v[i].w);
+      }
+    }
+    if (!valid) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = 0.f;
+    }
+  }
+};
+
 // =========================== channel-first ===============================================
+// A wave walks its row in PAIRS of 512-step chunks whose loads are all issued before the first is used: with one
+// 1-KB load per wave in flight the kernels ran at ~3.9 TB/s (bytes in flight per CU, not HBM, set the rate).
 template <typename T, int W, bool VEC>
 __global__ __launch_bounds__(256) void conv_cf_fwd_k(const T* __restrict__ x, int64_t sxb, int64_t sxd,
                                                      const float* __restrict__ w, const float* __restrict__ bias,
@@ -84,10 +117,7 @@ __global__ __launch_bounds__(256) void conv_cf_fwd_k(const T* __restrict__ x, in
   for (int k = 0; k < W; ++k) wk[k] = w[d * W + k];
   const float bs = bias ? bias[d] : 0.f;
   float carry[3] = {0.f, 0.f, 0.f};  // x[t0-3..t0-1] for lane 0 of the current chunk
-  for (int c0 = 0; c0 < L; c0 += 512) {
-    const int t0 = c0 + lane * 8;
-    float cur[8];
-    load_run<T, VEC>(xr + t0, t0, L, cur);
+  auto chunk = [&](const float (&cur)[8], int t0) {
     float prev[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
@@ -110,6 +140,26 @@ __global__ __launch_bounds__(256) void conv_cf_fwd_k(const T* __restrict__ x, in
       o[j] = act_fwd(a, silu);
     }
     if (t0 < L) store_run<T, VEC>(orow + t0, t0, L, o);
+  };
+  for (int c0 = 0; c0 < L; c0 += 1024) {
+    const int ta = c0 + lane * 8, tb = ta + 512;
+    float ca[8], cb[8];
+    if constexpr (VEC) {  // both loads in flight (clamped to a legal run), unpacked at use
+      Raw8<T> ra, rb;
+      ra.load(xr + min(ta, L - 8));
+      rb.load(xr + min(tb, L - 8));
+      ra.unpack(ca, ta < L);
+      chunk(ca, ta);
+      if (c0 + 512 < L) {
+        rb.unpack(cb, tb < L);
+        chunk(cb, tb);
+      }
+    } else {
+      load_run<T, VEC>(xr + ta, ta, L, ca);
+      load_run<T, VEC>(xr + tb, tb, L, cb);
+      chunk(ca, ta);
+      if (c0 + 512 < L) chunk(cb, tb);
+    }
   }
 }
 
@@ -134,19 +184,13 @@ __global__ __launch_bounds__(256) void conv_cf_bwd_k(const T* __restrict__ x, in
 #pragma unroll
   for (int k = 0; k < W; ++k) accw[k] = 0.f;
   float nextd[3] = {0.f, 0.f, 0.f};  // dpre[t_end .. t_end+2] of the chunk after this one
-  const int nchunks = (L + 511) / 512;
-  for (int ci = nchunks - 1; ci >= 0; --ci) {
-    const int c0 = ci * 512;
-    const int t0 = c0 + lane * 8;
-    float cur[8], g[8];
-    load_run<T, VEC>(xr + t0, t0, L, cur);
-    load_run<T, VEC>(gr + t0, t0, L, g);
+  // one chunk: cur / g its x and dout, halo = x[t0-3 .. t0-1] for lane 0
+  auto chunk = [&](const float (&cur)[8], const float (&g)[8], const float (&halo)[3], int t0) {
     float prev[3];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) prev[j] = __shfl_up(cur[5 + j], 1, 64);
-    if (lane == 0) {
-#pragma unroll
-      for (int j = 0; j < 3; ++j) prev[j] = (t0 - 3 + j >= 0) ? ld(xr + t0 - 3 + j) : 0.f;
+    for (int j = 0; j < 3; ++j) {
+      const float v = __shfl_up(cur[5 + j], 1, 64);
+      prev[j] = lane == 0 ? halo[j] : v;
     }
     float win[11];
 #pragma unroll
@@ -181,6 +225,47 @@ __global__ __launch_bounds__(256) void conv_cf_bwd_k(const T* __restrict__ x, in
       accb += dp[j];
     }
     if (t0 < L) store_run<T, VEC>(dxr + t0, t0, L, o);
+  };
+  // pairs of chunks from the last: (lo, hi) = chunks (2p, 2p + 1); every load of the pair, and lane 0's halo of
+  // the lo chunk, issued first; the hi chunk's halo is the lo chunk's last lane
+  const int npairs = (L + 1023) / 1024;
+  for (int pi = npairs - 1; pi >= 0; --pi) {
+    const int tl = pi * 1024 + lane * 8, th = tl + 512;
+    float xl[8], gl[8], xh[8], gh[8], hl[3] = {0.f, 0.f, 0.f}, hh[3];
+    if constexpr (VEC) {  // the four loads in flight (clamped to legal runs), unpacked at use
+      Raw8<T> rxl, rgl, rxh, rgh;
+      rxl.load(xr + min(tl, L - 8));
+      rgl.load(gr + min(tl, L - 8));
+      rxh.load(xr + min(th, L - 8));
+      rgh.load(gr + min(th, L - 8));
+      if (lane == 0) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) hl[j] = (tl - 3 + j >= 0) ? ld(xr + tl - 3 + j) : 0.f;
+      }
+      rxl.unpack(xl, tl < L);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) hh[j] = __shfl(xl[5 + j], 63, 64);
+      if (pi * 1024 + 512 < L) {
+        rxh.unpack(xh, th < L);
+        rgh.unpack(gh, th < L);
+        chunk(xh, gh, hh, th);
+      }
+      rgl.unpack(gl, tl < L);
+      chunk(xl, gl, hl, tl);
+    } else {
+      load_run<T, VEC>(xr + tl, tl, L, xl);
+      load_run<T, VEC>(gr + tl, tl, L, gl);
+      load_run<T, VEC>(xr + th, th, L, xh);
+      load_run<T, VEC>(gr + th, th, L, gh);
+      if (lane == 0) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) hl[j] = (tl - 3 + j >= 0) ? ld(xr + tl - 3 + j) : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 3; ++j) hh[j] = __shfl(xl[5 + j], 63, 64);
+      if (pi * 1024 + 512 < L) chunk(xh, gh, hh, th);
+      chunk(xl, gl, hl, tl);
+    }
   }
 #pragma unroll
   for (int k = 0; k < W; ++k) accw[k] = wave_sum(accw[k]);
