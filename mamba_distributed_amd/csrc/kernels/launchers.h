@@ -13,9 +13,11 @@ namespace mamba_amd {
 // plus the fp32 slab round trip of each extra split (P Q x 8 B at ~5 TB/s against 256 x 256 x 2K flop per CU
 // at ~3.5 TF/s: P Q / (23405 K) tile units), keeping >= min_k tokens per split.
 inline int split_k_count(int64_t tiles, int64_t P, int64_t Q, int64_t K, int64_t min_k) {
+  // up to 64 slices: a narrow output (the Mamba-1 x_proj / dt_proj weight gradients: 6 tiles) at the old cap of 16
+  // ran 96 workgroups on 256 CUs (profiles/r6/narrow_wgrad_splits.txt)
   int best = 1;
   double bc = 1e30;
-  for (int S = 1; S <= 16; ++S) {
+  for (int S = 1; S <= 64; ++S) {
     if (S > 1 && K / S < min_k) break;
     const double c = (double)((tiles * S + 255) / 256) / S + (double)S * P * Q / (23405.0 * K);
     if (c < bc - 1e-9) { bc = c; best = S; }

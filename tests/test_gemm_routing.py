@@ -43,3 +43,19 @@ def test_library_table_only_under_the_ab_switches(monkeypatch):
     assert not linear._pk_wins(65536, 3392, 768, "fwd")
     monkeypatch.setenv("MAMBA_AMD_PROJ_GEMM", "fwd_short,dgrad")
     assert linear._pk_wins(65536, 768, 3072, "dgrad_xc")  # role lists see the Mamba-1 roles as fwd / dgrad
+
+
+def test_split_k_rule_fills_a_round_for_narrow_outputs():
+    """launchers.h split_k_count through ops.gp_splits (host code, no GPU needed): a narrow weight gradient (the
+    Mamba-1 x_proj 80 x 1536 over 65536 tokens: 6 tiles) is split until one round of 256 CUs is nearly full
+    (the old cap of 16 slices left 160 CUs idle); the projection shapes keep their split counts."""
+    import pytest
+    from mamba_distributed_amd.ops import _ext
+    if not _ext.load():
+        pytest.skip("extension not built")
+    ops = _ext.ops()
+    s = ops.gp_splits(80, 1536, 65536)
+    assert 32 <= s <= 64 and 6 * s <= 256, s
+    assert ops.gp_splits(3392, 768, 65536) == 6     # Mamba-2 280M in_proj weight gradient
+    assert ops.gp_splits(768, 1536, 65536) == 14    # out_proj weight gradient
+    assert ops.gp_splits(8512, 2048, 32768) == 7    # 1.4B in_proj
