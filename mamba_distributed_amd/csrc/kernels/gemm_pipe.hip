@@ -1121,17 +1121,26 @@ __global__ __launch_bounds__(128 * WN) void gemm_pk_k(GemmPkArgs a) {
   }
 }
 
-// out[i] (+)= sum_s part[s][i] in fixed order (the K-split slabs of a weight gradient)
+// out[i] (+)= sum_s part[s][i] in fixed order (the K-split slabs of a weight gradient).  V = 4: a float4 per thread;
+// V = 1 for small outputs with many slabs (the 42-slab narrow weight gradients: 120 workgroups of float4 threads
+// would each walk 42 dependent slab reads)
+template <int V>
 __global__ void gp_reduce_k(const float* __restrict__ part, int S, int64_t stride, int64_t n, float* __restrict__ out,
                             bool accumulate) {
-  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * V;
   if (i >= n) return;
-  float4 s = accumulate ? *reinterpret_cast<const float4*>(out + i) : make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int k = 0; k < S; ++k) {
-    const float4 v = *reinterpret_cast<const float4*>(part + (int64_t)k * stride + i);
-    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  if constexpr (V == 4) {
+    float4 s = accumulate ? *reinterpret_cast<const float4*>(out + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < S; ++k) {
+      const float4 v = *reinterpret_cast<const float4*>(part + (int64_t)k * stride + i);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    *reinterpret_cast<float4*>(out + i) = s;
+  } else {
+    float s = accumulate ? out[i] : 0.f;
+    for (int k = 0; k < S; ++k) s += part[(int64_t)k * stride + i];
+    out[i] = s;
   }
-  *reinterpret_cast<float4*>(out + i) = s;
 }
 
 // waves per workgroup of the split-K engine (gemm_pipe_k, weight gradients): 8 (two per SIMD, 128 x 64 wave
@@ -1383,8 +1392,12 @@ hipError_t launch_gemm_pk(int la, int lb, const void* A, int64_t lda, const void
 hipError_t launch_gp_reduce(const float* part, int S, int64_t stride, int64_t n, float* out, bool accumulate,
                             hipStream_t st) {
   if (n % 4 || stride % 4) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(gp_reduce_k, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, st, part, S, stride, n, out,
-                     accumulate);
+  if (n / 4 < 512 * 256 && S >= 16)  // fewer than 2 float4 workgroups per CU: one element per thread
+    hipLaunchKernelGGL(gp_reduce_k<1>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part, S, stride, n, out,
+                       accumulate);
+  else
+    hipLaunchKernelGGL(gp_reduce_k<4>, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, st, part, S, stride, n,
+                       out, accumulate);
   return hipGetLastError();
 }
 
