@@ -331,3 +331,19 @@ def test_gp_wg_kc_pairs_default_rule(cuda):
         ops.gp_wg_kcpair(old)
     assert torch.equal(p0, p1)
     assert _rel(p1.sum(0), _ref(A, B, 0, 1)) < 1e-5
+
+
+@pytest.mark.parametrize("S,n", [(42, 80 * 1536), (16, 48 * 1536), (7, 3072 * 768)])
+def test_gp_reduce_forms(cuda, S, n):
+    """gp_reduce over S fp32 slabs in fixed order: the one-element-per-thread form (many slabs, small output: the
+    narrow weight gradients) and the float4 form give the fp64 sum, bitwise repeatably."""
+    ops = _ops()
+    g = torch.Generator(device=cuda).manual_seed(S)
+    part = torch.randn(S, n, device=cuda, generator=g)
+    out = torch.full((n,), 0.5, device=cuda)
+    ops.gp_reduce(part.view(S, 1, n), out.view(1, n), True)
+    want = part.double().sum(0) + 0.5
+    assert (out.double() - want).abs().max().item() < 1e-4
+    out2 = torch.full((n,), 0.5, device=cuda)
+    ops.gp_reduce(part.view(S, 1, n), out2.view(1, n), True)
+    assert torch.equal(out, out2)
