@@ -1088,7 +1088,7 @@ int64_t gp_wg_nb(int64_t nb) {
   return mamba_amd::gemm_wg_nb();
 }
 
-// staged-ring KC operand images: 0 = 32-deep, 1 = paired 64-deep for wide KC operands, 2 = paired for every KC
+// staged-ring KC operand images: 0 = 32-deep, 1 = paired 64-deep for wide long-K KC operands, 2 = paired for every KC
 // operand; v < 0 only reads it
 int64_t gp_wg_kcpair(int64_t v) {
   if (v >= 0) mamba_amd::set_gemm_wg_kcpair((int)v);

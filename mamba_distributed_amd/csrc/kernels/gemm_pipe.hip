@@ -1170,7 +1170,7 @@ int gemm_wg_nb() {
 }
 void set_gemm_wg_nb(int nb) { g_wg_nb = (nb == 4 || nb == 5) ? nb : 0; }
 
-// paired 64-deep KC images (gemm_wg_kp_k): 0 never, 1 for wide KC operands (default), 2 for every KC operand;
+// paired 64-deep KC images (gemm_wg_kp_k): 0 never, 1 for wide long-K KC operands (default), 2 for every KC operand;
 // MAMBA_AMD_WG_KCPAIR sets the process default, set_gemm_wg_kcpair overrides it
 static int g_wg_kcpair = -1;
 int gemm_wg_kcpair() {
@@ -1231,13 +1231,15 @@ hipError_t launch_gemm_pipe(int la, int lb, const void* A, int64_t lda, const vo
     a.nbA = (unsigned)((la ? (int64_t)(K - 1) * lda + M : (int64_t)(M - 1) * lda + K) * 2);
     a.nbB = (unsigned)((lb ? (int64_t)(K - 1) * ldb + N : (int64_t)(N - 1) * ldb + K) * 2);
     const int mi = bm == 128 ? 4 : 8;
-    // KC operands in paired 64-deep images (whole 128-B rows per DMA) when the KC operand is a wide streaming one:
-    // measured (profiles/r6/wg_kc_pairs.txt) 1.27x on the Mamba-1 in_proj weight gradient (3072 KC rows, either
-    // side), but slower when the KC operand is narrow or short-K (out_proj wgrad with 1536 KC rows +4%, the
-    // out_proj forward's 768-row weight +22%, the 48 / 80-row x_proj / dt_proj products +25-60%): the pair
-    // halves the prefetch distance of every even stage.  MAMBA_AMD_WG_KCPAIR: 0 off, 1 this rule, 2 every KC.
+    // KC operands in paired 64-deep images (whole 128-B rows per DMA) when the KC operand is a wide one streamed
+    // over a long reduction (a weight gradient): measured (profiles/r6/wg_kc_pairs.txt) 1.27x on the Mamba-1
+    // in_proj weight gradient (3072 KC rows) and +0.2-0.8% whole-step with the out_proj one (1536 rows) added;
+    // slower for short-K products with a small L2-resident KC operand (the out_proj forward's 768-row weight
+    // +14-22%) and the 48 / 80-row x_proj / dt_proj products (+25-60%): the pair halves the prefetch distance of
+    // every even stage.  MAMBA_AMD_WG_KCPAIR: 0 off, 1 this rule, 2 every KC operand.
     const int kpm = gemm_wg_kcpair();
-    const bool kp = kpm == 2 ? (la == 0 || lb == 0) : kpm == 1 && ((la == 0 && M >= 3072) || (lb == 0 && N >= 3072));
+    const bool kp = kpm == 2 ? (la == 0 || lb == 0)
+                             : kpm == 1 && K >= 16384 && ((la == 0 && M >= 1536) || (lb == 0 && N >= 1536));
 #define WG_L(LA_, LB_, E_, MI_)                                                                          \
   if constexpr (LA_ == 0 || LB_ == 0) {                                                                  \
     if (kp) hipLaunchKernelGGL((gemm_wg_kp_k<LA_, LB_, E_, MI_>), dim3(nwg), dim3(512), 0, st, a);       \

@@ -136,7 +136,8 @@ void set_gemm_pipe_waves(int w);
 // LDS slots (4 or 5) of the XC . XC fp32 weight-gradient engine gemm_wg_k, or 0: those products on gemm_pipe_k
 int gemm_wg_nb();
 void set_gemm_wg_nb(int nb);
-// paired 64-deep KC operand images in the staged-ring engine: 0 never, 1 wide KC operands (default), 2 always
+// paired 64-deep KC operand images in the staged-ring engine: 0 never, 1 KC operands of >= 1536 rows over K >= 16384
+// (default), 2 always
 int gemm_wg_kcpair();
 void set_gemm_wg_kcpair(int v);
 // out[i] (+)= sum_s part[s * stride + i], fixed order

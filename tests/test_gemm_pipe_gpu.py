@@ -316,11 +316,11 @@ def test_gp_wg_kc_pairs(cuda, la, lb, mode, M, N, K, S, bm):
 
 
 def test_gp_wg_kc_pairs_default_rule(cuda):
-    """The default rule pairs a KC operand of >= 3072 rows (the Mamba-1 in_proj weight gradient, either side) and
-    nothing narrower; either way the result is bitwise the unpaired engine's."""
+    """The default rule pairs a KC operand of >= 1536 rows over K >= 16384 (the Mamba-1 in_proj / out_proj weight
+    gradients); either way the result is bitwise the unpaired engine's."""
     ops = _ops()
     g = torch.Generator(device=cuda).manual_seed(5)
-    A, B = _mk(3072, 4096, 0, cuda, g), _mk(768, 4096, 1, cuda, g)
+    A, B = _mk(1536, 16384, 0, cuda, g), _mk(768, 16384, 1, cuda, g)
     old = ops.gp_wg_kcpair(-1)
     try:
         ops.gp_wg_kcpair(1)
