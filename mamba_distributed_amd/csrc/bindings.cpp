@@ -1090,6 +1090,14 @@ int64_t gp_wg_nb(int64_t nb) {
 
 // staged-ring KC operand images: 0 = 32-deep, 1 = paired 64-deep for wide long-K KC operands, 2 = paired for every KC
 // operand; v < 0 only reads it
+int64_t conv_cf_order_knob(int64_t v) {
+  if (v >= 0) mamba_amd::set_conv_cf_order((int)v);
+  return mamba_amd::conv_cf_order();
+}
+int64_t selscan_order_knob(int64_t v) {
+  if (v >= 0) mamba_amd::set_selscan_order((int)v);
+  return mamba_amd::selscan_order();
+}
 int64_t gp_wg_kcpair(int64_t v) {
   if (v >= 0) mamba_amd::set_gemm_wg_kcpair((int)v);
   return mamba_amd::gemm_wg_kcpair();
@@ -1292,6 +1300,8 @@ TORCH_LIBRARY(mamba_amd, m) {
   m.def("gp_waves(int w=0) -> int", &gp_waves);
   m.def("gp_wg_nb(int nb=-1) -> int", &gp_wg_nb);
   m.def("gp_wg_kcpair(int v=-1) -> int", &gp_wg_kcpair);
+  m.def("conv_cf_order(int v=-1) -> int", &conv_cf_order_knob);
+  m.def("selscan_order(int v=-1) -> int", &selscan_order_knob);
   m.def("ssd_stamps(Tensor? buf) -> ()", &ssd_stamps);
   m.def("ssd_segments(int n, int B, int H, int nc) -> int", &ssd_segments);
   m.def("gp_splits(int M, int N, int K) -> int", &gp_splits);

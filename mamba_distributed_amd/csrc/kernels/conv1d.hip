@@ -8,7 +8,8 @@
 //   previous chunk's lane 63 (carried in registers) — every x element is read from HBM once.
 //   Backward walks the chunks in reverse and carries the next chunk's first W-1 dpre values the
 //   same way; dw/db are wave-reduced per row and summed over the batch in a second, fixed-order
-//   pass (deterministic; no float atomics).
+//   pass (deterministic; no float atomics).  Rows are numbered in the input's memory order (cf_row), so the waves
+//   running together stream neighbouring rows.
 // Channel-last (Mamba-2; xBC is a column slice of the token-major in_proj output):
 //   lane = 8 consecutive channels (16-B), a wave = 512 channels of one time tile, each lane slides
 //   a W-row register window down its T_TILE timesteps.  dw/db: per-lane registers -> the block's
@@ -101,15 +102,137 @@ template <typename T> struct Raw8 {
 // =========================== channel-first ===============================================
 // A wave walks its row in PAIRS of 512-step chunks whose loads are all issued before the first is used: with one
 // 1-KB load per wave in flight the kernels ran at ~3.9 TB/s (bytes in flight per CU, not HBM, set the rate).
+
+// (b, d) of row r: rows are numbered in memory order, b fastest when the batch stride is the smaller one (Mamba-1's
+// (d, b, l) buffers), so neighbouring waves read neighbouring 2-KB rows instead of rows a whole (b, l) plane apart
+__device__ __forceinline__ void cf_row(int64_t r, int Bn, int Dn, bool binner, int& b, int& d) {
+  if (binner) { b = (int)(r % Bn); d = (int)(r / Bn); }
+  else { b = (int)(r / Dn); d = (int)(r % Dn); }
+}
+
+// one 512-step chunk of the forward: cur = x[t0 .. t0 + 7] of this lane; carry = lane 0's halo, advanced to this
+// chunk's last W-1 steps for the next chunk
+template <typename T, int W, bool VEC>
+__device__ __forceinline__ void cf_fwd_chunk(const float (&cur)[8], int t0, const float (&wk)[W], float bs,
+                                             float (&carry)[3], T* orow, int L, bool silu, int lane) {
+  float prev[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    float v = __shfl_up(cur[5 + j], 1, 64);
+    prev[j] = lane == 0 ? carry[j] : v;
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j) carry[j] = __shfl(cur[5 + j], 63, 64);
+  float win[11];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) win[j] = prev[j];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) win[3 + j] = cur[j];
+  float o[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float a = bs;
+#pragma unroll
+    for (int k = 0; k < W; ++k) a += wk[k] * win[3 + j - (W - 1) + k];
+    o[j] = act_fwd(a, silu);
+  }
+  if (t0 < L) store_run<T, VEC>(orow + t0, t0, L, o);
+}
+
+// one chunk of the backward: cur / g its x and dout, halo = x[t0-3 .. t0-1] for lane 0; nextd = dpre of the 3 steps
+// after the chunk (lane 63's), advanced to this chunk's first 3
+template <typename T, int W, bool VEC>
+__device__ __forceinline__ void cf_bwd_chunk(const float (&cur)[8], const float (&g)[8], const float (&halo)[3], int t0,
+                                             const float (&wk)[W], float bs, float (&nextd)[3], float (&accw)[W],
+                                             float& accb, T* dxr, int L, bool silu, int lane) {
+  float prev[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const float v = __shfl_up(cur[5 + j], 1, 64);
+    prev[j] = lane == 0 ? halo[j] : v;
+  }
+  float win[11];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) win[j] = prev[j];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) win[3 + j] = cur[j];
+  float dp[11];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float a = bs;
+#pragma unroll
+    for (int k = 0; k < W; ++k) a += wk[k] * win[3 + j - (W - 1) + k];
+    dp[j] = (t0 + j < L) ? act_bwd(a, g[j], silu) : 0.f;
+  }
+  // dpre of the next 3 steps: from lane+1, lane 63 from the carried next chunk
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    float v = __shfl_down(dp[j], 1, 64);
+    dp[8 + j] = lane == 63 ? nextd[j] : v;
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j) nextd[j] = __shfl(dp[j], 0, 64);
+  float o[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < W; ++k) s += wk[k] * dp[j + (W - 1) - k];
+    o[j] = s;
+#pragma unroll
+    for (int k = 0; k < W; ++k) accw[k] += dp[j] * win[3 + j - (W - 1) + k];
+    accb += dp[j];
+  }
+  if (t0 < L) store_run<T, VEC>(dxr + t0, t0, L, o);
+}
+
+// the loads of one backward chunk pair (VEC rows): x / dout of the lo (tl) and hi (tl + 512) chunks, clamped to legal
+// runs and kept packed, and lane 0's halo of the lo chunk
+template <typename T> struct CfBwdPair {
+  Raw8<T> xl, gl, xh, gh;
+  float hl[3];
+  __device__ __forceinline__ void load(const T* xr, const T* gr, int tl, int L, int lane) {
+    xl.load(xr + min(tl, L - 8));
+    gl.load(gr + min(tl, L - 8));
+    xh.load(xr + min(tl + 512, L - 8));
+    gh.load(gr + min(tl + 512, L - 8));
+#pragma unroll
+    for (int j = 0; j < 3; ++j) hl[j] = 0.f;
+    if (lane == 0) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) hl[j] = (tl - 3 + j >= 0) ? ld(xr + tl - 3 + j) : 0.f;
+    }
+  }
+  // hi chunk first (reverse time), its halo is the lo chunk's last lane
+  template <int W>
+  __device__ __forceinline__ void run(int p0, const float (&wk)[W], float bs, float (&nextd)[3], float (&accw)[W],
+                                      float& accb, T* dxr, int L, bool silu, int lane) const {
+    const int tl = p0 + lane * 8, th = tl + 512;
+    float x0[8], g0[8], hh[3];
+    xl.unpack(x0, tl < L);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) hh[j] = __shfl(x0[5 + j], 63, 64);
+    if (p0 + 512 < L) {
+      float x1[8], g1[8];
+      xh.unpack(x1, th < L);
+      gh.unpack(g1, th < L);
+      cf_bwd_chunk<T, W, true>(x1, g1, hh, th, wk, bs, nextd, accw, accb, dxr, L, silu, lane);
+    }
+    gl.unpack(g0, tl < L);
+    cf_bwd_chunk<T, W, true>(x0, g0, hl, tl, wk, bs, nextd, accw, accb, dxr, L, silu, lane);
+  }
+};
+
 template <typename T, int W, bool VEC>
 __global__ __launch_bounds__(256) void conv_cf_fwd_k(const T* __restrict__ x, int64_t sxb, int64_t sxd,
                                                      const float* __restrict__ w, const float* __restrict__ bias,
                                                      T* __restrict__ out, int64_t sob, int64_t sod, int Bn, int Dn,
-                                                     int L, bool silu) {
+                                                     int L, bool silu, bool binner) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= (int64_t)Bn * Dn) return;  // whole wave exits together
-  const int b = (int)(row / Dn), d = (int)(row % Dn);
+  int b, d;
+  cf_row(row, Bn, Dn, binner, b, d);
   const T* xr = x + b * sxb + d * sxd;
   T* orow = out + b * sob + d * sod;
   float wk[W];
@@ -117,30 +240,6 @@ __global__ __launch_bounds__(256) void conv_cf_fwd_k(const T* __restrict__ x, in
   for (int k = 0; k < W; ++k) wk[k] = w[d * W + k];
   const float bs = bias ? bias[d] : 0.f;
   float carry[3] = {0.f, 0.f, 0.f};  // x[t0-3..t0-1] for lane 0 of the current chunk
-  auto chunk = [&](const float (&cur)[8], int t0) {
-    float prev[3];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      float v = __shfl_up(cur[5 + j], 1, 64);
-      prev[j] = lane == 0 ? carry[j] : v;
-    }
-#pragma unroll
-    for (int j = 0; j < 3; ++j) carry[j] = __shfl(cur[5 + j], 63, 64);
-    float win[11];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) win[j] = prev[j];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) win[3 + j] = cur[j];
-    float o[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float a = bs;
-#pragma unroll
-      for (int k = 0; k < W; ++k) a += wk[k] * win[3 + j - (W - 1) + k];
-      o[j] = act_fwd(a, silu);
-    }
-    if (t0 < L) store_run<T, VEC>(orow + t0, t0, L, o);
-  };
   for (int c0 = 0; c0 < L; c0 += 1024) {
     const int ta = c0 + lane * 8, tb = ta + 512;
     float ca[8], cb[8];
@@ -149,16 +248,16 @@ __global__ __launch_bounds__(256) void conv_cf_fwd_k(const T* __restrict__ x, in
       ra.load(xr + min(ta, L - 8));
       rb.load(xr + min(tb, L - 8));
       ra.unpack(ca, ta < L);
-      chunk(ca, ta);
+      cf_fwd_chunk<T, W, VEC>(ca, ta, wk, bs, carry, orow, L, silu, lane);
       if (c0 + 512 < L) {
         rb.unpack(cb, tb < L);
-        chunk(cb, tb);
+        cf_fwd_chunk<T, W, VEC>(cb, tb, wk, bs, carry, orow, L, silu, lane);
       }
     } else {
       load_run<T, VEC>(xr + ta, ta, L, ca);
       load_run<T, VEC>(xr + tb, tb, L, cb);
-      chunk(ca, ta);
-      if (c0 + 512 < L) chunk(cb, tb);
+      cf_fwd_chunk<T, W, VEC>(ca, ta, wk, bs, carry, orow, L, silu, lane);
+      if (c0 + 512 < L) cf_fwd_chunk<T, W, VEC>(cb, tb, wk, bs, carry, orow, L, silu, lane);
     }
   }
 }
@@ -168,11 +267,13 @@ __global__ __launch_bounds__(256) void conv_cf_bwd_k(const T* __restrict__ x, in
                                                      const float* __restrict__ w, const float* __restrict__ bias,
                                                      const T* __restrict__ dout, int64_t sgb, int64_t sgd,
                                                      T* __restrict__ dx, int64_t sdb, int64_t sdd,
-                                                     float* __restrict__ part, bool pacc, int Bn, int Dn, int L, bool silu) {
+                                                     float* __restrict__ part, bool pacc, int Bn, int Dn, int L, bool silu,
+                                                     bool binner) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= (int64_t)Bn * Dn) return;
-  const int b = (int)(row / Dn), d = (int)(row % Dn);
+  int b, d;
+  cf_row(row, Bn, Dn, binner, b, d);
   const T* xr = x + b * sxb + d * sxd;
   const T* gr = dout + b * sgb + d * sgd;
   T* dxr = dx + b * sdb + d * sdd;
@@ -184,75 +285,17 @@ __global__ __launch_bounds__(256) void conv_cf_bwd_k(const T* __restrict__ x, in
 #pragma unroll
   for (int k = 0; k < W; ++k) accw[k] = 0.f;
   float nextd[3] = {0.f, 0.f, 0.f};  // dpre[t_end .. t_end+2] of the chunk after this one
-  // one chunk: cur / g its x and dout, halo = x[t0-3 .. t0-1] for lane 0
-  auto chunk = [&](const float (&cur)[8], const float (&g)[8], const float (&halo)[3], int t0) {
-    float prev[3];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const float v = __shfl_up(cur[5 + j], 1, 64);
-      prev[j] = lane == 0 ? halo[j] : v;
-    }
-    float win[11];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) win[j] = prev[j];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) win[3 + j] = cur[j];
-    float dp[11];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float a = bs;
-#pragma unroll
-      for (int k = 0; k < W; ++k) a += wk[k] * win[3 + j - (W - 1) + k];
-      dp[j] = (t0 + j < L) ? act_bwd(a, g[j], silu) : 0.f;
-    }
-    // dpre of the next 3 steps: from lane+1, lane 63 from the carried next chunk
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      float v = __shfl_down(dp[j], 1, 64);
-      dp[8 + j] = lane == 63 ? nextd[j] : v;
-    }
-#pragma unroll
-    for (int j = 0; j < 3; ++j) nextd[j] = __shfl(dp[j], 0, 64);
-    float o[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float s = 0.f;
-#pragma unroll
-      for (int k = 0; k < W; ++k) s += wk[k] * dp[j + (W - 1) - k];
-      o[j] = s;
-#pragma unroll
-      for (int k = 0; k < W; ++k) accw[k] += dp[j] * win[3 + j - (W - 1) + k];
-      accb += dp[j];
-    }
-    if (t0 < L) store_run<T, VEC>(dxr + t0, t0, L, o);
-  };
   // pairs of chunks from the last: (lo, hi) = chunks (2p, 2p + 1); every load of the pair, and lane 0's halo of
   // the lo chunk, issued first; the hi chunk's halo is the lo chunk's last lane
   const int npairs = (L + 1023) / 1024;
   for (int pi = npairs - 1; pi >= 0; --pi) {
     const int tl = pi * 1024 + lane * 8, th = tl + 512;
-    float xl[8], gl[8], xh[8], gh[8], hl[3] = {0.f, 0.f, 0.f}, hh[3];
-    if constexpr (VEC) {  // the four loads in flight (clamped to legal runs), unpacked at use
-      Raw8<T> rxl, rgl, rxh, rgh;
-      rxl.load(xr + min(tl, L - 8));
-      rgl.load(gr + min(tl, L - 8));
-      rxh.load(xr + min(th, L - 8));
-      rgh.load(gr + min(th, L - 8));
-      if (lane == 0) {
-#pragma unroll
-        for (int j = 0; j < 3; ++j) hl[j] = (tl - 3 + j >= 0) ? ld(xr + tl - 3 + j) : 0.f;
-      }
-      rxl.unpack(xl, tl < L);
-#pragma unroll
-      for (int j = 0; j < 3; ++j) hh[j] = __shfl(xl[5 + j], 63, 64);
-      if (pi * 1024 + 512 < L) {
-        rxh.unpack(xh, th < L);
-        rgh.unpack(gh, th < L);
-        chunk(xh, gh, hh, th);
-      }
-      rgl.unpack(gl, tl < L);
-      chunk(xl, gl, hl, tl);
+    if constexpr (VEC) {  // the four loads in flight, unpacked at use
+      CfBwdPair<T> pr;
+      pr.load(xr, gr, tl, L, lane);
+      pr.template run<W>(pi * 1024, wk, bs, nextd, accw, accb, dxr, L, silu, lane);
     } else {
+      float xl[8], gl[8], xh[8], gh[8], hl[3] = {0.f, 0.f, 0.f}, hh[3];
       load_run<T, VEC>(xr + tl, tl, L, xl);
       load_run<T, VEC>(gr + tl, tl, L, gl);
       load_run<T, VEC>(xr + th, th, L, xh);
@@ -263,15 +306,15 @@ __global__ __launch_bounds__(256) void conv_cf_bwd_k(const T* __restrict__ x, in
       }
 #pragma unroll
       for (int j = 0; j < 3; ++j) hh[j] = __shfl(xl[5 + j], 63, 64);
-      if (pi * 1024 + 512 < L) chunk(xh, gh, hh, th);
-      chunk(xl, gl, hl, tl);
+      if (pi * 1024 + 512 < L) cf_bwd_chunk<T, W, VEC>(xh, gh, hh, th, wk, bs, nextd, accw, accb, dxr, L, silu, lane);
+      cf_bwd_chunk<T, W, VEC>(xl, gl, hl, tl, wk, bs, nextd, accw, accb, dxr, L, silu, lane);
     }
   }
 #pragma unroll
   for (int k = 0; k < W; ++k) accw[k] = wave_sum(accw[k]);
   accb = wave_sum(accb);
   if (lane == 0) {
-    float* pr = part + row * (W + 1);
+    float* pr = part + ((int64_t)b * Dn + d) * (W + 1);
 #pragma unroll
     for (int k = 0; k < W; ++k) pr[k] = pacc ? pr[k] + accw[k] : accw[k];
     pr[W] = pacc ? pr[W] + accb : accb;
@@ -862,17 +905,31 @@ __global__ void conv_update_k(const T* __restrict__ x, int64_t sxb, T* __restric
     else return hipErrorInvalidValue;                             \
   } while (0)
 
+// row order of the channel-first kernels: 1 = memory order of the input (default), 0 = b-major;
+// MAMBA_AMD_CONV_CF_ORDER sets the process default, set_conv_cf_order overrides it
+static int g_cf_order = -1;
+int conv_cf_order() {
+  if (g_cf_order < 0) {
+    const char* e = getenv("MAMBA_AMD_CONV_CF_ORDER");
+    g_cf_order = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  return g_cf_order;
+}
+void set_conv_cf_order(int v) { g_cf_order = v == 0 ? 0 : 1; }
+static bool cf_batch_inner(int64_t sxb, int64_t sxd) { return conv_cf_order() != 0 && sxb < sxd; }
+
 template <typename T>
 static hipError_t cf_fwd(const T* x, int64_t sxb, int64_t sxd, const float* w, const float* bias, T* out,
                          int64_t sob, int64_t sod, int Bn, int Dn, int L, int Wd, bool silu, hipStream_t st) {
   const bool vec = (L % 8 == 0) && (sxb % 8 == 0) && (sxd % 8 == 0) && (sob % 8 == 0) && (sod % 8 == 0) &&
                    ((uintptr_t)x % 16 == 0) && ((uintptr_t)out % 16 == 0);
   dim3 grid((unsigned)(((int64_t)Bn * Dn + 3) / 4)), block(256);
+  const bool binner = cf_batch_inner(sxb, sxd);
   W_SWITCH(Wd, {
     if (vec) hipLaunchKernelGGL((conv_cf_fwd_k<T, WW, true>), grid, block, 0, st, x, sxb, sxd, w, bias, out, sob,
-                                sod, Bn, Dn, L, silu);
+                                sod, Bn, Dn, L, silu, binner);
     else hipLaunchKernelGGL((conv_cf_fwd_k<T, WW, false>), grid, block, 0, st, x, sxb, sxd, w, bias, out, sob, sod,
-                            Bn, Dn, L, silu);
+                            Bn, Dn, L, silu, binner);
   });
   return hipGetLastError();
 }
@@ -895,11 +952,12 @@ static hipError_t cf_bwd(const T* x, int64_t sxb, int64_t sxd, const float* w, c
                    (sdb % 8 == 0) && (sdd % 8 == 0) && ((uintptr_t)x % 16 == 0) && ((uintptr_t)g % 16 == 0) &&
                    ((uintptr_t)dx % 16 == 0);
   dim3 grid((unsigned)(((int64_t)Bn * Dn + 3) / 4)), block(256);
+  const bool binner = cf_batch_inner(sxb, sxd);
   W_SWITCH(Wd, {
     if (vec) hipLaunchKernelGGL((conv_cf_bwd_k<T, WW, true>), grid, block, 0, st, x, sxb, sxd, w, bias, g, sgb, sgd,
-                                dx, sdb, sdd, part, pacc, Bn, Dn, L, silu);
+                                dx, sdb, sdd, part, pacc, Bn, Dn, L, silu, binner);
     else hipLaunchKernelGGL((conv_cf_bwd_k<T, WW, false>), grid, block, 0, st, x, sxb, sxd, w, bias, g, sgb, sgd, dx,
-                            sdb, sdd, part, pacc, Bn, Dn, L, silu);
+                            sdb, sdd, part, pacc, Bn, Dn, L, silu, binner);
   });
   MAMBA_HIP_CHECK(hipGetLastError());
   return dw ? launch_colsum(part, Bn, Dn * (Wd + 1), dw, st) : hipSuccess;  // dw buffer holds (D, W+1): [w taps | bias]

@@ -139,6 +139,8 @@ void set_gemm_wg_nb(int nb);
 // paired 64-deep KC operand images in the staged-ring engine: 0 never, 1 KC operands of >= 1536 rows over K >= 16384
 // (default), 2 always
 int gemm_wg_kcpair();
+int conv_cf_order();
+void set_conv_cf_order(int v);
 void set_gemm_wg_kcpair(int v);
 // out[i] (+)= sum_s part[s * stride + i], fixed order
 hipError_t launch_transpose_bf16(const void* x, int64_t ldx, void* y, int64_t ldy, int R, int C, hipStream_t st);

@@ -38,6 +38,8 @@ struct SelScanArgs {
   // computed per 16-step tile with MFMA inside the scan (delta_ unused, never materialised).  dtw (D, R) bf16
   // contiguous, dtx (R, B L) bf16 rows (row stride sdtx, unit column stride); R % 8 == 0, R <= 128.
   const void* dtw_; const void* dtx_; int64_t sdtx; int R;
+  // workgroup order of the wave-per-state-group kernels: b fastest (set by the launchers for (d, b, l) memory)
+  bool binner;
 };
 
 struct SSMUpdateArgs {
@@ -62,5 +64,7 @@ int selscan_bwd_kc(const SelScanArgs& a);
 bool selscan_dt_fusable(const SelScanArgs& a);  // fused dt_proj (dtw_ / dtx_) supported for this shape
 bool selscan_bwd_sequential(const SelScanArgs& a);  // the wave-per-state-group kernel runs (supports pacc)
 hipError_t launch_ssm_update(const SSMUpdateArgs& a, hipStream_t st);
+int selscan_order();
+void set_selscan_order(int v);
 
 }  // namespace mamba_amd

@@ -296,7 +296,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
   bf16_t* const xS = reinterpret_cast<bf16_t*>(&yS[0][0][0]);  // DTF: x_dbl tile [32 ceil(R / 32)][16]
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int wgs_per_b = a.D / 64;
-  const int b = blockIdx.x / wgs_per_b, d0 = (blockIdx.x % wgs_per_b) * 64;
+  const int b = a.binner ? blockIdx.x % a.B : blockIdx.x / wgs_per_b;
+  const int d0 = (a.binner ? blockIdx.x / a.B : blockIdx.x % wgs_per_b) * 64;
   const int g = d0 / (a.D / a.G);
   const int d = d0 + lane;  // step loop: this lane's channel
   // staging / epilogue role: channel sr = tid >> 2, 4 steps at 4 * (tid & 3)
@@ -1217,7 +1218,8 @@ __global__ __launch_bounds__(256) void selscan_bwd_sg_k(SelScanArgs a) {
   __shared__ __attribute__((aligned(16))) float BCs[4][T][8];  // per wave and step: B of its 4 states, C
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int wgs_per_b = a.D / 64;
-  const int b = blockIdx.x / wgs_per_b, dg = blockIdx.x % wgs_per_b, d0 = dg * 64;
+  const int b = a.binner ? blockIdx.x % a.B : blockIdx.x / wgs_per_b;
+  const int dg = a.binner ? blockIdx.x / a.B : blockIdx.x % wgs_per_b, d0 = dg * 64;
   const int g = d0 / (a.D / a.G);
   const int d = d0 + lane;
   // staging / finishing role: channel sr, steps 2 sp, 2 sp + 1 of each half tile.  Rows are addressed
@@ -1544,7 +1546,28 @@ bool selscan_dt_fusable(const SelScanArgs& a) {
 }
 bool selscan_bwd_sequential(const SelScanArgs& a) { return use_bwd_sg(a); }
 
-hipError_t launch_selscan_fwd(const SelScanArgs& a, hipStream_t st) {
+// workgroup order of the wave-per-state-group walks: 0 = b-major (default), 1 = b fastest when the channels' rows are
+// (d, b, l) memory (the Mamba-1 layout), so concurrently running workgroups read neighbouring rows.  Unlike the
+// bandwidth-bound channel-first conv (15-20% faster in memory order) the VALU-bound walks lose 0.5% of the Mamba-1
+// 280M step with it (profiles/r6/row_order.txt).  MAMBA_AMD_SELSCAN_ORDER sets the process default,
+// set_selscan_order overrides it.
+static int g_ss_order = -1;
+int selscan_order() {
+  if (g_ss_order < 0) {
+    const char* e = getenv("MAMBA_AMD_SELSCAN_ORDER");
+    g_ss_order = (e && atoi(e) == 1) ? 1 : 0;
+  }
+  return g_ss_order;
+}
+void set_selscan_order(int v) { g_ss_order = v == 1 ? 1 : 0; }
+static SelScanArgs with_order(const SelScanArgs& a) {
+  SelScanArgs c = a;
+  c.binner = selscan_order() != 0 && a.sub < a.sud;
+  return c;
+}
+
+hipError_t launch_selscan_fwd(const SelScanArgs& a_in, hipStream_t st) {
+  const SelScanArgs a = with_order(a_in);
   const int64_t rows = (int64_t)a.B * a.D;
   dim3 grid((unsigned)((rows + 3) / 4)), block(256);
   if (a.carries && a.nct != (a.L + a.carry_t - 1) / a.carry_t) return hipErrorInvalidValue;
@@ -1570,7 +1593,8 @@ hipError_t launch_selscan_fwd(const SelScanArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_selscan_bwd(const SelScanArgs& a, hipStream_t st) {
+hipError_t launch_selscan_bwd(const SelScanArgs& a_in, hipStream_t st) {
+  const SelScanArgs a = with_order(a_in);
   if (a.Kc != selscan_bwd_kc(a) || (a.carry_t != SGB_T && a.carry_t != SB_T) ||
       a.nct != (a.L + a.carry_t - 1) / a.carry_t)
     return hipErrorInvalidValue;

@@ -1,7 +1,7 @@
 """Channel-first causal conv (Mamba-1 conv1d, kernels/conv1d.hip conv_cf_*) at the Mamba-1 280M / 370M layer shapes:
 forward and backward microseconds (HIP events) and effective HBM bandwidth, plus a check against the fp32 reference.
 
-  python scripts/conv_cf_bench.py [--reps 20]
+  python scripts/conv_cf_bench.py [--reps 20] [--orders 0,1]   (conv_cf_order knob values, interleaved)
 """
 import argparse
 import json
@@ -30,6 +30,7 @@ def timeit(fn, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--orders", default="")
     a = ap.parse_args()
     assert _ext.load(), _ext.error()
     ops = _ext.ops()
@@ -45,12 +46,16 @@ def main():
         y = ops.conv1d_cf_fwd(x, w, bias, True)
         ref = causal_conv1d_ref(x.float(), w, bias, "silu")
         rel = ((y.float() - ref).norm() / ref.norm()).item()
-        t_f = timeit(lambda: ops.conv1d_cf_fwd(x, w, bias, True), a.reps)
-        t_b = timeit(lambda: ops.conv1d_cf_bwd(x, w, bias, go, True, dx), a.reps)
-        nb = x.numel() * 2
-        print(json.dumps({"shape": name, "fwd_us": round(t_f, 1), "fwd_TBs": round(2 * nb / t_f / 1e6, 2),
-                          "bwd_us": round(t_b, 1), "bwd_TBs": round(3 * nb / t_b / 1e6, 2), "fwd_rel": round(rel, 5)}),
-              flush=True)
+        knobs = [int(v) for v in a.orders.split(",")] if a.orders else [ops.conv_cf_order(-1)]
+        for rep in range(2 if a.orders else 1):
+            for kv in knobs:
+                ops.conv_cf_order(kv)
+                t_f = timeit(lambda: ops.conv1d_cf_fwd(x, w, bias, True), a.reps)
+                t_b = timeit(lambda: ops.conv1d_cf_bwd(x, w, bias, go, True, dx), a.reps)
+                nb = x.numel() * 2
+                print(json.dumps({"shape": name, "order": kv, "fwd_us": round(t_f, 1),
+                                  "fwd_TBs": round(2 * nb / t_f / 1e6, 2), "bwd_us": round(t_b, 1),
+                                  "bwd_TBs": round(3 * nb / t_b / 1e6, 2), "fwd_rel": round(rel, 5)}), flush=True)
 
 
 if __name__ == "__main__":

@@ -152,6 +152,37 @@ def test_conv1d_channel_first_whole_chunks(cuda, L, act):
         assert rel(a, b_) < 2e-2
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("b,d,L", [(3, 520, 1024), (2, 136, 1536), (2, 64, 2048), (5, 7, 48)])
+def test_conv1d_cf_row_order(cuda, dtype, b, d, L):
+    """Channel-first rows numbered in memory order ((d, b, l) buffers: b fastest, the default) against b-major
+    numbering, bitwise (same per-row math), including the accumulated per-row tap / bias partials."""
+    from mamba_distributed_amd.ops import _ext
+    ops = _ext.ops()
+    torch.manual_seed(9)
+    W = 4
+    x = torch.randn(d, b, L, device=cuda).to(dtype).permute(1, 0, 2)
+    go = torch.randn(d, b, L, device=cuda).to(dtype).permute(1, 0, 2)
+    w = torch.randn(d, W, device=cuda) * 0.5
+    bias = torch.randn(d, device=cuda) * 0.1
+    part_init = torch.randn(b, d, W + 1, device=cuda)
+    prev = ops.conv_cf_order(-1)
+    outs = []
+    try:
+        for order in (0, 1):
+            ops.conv_cf_order(order)
+            y = ops.conv1d_cf_fwd(x, w, bias, True)
+            dx, dw, db = ops.conv1d_cf_bwd(x, w, bias, go, True, None)
+            p = part_init.clone()
+            ops.conv1d_cf_bwd(x, w, bias, go, True, None, p, 2)  # accumulate into the per-row partials
+            outs.append((y, dx, dw, db, p))
+        torch.cuda.synchronize()
+    finally:
+        ops.conv_cf_order(prev)
+    for u, v in zip(*outs):
+        assert torch.equal(u, v)
+
+
 def test_cross_entropy(cuda):
     from mamba_distributed_amd.ops.cross_entropy import cross_entropy, fused_linear_cross_entropy
     torch.manual_seed(3)
@@ -1324,6 +1355,52 @@ def test_late_colsum(cuda, preset):
     again = run()
     for a_, b_ in zip(got, again):
         assert torch.equal(a_, b_)
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_selective_scan_walk_order(cuda, fused):
+    """The sequential walks with workgroups numbered b-fastest (MAMBA_AMD_SELSCAN_ORDER=1, for (d, b, l) memory) against
+    the default b-major numbering: bitwise-equal outputs, carries, last state and every gradient (each workgroup's math is unchanged)."""
+    torch.manual_seed(13)
+    b, d, L, Rk, n = 40, 1536, 128, 48, 16
+    ops = torch.ops.mamba_amd
+    M = b * L
+    cm = lambda t2: t2.view(t2.shape[0], b, L).permute(1, 0, 2)  # noqa: E731
+    u, z = cm(torch.randn(d, M, device=cuda).to(torch.bfloat16)), cm(torch.randn(d, M, device=cuda).to(torch.bfloat16))
+    x_dbl = torch.randn(Rk + 2 * n, M, device=cuda).to(torch.bfloat16)
+    W = (torch.randn(d, Rk, device=cuda) * Rk ** -0.5).to(torch.bfloat16)
+    A = -torch.rand(d, n, device=cuda) * 4 - 0.1
+    D = torch.randn(d, device=cuda)
+    db = torch.randn(d, device=cuda) * 0.3 - 1.0
+    delta = cm((W.float() @ x_dbl[:Rk].float()).to(torch.bfloat16))
+    Bm, Cm = cm(x_dbl[Rk:Rk + n]).unsqueeze(1), cm(x_dbl[Rk + n:]).unsqueeze(1)
+    go2 = torch.randn(d, M, device=cuda).to(torch.bfloat16)
+
+    def run():
+        if fused:
+            y, car, last = ops.selscan_fwd_dt(u, W, x_dbl[:Rk], A, Bm, Cm, D, z, db, True)
+        else:
+            y, car, last = ops.selscan_fwd(u, delta, A, Bm, Cm, D, z, db, True)
+        dz2 = torch.empty(d, M, device=cuda, dtype=torch.bfloat16)
+        dx = torch.empty(2 * n, M, device=cuda, dtype=torch.bfloat16)
+        outs = (cm(dz2), cm(dx[:n]).unsqueeze(1), cm(dx[n:]).unsqueeze(1))
+        if fused:
+            g = ops.selscan_bwd_dt_into(cm(go2), u, W, x_dbl[:Rk], A, Bm, Cm, D, z, db, car, True, *outs)
+        else:
+            g = ops.selscan_bwd_into(cm(go2), u, delta, A, Bm, Cm, D, z, db, car, True, *outs)
+        return [y, car, last, dz2, dx] + [t for t in g if t is not None]
+
+    prev = ops.selscan_order(-1)
+    try:
+        ops.selscan_order(0)
+        ref = run()
+        ops.selscan_order(1)
+        got = run()
+        torch.cuda.synchronize()
+    finally:
+        ops.selscan_order(prev)
+    for i, (a_, b_) in enumerate(zip(got, ref)):
+        assert torch.equal(a_, b_), i
 
 
 @pytest.mark.parametrize("b,d,L,Rk,with_z", [(32, 1536, 256, 48, True), (32, 1024, 128, 64, False),
