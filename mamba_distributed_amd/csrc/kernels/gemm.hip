@@ -560,7 +560,10 @@ hipError_t launch_gemm_skinny(const void* A, int64_t lda, const void* B, int64_t
       hipLaunchKernelGGL((gemm_skinny_k<TMV, BKV, false>), grid, block, 0, st, (const bf16_t*)A, lda,            \
                          (const bf16_t*)B, ldb, (bf16_t*)C, ldc, N, K, M);                                    \
   }
-  if (wide) SK_LAUNCH(256, 32) else SK_LAUNCH(128, 128)
+  // write-only wide products (delta = W_dt x_dbl[:R]) take 128-token tiles: half the LDS per workgroup, twice the
+  // workgroups (and stores) in flight, 45.4 -> 40.4 us at the 280M shape; the read-add-write ones (dconv += W_x^T
+  // dx_dbl) stay at 256 (81.8 vs 89.3 us at 128; scripts/skinny_bench.py, profiles/r6/skinny_tiles.txt)
+  if (wide && !accumulate) SK_LAUNCH(128, 32) else if (wide) SK_LAUNCH(256, 32) else SK_LAUNCH(128, 128)
 #undef SK_LAUNCH
   return hipGetLastError();
 }

@@ -1132,7 +1132,7 @@ def test_activation_checkpointing_bitwise_on_gpu(cuda, layer):
 
 
 @pytest.mark.parametrize("N,K,M", [(80, 1536, 32768), (1536, 48, 32768), (48, 1536, 4096), (1536, 80, 4096),
-                                   (72, 40, 1000), (130, 24, 264)])
+                                   (72, 40, 1000), (130, 24, 264), (300, 24, 1000)])
 @pytest.mark.parametrize("acc", [False, True])
 def test_gemm_skinny(cuda, N, K, M, acc):
     """gemm_skinny_k (channel-major Mamba-1 x_proj / dt_proj family) vs an fp32 matmul, including
