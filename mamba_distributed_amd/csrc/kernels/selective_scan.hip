@@ -1501,6 +1501,36 @@ __global__ void selscan_reduce_bc_k(SelScanArgs a) {
   st(((T*)a.dC_) + (int64_t)b * a.sdCb + (int64_t)g * a.sdCg + (int64_t)n * a.sdCn + t, sc);
 }
 
+// the same sum, 4 consecutive steps per thread (16-B partial loads, 8-B bf16 stores) with the channel groups' loads
+// unrolled 4 deep: the scalar form above kept one 4-B load pair per group in flight (48 -> see
+// profiles/r6/reduce_bc_vec.txt).  Needs L % 4 == 0 and 8-B aligned dB / dC rows (host-checked).
+__global__ void selscan_reduce_bc4_k(SelScanArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // over B*G*N*L/4
+  const int N = a.N, L4 = a.L >> 2;
+  const int64_t total = (int64_t)a.B * a.G * N * L4;
+  if (i >= total) return;
+  const int t = (int)(i % L4) * 4;
+  const int n = (int)((i / L4) % N);
+  const int g = (int)((i / ((int64_t)L4 * N)) % a.G);
+  const int b = (int)(i / ((int64_t)L4 * N * a.G));
+  const int ndg = (a.D + a.Kc - 1) / a.Kc;
+  const int dpg = a.D / a.G;
+  const int dg0 = (g * dpg) / a.Kc, dg1 = ((g + 1) * dpg + a.Kc - 1) / a.Kc;
+  float4 sb = make_float4(0.f, 0.f, 0.f, 0.f), sc = sb;
+#pragma unroll 4
+  for (int dg = dg0; dg < dg1; ++dg) {
+    const int64_t o = (((int64_t)b * ndg + dg) * N + n) * a.L + t;
+    const float4 pb = *reinterpret_cast<const float4*>(a.part_dB + o);
+    const float4 pc = *reinterpret_cast<const float4*>(a.part_dC + o);
+    sb.x += pb.x; sb.y += pb.y; sb.z += pb.z; sb.w += pb.w;
+    sc.x += pc.x; sc.y += pc.y; sc.z += pc.z; sc.w += pc.w;
+  }
+  bf16_t* db = ((bf16_t*)a.dB_) + (int64_t)b * a.sdBb + (int64_t)g * a.sdBg + (int64_t)n * a.sdBn + t;
+  bf16_t* dc = ((bf16_t*)a.dC_) + (int64_t)b * a.sdCb + (int64_t)g * a.sdCg + (int64_t)n * a.sdCn + t;
+  *reinterpret_cast<uint2*>(db) = make_uint2(pack2(sb.x, sb.y), pack2(sb.z, sb.w));
+  *reinterpret_cast<uint2*>(dc) = make_uint2(pack2(sc.x, sc.y), pack2(sc.z, sc.w));
+}
+
 #define SS_DISPATCH(...)                                                            \
   do {                                                                              \
     if (a.dtype == kBF16 && a.N == 16) { using TT = bf16_t; constexpr int NN = 16; __VA_ARGS__; } \
@@ -1624,7 +1654,12 @@ hipError_t launch_selscan_bwd(const SelScanArgs& a_in, hipStream_t st) {
   }
   MAMBA_HIP_CHECK(hipGetLastError());
   const int64_t total = (int64_t)a.B * a.G * a.N * a.L;
-  if (a.dtype == kBF16)
+  const bool v4 = a.dtype == kBF16 && a.L % 4 == 0 && a.sdBb % 4 == 0 && a.sdBg % 4 == 0 && a.sdBn % 4 == 0 &&
+                  a.sdCb % 4 == 0 && a.sdCg % 4 == 0 && a.sdCn % 4 == 0 && (uintptr_t)a.dB_ % 8 == 0 &&
+                  (uintptr_t)a.dC_ % 8 == 0;
+  if (v4)
+    hipLaunchKernelGGL(selscan_reduce_bc4_k, dim3((unsigned)((total / 4 + 255) / 256)), dim3(256), 0, st, a);
+  else if (a.dtype == kBF16)
     hipLaunchKernelGGL(selscan_reduce_bc_k<bf16_t>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, a);
   else
     hipLaunchKernelGGL(selscan_reduce_bc_k<float>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, a);
