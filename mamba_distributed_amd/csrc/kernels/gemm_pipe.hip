@@ -1236,10 +1236,12 @@ hipError_t launch_gemm_pipe(int la, int lb, const void* A, int64_t lda, const vo
     // in_proj weight gradient (3072 KC rows) and +0.2-0.8% whole-step with the out_proj one (1536 rows) added;
     // slower for short-K products with a small L2-resident KC operand (the out_proj forward's 768-row weight
     // +14-22%) and the 48 / 80-row x_proj / dt_proj products (+25-60%): the pair halves the prefetch distance of
-    // every even stage.  MAMBA_AMD_WG_KCPAIR: 0 off, 1 this rule, 2 every KC operand.
+    // every even stage.  256-row tiles only: the x_proj / dt_proj weight gradients on 128-row tiles pair their wide
+    // (1536-row) KC operand under the size test but ran 60.8 vs 56.4 us paired (profiles/r6/prof_mamba1-280m_serial_*).
+    // MAMBA_AMD_WG_KCPAIR: 0 off, 1 this rule, 2 every KC operand.
     const int kpm = gemm_wg_kcpair();
     const bool kp = kpm == 2 ? (la == 0 || lb == 0)
-                             : kpm == 1 && K >= 16384 && ((la == 0 && M >= 1536) || (lb == 0 && N >= 1536));
+                             : kpm == 1 && mi == 8 && K >= 16384 && ((la == 0 && M >= 1536) || (lb == 0 && N >= 1536));
 #define WG_L(LA_, LB_, E_, MI_)                                                                          \
   if constexpr (LA_ == 0 || LB_ == 0) {                                                                  \
     if (kp) hipLaunchKernelGGL((gemm_wg_kp_k<LA_, LB_, E_, MI_>), dim3(nwg), dim3(512), 0, st, a);       \
