@@ -153,10 +153,11 @@ def test_conv1d_channel_first_whole_chunks(cuda, L, act):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("b,d,L", [(3, 520, 1024), (2, 136, 1536), (2, 64, 2048), (5, 7, 48)])
+@pytest.mark.parametrize("b,d,L", [(3, 520, 1024), (2, 136, 1536), (2, 64, 2048), (5, 7, 48), (3, 40, 77)])
 def test_conv1d_cf_row_order(cuda, dtype, b, d, L):
     """Channel-first rows numbered in memory order ((d, b, l) buffers: b fastest, the default) against b-major
-    numbering, bitwise (same per-row math), including the accumulated per-row tap / bias partials."""
+    numbering, bitwise (same per-row math), including the accumulated per-row tap / bias partials; L = 77 takes the
+    scalar (non-16-B) kernels."""
     from mamba_distributed_amd.ops import _ext
     ops = _ext.ops()
     torch.manual_seed(9)
