@@ -1121,25 +1121,48 @@ __global__ __launch_bounds__(128 * WN) void gemm_pk_k(GemmPkArgs a) {
   }
 }
 
-// out[i] (+)= sum_s part[s][i] in fixed order (the K-split slabs of a weight gradient).  V = 4: a float4 per thread;
-// V = 1 for small outputs with many slabs (the 42-slab narrow weight gradients: 120 workgroups of float4 threads
-// would each walk 42 dependent slab reads)
-template <int V>
+// out[i] (+)= sum_s part[s][i] in fixed order (the K-split slabs of a weight gradient), a float4 per thread
 __global__ void gp_reduce_k(const float* __restrict__ part, int S, int64_t stride, int64_t n, float* __restrict__ out,
                             bool accumulate) {
-  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * V;
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (i >= n) return;
-  if constexpr (V == 4) {
-    float4 s = accumulate ? *reinterpret_cast<const float4*>(out + i) : make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int k = 0; k < S; ++k) {
+  float4 s = accumulate ? *reinterpret_cast<const float4*>(out + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int k = 0; k < S; ++k) {
+    const float4 v = *reinterpret_cast<const float4*>(part + (int64_t)k * stride + i);
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  *reinterpret_cast<float4*>(out + i) = s;
+}
+
+// Many slabs over a small output (the 42 / 16-slab narrow weight gradients): wave w of the workgroup sums the slab
+// quarter [w S / 4, (w + 1) S / 4) for 256 consecutive outputs (a float4 per lane), and the four quarter sums are
+// added in quarter order through LDS (fixed order: deterministic).  The one-element-per-thread form it replaced
+// issued S 4-B loads per lane; this one S / 4 16-B loads (profiles/r6/gp_reduce_quarters.txt).
+__global__ __launch_bounds__(256) void gp_reduce_q_k(const float* __restrict__ part, int S, int64_t stride, int64_t n,
+                                                     float* __restrict__ out, bool accumulate) {
+  __shared__ float4 q[3][64];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t i = ((int64_t)blockIdx.x * 64 + lane) * 4;
+  const bool ok = i < n;
+  const int k0 = w * S / 4, k1 = (w + 1) * S / 4;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (ok) {
+    for (int k = k0; k < k1; ++k) {
       const float4 v = *reinterpret_cast<const float4*>(part + (int64_t)k * stride + i);
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
-    *reinterpret_cast<float4*>(out + i) = s;
-  } else {
-    float s = accumulate ? out[i] : 0.f;
-    for (int k = 0; k < S; ++k) s += part[(int64_t)k * stride + i];
-    out[i] = s;
+  }
+  if (w > 0) q[w - 1][lane] = s;
+  __syncthreads();
+  if (w == 0 && ok) {
+    float4 o = accumulate ? *reinterpret_cast<const float4*>(out + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+    o.x += s.x; o.y += s.y; o.z += s.z; o.w += s.w;
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const float4 v = q[u][lane];
+      o.x += v.x; o.y += v.y; o.z += v.z; o.w += v.w;
+    }
+    *reinterpret_cast<float4*>(out + i) = o;
   }
 }
 
@@ -1396,11 +1419,11 @@ hipError_t launch_gemm_pk(int la, int lb, const void* A, int64_t lda, const void
 hipError_t launch_gp_reduce(const float* part, int S, int64_t stride, int64_t n, float* out, bool accumulate,
                             hipStream_t st) {
   if (n % 4 || stride % 4) return hipErrorInvalidValue;
-  if (n / 4 < 512 * 256 && S >= 16)  // fewer than 2 float4 workgroups per CU: one element per thread
-    hipLaunchKernelGGL(gp_reduce_k<1>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part, S, stride, n, out,
+  if (n / 4 < 512 * 256 && S >= 16)  // fewer than 2 float4 workgroups per CU: the slab quarters per wave
+    hipLaunchKernelGGL(gp_reduce_q_k, dim3((unsigned)((n / 4 + 63) / 64)), dim3(256), 0, st, part, S, stride, n, out,
                        accumulate);
   else
-    hipLaunchKernelGGL(gp_reduce_k<4>, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, st, part, S, stride, n,
+    hipLaunchKernelGGL(gp_reduce_k, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, st, part, S, stride, n,
                        out, accumulate);
   return hipGetLastError();
 }
