@@ -335,8 +335,8 @@ def test_gp_wg_kc_pairs_default_rule(cuda):
 
 @pytest.mark.parametrize("S,n", [(42, 80 * 1536), (16, 48 * 1536), (7, 3072 * 768)])
 def test_gp_reduce_forms(cuda, S, n):
-    """gp_reduce over S fp32 slabs in fixed order: the one-element-per-thread form (many slabs, small output: the
-    narrow weight gradients) and the float4 form give the fp64 sum, bitwise repeatably."""
+    """gp_reduce over S fp32 slabs in fixed order: the slab-quarter form (many slabs, small output: the narrow weight
+    gradients) and the float4 form give the fp64 sum, bitwise repeatably."""
     ops = _ops()
     g = torch.Generator(device=cuda).manual_seed(S)
     part = torch.randn(S, n, device=cuda, generator=g)
